@@ -1,0 +1,76 @@
+"""ctypes binding of oracle/liboracle.so (the CPU restatement checker)."""
+import ctypes
+import pathlib
+import subprocess
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+LIB = ROOT / "oracle" / "liboracle.so"
+
+
+class Info(ctypes.Structure):
+    _fields_ = [("frame_bytes", ctypes.c_int), ("channels", ctypes.c_int), ("hz", ctypes.c_int),
+                ("layer", ctypes.c_int), ("bitrate_kbps", ctypes.c_int)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            subprocess.check_call(["make", "-s", "-C", str(ROOT / "oracle")])
+        L = ctypes.CDLL(str(LIB))
+        L.orc_create.restype = ctypes.c_void_p
+        L.orc_destroy.argtypes = [ctypes.c_void_p]
+        L.orc_decode_frame.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p,
+                                       ctypes.POINTER(Info)]
+        L.orc_get_taps.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 4
+        L.orc_decode_stream.argtypes = [ctypes.c_char_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_long,
+                                        ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+        L.orc_decode_stream.restype = ctypes.c_long
+        L.orc_synth_only.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_skip_id3v2.argtypes = [ctypes.c_char_p, ctypes.c_long]
+        L.orc_skip_id3v2.restype = ctypes.c_long
+        _lib = L
+    return _lib
+
+
+def decode_stream(data: bytes, max_frames=100000):
+    """Planar float32 [nch, frames*1152] (ID3v2 and Xing/Info frame skipped)."""
+    L = lib()
+    out = np.zeros((2, max_frames * 1152), np.float32)
+    nch, hz = ctypes.c_int(), ctypes.c_int()
+    nf = L.orc_decode_stream(data, len(data), out.ctypes.data, max_frames, ctypes.byref(nch), ctypes.byref(hz))
+    return out[: nch.value, : nf * 1152], hz.value
+
+
+class Decoder:
+    """Per-frame oracle decoder with parity taps."""
+
+    def __init__(self):
+        self.L = lib()
+        self.d = self.L.orc_create()
+
+    def __del__(self):
+        try:
+            self.L.orc_destroy(self.d)
+        except Exception:
+            pass
+
+    def decode_frame(self, frame: bytes):
+        pcm = np.zeros((2, 1152), np.float32)
+        info = Info()
+        r = self.L.orc_decode_frame(self.d, frame, len(frame), pcm.ctypes.data, ctypes.byref(info))
+        return r, pcm[: info.channels], info
+
+    def taps(self):
+        is_ = np.zeros((2, 2, 576), np.int16)
+        sf = np.zeros((2, 2, 40), np.uint8)
+        xr = np.zeros((2, 2, 576), np.float32)
+        side = np.zeros((2, 2, 20), np.int32)
+        self.L.orc_get_taps(self.d, is_.ctypes.data, sf.ctypes.data, xr.ctypes.data, side.ctypes.data)
+        return is_, sf, xr, side

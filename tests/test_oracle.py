@@ -1,0 +1,65 @@
+"""The CPU oracle (oracle/mp3_oracle.c) pinned against the FFmpeg golden
+vectors (tests/golden/, produced by tests/golden/make_golden.py) and the
+generator's by-construction integer truth."""
+import numpy as np
+import pytest
+
+import _gen
+import _golden
+import _oracle
+
+
+@pytest.mark.parametrize("name", _golden.names())
+def test_oracle_matches_ffmpeg_golden(name):
+    data, ref = _golden.case(name)
+    pcm, hz = _oracle.decode_stream(data)
+    ours = _golden.to_int16(pcm)
+    assert ours.shape == ref.shape
+    d = np.abs(ours.astype(np.int32) - ref.astype(np.int32))
+    assert d.max() <= 1, (name, int(d.max()))  # ±1 LSB (north_star tolerance)
+    assert (d == 0).mean() > 0.6  # FFmpeg is fixed-point: ~75% exact
+
+
+def test_keypress_bitstream_facts():
+    """21 audio frames, 128 kbps joint stereo M/S,
+    part2_3_length == 0 in frames 12-21, main_data_begin in 0..511."""
+    data, _ = _golden.case("keypress_128k_js")
+    pos = 253
+    dec = _oracle.Decoder()
+    mdbs, nonempty = [], 0
+    for f in range(21):
+        fb = 144000 * 128 // 44100 + ((data[pos + 2] >> 1) & 1)
+        r, pcm, info = dec.decode_frame(data[pos:pos + fb])
+        assert r == 1152 and info.bitrate_kbps == 128 and info.channels == 2
+        assert (data[pos + 3] >> 6) == 1 and ((data[pos + 3] >> 4) & 3) == 2
+        is_, sf, xr, side = dec.taps()
+        mdbs.append(int(side[0, 0, 15]))
+        p23 = side[:, :, 0]
+        if f >= 11:
+            assert (p23 == 0).all()
+        nonempty += int((p23 > 0).sum())
+        # bit accounting: every unit consumes exactly part2_3_length bits
+        assert np.array_equal(side[:, :, 16], p23), (f, side[:, :, 16], p23)
+        pos += fb
+    assert pos == len(data)
+    assert max(mdbs) == 511 and min(mdbs) == 0
+    assert nonempty == 37  # measured (SURVEY App. C quotes 44 = all units of frames 1-11)
+
+
+@pytest.mark.parametrize("cfg,seed", [(_gen.C3, 11), (_gen.C3, 12), (_gen.C5, 13), (_gen.C5, 14), (_gen.C5, 15)])
+def test_integer_stage_roundtrip(cfg, seed):
+    """Generator-encoded is[] / scalefactors decode back exactly (bit-exact)."""
+    nf = 12
+    data, offs, truth = _gen.stream(cfg, seed, nf, truth=True)
+    dec = _oracle.Decoder()
+    for f in range(nf):
+        end = offs[f + 1] if f + 1 < nf else len(data)
+        r, pcm, info = dec.decode_frame(data[offs[f]:end])
+        assert r == 1152
+        is_, sf, xr, side = dec.taps()
+        for gr in range(2):
+            for ch in range(info.channels):
+                assert np.array_equal(is_[gr, ch], truth[f, gr, ch]["is"]), (f, gr, ch)
+                assert np.array_equal(sf[gr, ch], truth[f, gr, ch]["sf"]), (f, gr, ch)
+                assert side[gr, ch, 0] == truth[f, gr, ch]["part2_3_length"]
+                assert side[gr, ch, 16] == side[gr, ch, 0]

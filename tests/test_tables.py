@@ -1,0 +1,83 @@
+"""ISO 11172-3 constant tables: structural checks + byte-presence in the
+FFmpeg copy of the same tables in the container's kaleido binary (SURVEY.md
+Appendix B.3; skipped where that binary is absent, e.g. on the GPU box)."""
+import os
+
+import numpy as np
+import pytest
+
+import _tables as T
+
+KBIN = "/usr/local/lib/python3.10/dist-packages/kaleido/executable/bin/kaleido"
+t = T.load()
+
+
+@pytest.mark.parametrize("num", T.HTAB_ISO)
+def test_huffman_complete_prefix_code(num):
+    codes, lens = T.htab(t, num)
+    assert sum(2.0 ** -int(l) for l in lens) == pytest.approx(1.0, abs=1e-12)
+    words = [format(int(c), "0%db" % int(l)) for c, l in zip(codes, lens)]
+    assert len(set(words)) == len(words)
+    for i, a in enumerate(words):
+        for j, b in enumerate(words):
+            assert i == j or not b.startswith(a)
+    assert int(lens.max()) <= 19
+
+
+def test_quad_tables():
+    for q in range(2):
+        assert sum(2.0 ** -int(l) for l in t["MP3D_QUAD_LEN"][q]) == pytest.approx(1.0)
+    assert list(t["MP3D_QUAD_CODE"][1]) == list(range(15, -1, -1))
+
+
+def test_band_tables():
+    for s in range(3):
+        assert int(t["MP3D_SFB_LONG_WIDTH"][s].sum()) == 576
+        assert int(t["MP3D_SFB_SHORT_WIDTH"][s].sum()) == 192
+        # first 8 long bands always cover 36 lines (mixed-block boundary)
+        assert int(t["MP3D_SFB_LONG_WIDTH"][s][:8].sum()) == 36
+        assert int(t["MP3D_SFB_SHORT_WIDTH"][s][:3].sum()) * 3 == 36
+
+
+def test_synthesis_window_shape():
+    w = t["MP3D_SYNTH_WINDOW_Q16"].astype(np.int64)
+    assert w.shape == (257,) and w[0] == 0 and w[256] == 75038
+    D = np.zeros(512)
+    D[:257] = w / 65536.0
+    for i in range(1, 256):
+        D[512 - i] = D[i] if i % 64 == 0 else -D[i]
+    # the window's DC gain is the filterbank's passband normalisation
+    assert abs(D[256]) == D.__abs__().max()
+
+
+def test_select_maps():
+    sel = t["MP3D_HTAB_OF_SELECT"]
+    assert sel[0] == -1 and sel[4] == -1 and sel[14] == -1
+    assert all(sel[16:24] == 13) and all(sel[24:32] == 14)
+    assert list(t["MP3D_LINBITS"][16:]) == [1, 2, 3, 4, 6, 8, 10, 13, 4, 5, 6, 7, 8, 9, 11, 13]
+
+
+@pytest.mark.skipif(not os.path.exists(KBIN), reason="kaleido binary only in the build container")
+def test_tables_present_in_ffmpeg_copy():
+    kb = open(KBIN, "rb").read()
+    region = (26_340_000, 26_360_000)  # FFmpeg mpegaudiodec tables
+
+    def in_region(b):
+        i = kb.find(b, region[0], region[1])
+        return i >= 0
+
+    for num in T.HTAB_ISO:
+        codes, lens = T.htab(t, num)
+        if num == 1:
+            continue  # 4-entry table: too short to be a unique pattern
+        assert in_region(codes.astype("<u2").tobytes()), num
+        assert in_region(lens.tobytes()), num
+    assert in_region(t["MP3D_QUAD_CODE"][0].tobytes()) and in_region(t["MP3D_QUAD_LEN"][0].tobytes())
+    assert in_region(t["MP3D_SYNTH_WINDOW_Q16"].astype("<i4").tobytes())
+    assert in_region(t["MP3D_PRETAB"].tobytes())
+    for s in range(3):
+        assert in_region(t["MP3D_SFB_LONG_WIDTH"][s].tobytes())
+        assert in_region(t["MP3D_SFB_SHORT_WIDTH"][s].tobytes())
+    assert in_region(t["MP3D_BITRATE_L3"].astype("<u2").tobytes())
+    assert kb.find(t["MP3D_SLEN"].tobytes()) >= 0
+    assert kb.find(t["MP3D_ALIAS_C"].astype("<f4").tobytes()) >= 0
