@@ -1,0 +1,239 @@
+#!/usr/bin/env python3
+"""Benchmark: stereo MP3 frames/s (128 kbps, 44.1 kHz) on MI355X.
+
+Workload (BASELINE.json configs[2]): 65,536 synthetic CBR
+128 kbps 44.1 kHz joint-stereo streams x 32 frames per step, per GPU.  A step
+is one mp3d_batch_decode call over every stream's next 32 frames (the full
+hot path: demux + reservoir + Huffman + requantise/stereo + IMDCT +
+polyphase synthesis -> int16 PCM), inputs resident in HBM, PCM written to
+HBM.  Per-stream decoder state stays resident across steps.
+
+Multi-GPU: one process per GPU (torchrun), streams sharded by global stream
+id (seed 3_000_003 + id), no collective on the data path -> weak scaling.
+Timing: barrier + synchronize on both sides of exactly K steps, max over
+ranks.  The dominant kernel's duration comes from HIP events recorded on
+the stream the kernels run on (mp3d_batch_kernel_times).
+
+The CPU baseline is the oracle restatement (oracle/liboracle.so, "port")
+on a bounded sample of the same workload, rank 0 only.
+"""
+import argparse
+import ctypes
+import json
+import os
+import pathlib
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+
+HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md)
+FP32_PEAK_TFLOPS = 157.3       # FP32 vector == FP32 MFMA (MI355X_MICROARCH.md)
+BYTES_IN_PER_FRAME = 417.96    # 128 kbps @ 44.1 kHz
+PCM_BYTES_PER_FRAME = 4608.0   # 1152 x 2 ch x int16
+# algorithmic FLOPs per stereo frame: dense 32x32 matrixing
+# + 512-tap window per slot (72 slot-channels) + IMDCT (4 units x 32 sb x 2*18*18)
+FLOP_PER_FRAME = 72 * (2 * 32 * 32 + 2 * 512) + 4 * 32 * 2 * 18 * 18
+# k_synth algorithmic bytes per frame: is[] int16 in (4 x 576 x 2) + PCM out
+SYNTH_BYTES_PER_FRAME = 4 * 576 * 2 + PCM_BYTES_PER_FRAME
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(n_frames_target=2048, threads=None, budget_s=15.0):
+    """Oracle (scalar C restatement) on a bounded sample of the C3 workload,
+    one stream per task, all host threads; returns the result dict."""
+    import _gen
+    import _oracle
+    threads = threads or min(16, os.cpu_count() or 1)
+    F = 32
+    n_streams = max(threads, n_frames_target // F)
+    buf, offs, sizes = _gen.batch(_gen.C3, 3_000_003, n_streams, F, threads=threads)
+    L = _oracle.lib()
+    streams = [bytes(buf[offs[s]:offs[s] + sizes[s]]) for s in range(n_streams)]
+    out = [np.zeros((2, F * 1152), np.float32) for _ in range(threads)]
+    # one warm call initialises the oracle's tables before threads start
+    _oracle.decode_stream(streams[0], F)
+    done = [0] * threads
+    t_end = [0.0]
+
+    def work(tid):
+        nch, hz = ctypes.c_int(), ctypes.c_int()
+        for s in range(tid, n_streams, threads):
+            d = streams[s]
+            done[tid] += L.orc_decode_stream(d, len(d), out[tid].ctypes.data, F, ctypes.byref(nch), ctypes.byref(hz))
+            if time.perf_counter() > t_end[0]:
+                break
+
+    t0 = time.perf_counter()
+    t_end[0] = t0 + budget_s
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    dt = time.perf_counter() - t0
+    frames = sum(done)
+    return {"value": frames / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": "%d C3 frames (%d streams x up to %d frames, 128 kbps 44.1 kHz joint stereo), "
+                      "oracle/liboracle.so double-precision scalar restatement, %d threads, %.1f s"
+                      % (frames, n_streams, F, threads, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--streams", type=int, default=65536, help="streams per GPU")
+    ap.add_argument("--frames", type=int, default=32, help="frames per stream per step")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gather", action="store_true", help="also time an RCCL PCM gather to rank 0 (reported apart)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import _gen
+    import mp3_amd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    n, F = args.streams, args.frames
+
+    # --- synthetic C3 shard of this rank (seed by global stream id) -------
+    t0 = time.time()
+    gen_threads = min(16, os.cpu_count() or 1)
+    buf, offs, sizes = _gen.batch(_gen.C3, 3_000_003 + rank * n, n, F, threads=gen_threads)
+    log("rank %d: generated %d streams x %d frames (%.1f MB) in %.1fs" % (rank, n, F, buf.size / 1e6, time.time() - t0))
+    d_in = torch.from_numpy(buf).to(dev)
+    pcm = torch.empty((n, F, 2304), dtype=torch.int16, device=dev)
+    infos = torch.zeros((n, F, 6), dtype=torch.int32, device=dev)
+    dec = mp3_amd.BatchDecoder(n, F, device=local)
+    strm = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        dec.decode(d_in, offs, sizes, F, pcm=pcm, infos=infos, stream=strm)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    ok = int((infos[..., 5] == 1152).sum().item())
+    if ok != n * F:
+        raise SystemExit("decode produced %d/%d frames" % (ok, n * F))
+
+    # --- timed region -------------------------------------------------------
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    frames_total = n * F * world * args.steps
+    value = frames_total / dt
+    ms_per_step = dt / args.steps * 1e3
+
+    # --- per-kernel device time (HIP events on the decode stream) ---------
+    dec.set_timing(True)
+    kt = {"scan": 0.0, "gather": 0.0, "huffman": 0.0, "synth": 0.0}
+    reps = max(1, min(3, args.steps))
+    for _ in range(reps):
+        step()
+        for k, v in dec.kernel_times_us().items():
+            kt[k] += v / reps
+    dec.set_timing(False)
+    torch.cuda.synchronize(dev)
+    dom = max(kt, key=kt.get)
+    frames_per_launch = n * F
+    synth_s = kt["synth"] * 1e-6
+    flops = FLOP_PER_FRAME * frames_per_launch
+    achieved_tf = flops / synth_s / 1e12 if synth_s > 0 else 0.0
+
+    traffic = None
+    prof = ROOT / "profiles" / "pmc_traffic.json"
+    if prof.exists():
+        try:
+            pj = json.loads(prof.read_text())
+            if pj.get("streams") == n and pj.get("frames") == F:
+                traffic = pj.get("k_synth_hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    gather = None
+    if args.gather and world > 1:
+        # optional xGMI PCM gather to rank 0 (RCCL), timed apart from decode
+        out = [torch.empty_like(pcm) for _ in range(world)] if rank == 0 else None
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        tg = time.perf_counter()
+        dist.gather(pcm, out, dst=0)
+        torch.cuda.synchronize(dev)
+        gather = {"ms": (time.perf_counter() - tg) * 1e3, "bytes": pcm.numel() * 2 * world}
+
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline()
+        step_s = dt / args.steps
+        res = {
+            "metric": "stereo MP3 frames/s (128 kbps 44.1 kHz) at 1/2/4/8 GPU; % HBM roofline",
+            "value": value,
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded generator: valid CBR 128 kbps 44.1 kHz joint-stereo MP3 frames)",
+            "config": {"workload": "C3: full Layer III decode (Huffman->PCM), %d streams x %d frames per GPU per step"
+                                   % (n, F),
+                       "streams_per_gpu": n, "frames_per_stream": F, "bitrate_kbps": 128, "hz": 44100,
+                       "parallelism": "streams sharded, 1 process per GPU, no data-path collective"},
+            "roofline": {
+                "kernel": "k_synth", "bound": "mfma", "unit": "TFLOP/s",
+                "achieved": achieved_tf, "peak": FP32_PEAK_TFLOPS, "frac": achieved_tf / FP32_PEAK_TFLOPS,
+                "flop_per_frame": FLOP_PER_FRAME, "frames_per_launch": frames_per_launch,
+                "launch_us": kt["synth"],
+                "achieved_GBs_algorithmic": SYNTH_BYTES_PER_FRAME * frames_per_launch / synth_s / 1e9 if synth_s else 0,
+                "traffic": traffic,
+            },
+            "hbm": {
+                "hbm_rw_frac": value / world * (BYTES_IN_PER_FRAME + PCM_BYTES_PER_FRAME) / (HBM_PEAK_GBS * 1e9),
+                "hbm_read_frac": value / world * BYTES_IN_PER_FRAME / (HBM_PEAK_GBS * 1e9),
+                "bytes_per_frame_rw": BYTES_IN_PER_FRAME + PCM_BYTES_PER_FRAME,
+            },
+            "kernel_us": kt,
+            "dominant_kernel": "k_" + dom,
+            "cpu_baseline": cpu,
+        }
+        if gather:
+            res["gather"] = gather
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

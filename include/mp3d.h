@@ -1,0 +1,129 @@
+/*
+ * mp3d.h -- C ABI of the MI355X-native batched MPEG-1 Layer III decoder.
+ *
+ * Drop-in boundary for the decode hot path of lxm0851/mp3.  The reference
+ * snapshot contains no decoder source and therefore no FFI surface to copy
+ * (SURVEY.md §8(b)): the player it describes (REF/README.md:2-3, "audio
+ * player ... crackle and noise during playback") decodes MP3 frame by frame
+ * in its playback loop, and REF/README.md:44 says it runs from source.  The
+ * per-frame entry point below replaces that (absent) per-frame decode call
+ * with the conventional shape of public C MP3 decoders (decoder handle,
+ * frame bytes in, interleaved int16 PCM + frame info out); the batch entry
+ * points expose the same path for tens of thousands of concurrent streams.
+ * INTEGRATION.md shows the ctypes / cffi / C++ bindings a host adds.
+ *
+ * Conventions
+ *  - Plain C types only.  All calls return >= 0 on success, a negative
+ *    MP3D_E* code on failure; nothing throws or aborts across the ABI.
+ *  - Caller owns every buffer passed in.  A handle owns its device memory
+ *    and decoder state; *_destroy frees it.
+ *  - PCM is int16, interleaved L/R, 1152 samples per channel per frame
+ *    (MPEG-1 Layer III).  Mono frames fill 1152 samples.
+ *  - The compute path is HIP on an AMD Instinct MI355X (gfx950).  There is
+ *    no CPU fallback: without a usable GPU, create calls fail with
+ *    MP3D_E_NO_DEVICE.
+ */
+#ifndef MP3D_H
+#define MP3D_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MP3D_ABI_VERSION 1
+
+#if defined(__GNUC__) || defined(__clang__)
+#define MP3D_API __attribute__((visibility("default")))
+#else
+#define MP3D_API
+#endif
+
+/* error codes */
+#define MP3D_OK 0
+#define MP3D_E_ARG (-1)        /* bad argument                                 */
+#define MP3D_E_NO_DEVICE (-2)  /* no HIP device / device ordinal out of range  */
+#define MP3D_E_HIP (-3)        /* HIP runtime error (see mp3d_last_hip_error)  */
+#define MP3D_E_NOMEM (-4)      /* device or host allocation failed             */
+#define MP3D_E_CAPACITY (-5)   /* batch larger than the handle was created for */
+#define MP3D_E_NEED_MORE (-6)  /* buffer holds no complete frame               */
+
+typedef struct mp3d_frame_info {
+    int frame_bytes;  /* bytes consumed (0: no frame found)                */
+    int channels;     /* 1 or 2                                            */
+    int hz;           /* 32000, 44100 or 48000                             */
+    int layer;        /* 3                                                 */
+    int bitrate_kbps; /* 32..320                                           */
+    int samples;      /* PCM samples per channel produced (1152 or 0)      */
+} mp3d_frame_info;
+
+typedef struct mp3d_dec mp3d_dec;
+typedef struct mp3d_batch mp3d_batch;
+
+/* ---- per-frame decoder (the player's decode call) ---------------------- *
+ * One decoder per audio stream and host thread.  mp3d_decode_frame finds
+ * the next frame in buf (skipping an ID3v2 tag / garbage before the sync
+ * word), decodes it on the GPU and returns samples per channel: 1152, or 0
+ * when bytes were consumed without audio (Xing/Info tag frame, invalid
+ * frame).  info->frame_bytes (+ any skipped prefix) tells how far to
+ * advance; pcm may be NULL (decode for state only).  Reservoir underflow
+ * (a stream entered mid-way) follows FFmpeg: the affected granules decode
+ * as silence.                                                               */
+MP3D_API int mp3d_dec_create(mp3d_dec **out);
+MP3D_API int mp3d_dec_create_on(int device, mp3d_dec **out);
+MP3D_API void mp3d_dec_destroy(mp3d_dec *dec);
+MP3D_API void mp3d_dec_reset(mp3d_dec *dec);
+MP3D_API int mp3d_decode_frame(mp3d_dec *dec, const uint8_t *buf, size_t bytes, int16_t *pcm /* <= 2304 */,
+                      mp3d_frame_info *info);
+
+/* ---- batched decoder (many concurrent streams on one GPU) -------------- *
+ * A batch handle keeps per-stream decoder state resident in HBM across
+ * calls: call k decodes frames [k*F, (k+1)*F) of every stream.
+ *
+ * frames           all streams' bytes; host memory or a device pointer on
+ *                  the handle's GPU (detected per call)
+ * offsets, sizes   host arrays [n_streams]: stream s occupies
+ *                  frames[offsets[s] .. offsets[s] + sizes[s])
+ * pcm              [n_streams][frames_per_stream][2304] int16, host or
+ *                  device; frames with info.samples == 0 are left untouched
+ * infos            [n_streams][frames_per_stream] or NULL, host or device
+ * hip_stream       hipStream_t to run on (NULL: the handle's own stream)
+ * The call is asynchronous when every pointer is device memory; otherwise
+ * it synchronises before returning.                                         */
+MP3D_API int mp3d_batch_create(int device, int max_streams, int max_frames, mp3d_batch **out);
+MP3D_API void mp3d_batch_destroy(mp3d_batch *b);
+MP3D_API int mp3d_batch_reset(mp3d_batch *b); /* forget all per-stream state         */
+MP3D_API int mp3d_batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets, const uint32_t *sizes,
+                      int n_streams, int frames_per_stream, int16_t *pcm, mp3d_frame_info *infos,
+                      void *hip_stream);
+MP3D_API int mp3d_batch_sync(mp3d_batch *b);
+
+/* ---- staged entry points (parity taps / BASELINE config 2) ------------- *
+ * huffman_only: run demux + reservoir + scalefactors + Huffman and return
+ *   is_out [n_streams][F][2][2][576] int16 and sf_out [..][2][2][40] uint8
+ *   (either may be NULL).  Advances per-stream state like a decode.
+ * synth_only: stages a8..a11 from spectra: xr [n_streams][F][2 gr][nch][576]
+ *   f32 (requantised, after stereo, bitstream order), block_type / mixed
+ *   [n_streams][F][2][nch]; pcm as in mp3d_batch_decode.                    */
+MP3D_API int mp3d_batch_huffman_only(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets, const uint32_t *sizes,
+                            int n_streams, int frames_per_stream, int16_t *is_out, uint8_t *sf_out,
+                            void *hip_stream);
+MP3D_API int mp3d_batch_synth_only(mp3d_batch *b, const float *xr, const uint8_t *block_type, const uint8_t *mixed,
+                          int n_streams, int frames_per_stream, int nch, int sample_rate_hz, int16_t *pcm,
+                          void *hip_stream);
+
+/* ---- diagnostics -------------------------------------------------------- */
+MP3D_API const char *mp3d_strerror(int err);
+MP3D_API int mp3d_last_hip_error(void);
+MP3D_API int mp3d_abi_version(void);
+/* device-side microseconds of each pipeline kernel in the last batch call
+ * (scan, gather, huffman, synth); needs mp3d_batch_set_timing(b, 1).        */
+MP3D_API int mp3d_batch_set_timing(mp3d_batch *b, int enable);
+MP3D_API int mp3d_batch_kernel_times(mp3d_batch *b, float *us4);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MP3D_H */

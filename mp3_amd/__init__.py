@@ -1,0 +1,242 @@
+"""mp3_amd -- MI355X-native batched MPEG-1 Layer III decoder (Python host side).
+
+Mirrors the C ABI of include/mp3d.h (the drop-in boundary for the reference
+player's per-frame decode call):
+
+  Decoder       per-frame decode (mp3d_decode_frame): bytes -> int16 PCM
+  BatchDecoder  many concurrent streams on one GPU (mp3d_batch_*), inputs and
+                outputs as numpy arrays (host) or torch tensors (device)
+
+The compute path is the HIP library mp3_amd/libmp3d.so; there is no CPU
+fallback.  Importing works without a GPU; creating a decoder does not.
+"""
+import ctypes
+import pathlib
+
+import numpy as np
+
+_HERE = pathlib.Path(__file__).resolve().parent
+LIB_PATH = _HERE / "libmp3d.so"
+
+MP3D_E = {0: "ok", -1: "bad argument", -2: "no usable HIP device", -3: "HIP runtime error", -4: "out of memory",
+          -5: "batch exceeds handle capacity", -6: "no complete frame in buffer"}
+
+
+class FrameInfo(ctypes.Structure):
+    _fields_ = [("frame_bytes", ctypes.c_int), ("channels", ctypes.c_int), ("hz", ctypes.c_int),
+                ("layer", ctypes.c_int), ("bitrate_kbps", ctypes.c_int), ("samples", ctypes.c_int)]
+
+
+FRAME_INFO_DT = np.dtype([("frame_bytes", np.int32), ("channels", np.int32), ("hz", np.int32),
+                          ("layer", np.int32), ("bitrate_kbps", np.int32), ("samples", np.int32)])
+
+EXPORTS = ["mp3d_dec_create", "mp3d_dec_create_on", "mp3d_dec_destroy", "mp3d_dec_reset", "mp3d_decode_frame",
+           "mp3d_batch_create", "mp3d_batch_destroy", "mp3d_batch_reset", "mp3d_batch_decode", "mp3d_batch_sync",
+           "mp3d_batch_huffman_only", "mp3d_batch_synth_only", "mp3d_strerror", "mp3d_last_hip_error",
+           "mp3d_abi_version", "mp3d_batch_set_timing", "mp3d_batch_kernel_times"]
+
+_lib = None
+
+
+class MP3DError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libmp3d.so (fails loudly if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise ImportError("mp3_amd: %s missing -- run __graft_entry__.build() (no CPU fallback exists)" % LIB_PATH)
+        L = ctypes.CDLL(str(LIB_PATH))
+        vp, i, u64p, u32p = ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p
+        L.mp3d_dec_create.argtypes = [ctypes.POINTER(vp)]
+        L.mp3d_dec_create_on.argtypes = [i, ctypes.POINTER(vp)]
+        L.mp3d_dec_destroy.argtypes = [vp]
+        L.mp3d_dec_destroy.restype = None
+        L.mp3d_dec_reset.argtypes = [vp]
+        L.mp3d_dec_reset.restype = None
+        L.mp3d_decode_frame.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t, vp, ctypes.POINTER(FrameInfo)]
+        L.mp3d_batch_create.argtypes = [i, i, i, ctypes.POINTER(vp)]
+        L.mp3d_batch_destroy.argtypes = [vp]
+        L.mp3d_batch_destroy.restype = None
+        L.mp3d_batch_reset.argtypes = [vp]
+        L.mp3d_batch_decode.argtypes = [vp, vp, u64p, u32p, i, i, vp, vp, vp]
+        L.mp3d_batch_sync.argtypes = [vp]
+        L.mp3d_batch_huffman_only.argtypes = [vp, vp, u64p, u32p, i, i, vp, vp, vp]
+        L.mp3d_batch_synth_only.argtypes = [vp, vp, vp, vp, i, i, i, i, vp, vp]
+        L.mp3d_strerror.argtypes = [i]
+        L.mp3d_strerror.restype = ctypes.c_char_p
+        L.mp3d_batch_set_timing.argtypes = [vp, i]
+        L.mp3d_batch_kernel_times.argtypes = [vp, vp]
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc < 0:
+        L = lib()
+        raise MP3DError("mp3d error %d (%s), hip error %d" % (rc, L.mp3d_strerror(rc).decode(), L.mp3d_last_hip_error()))
+    return rc
+
+
+def _ptr(x):
+    """(pointer, keepalive) for a numpy array, torch tensor, bytes or None."""
+    if x is None:
+        return None, None
+    if isinstance(x, (bytes, bytearray)):
+        a = np.frombuffer(bytes(x), np.uint8)
+        return a.ctypes.data, a
+    if isinstance(x, np.ndarray):
+        if not x.flags.c_contiguous:
+            raise ValueError("array must be C-contiguous")
+        return x.ctypes.data, x
+    if hasattr(x, "data_ptr"):
+        if not x.is_contiguous():
+            raise ValueError("tensor must be contiguous")
+        return x.data_ptr(), x
+    raise TypeError("unsupported buffer type %r" % type(x))
+
+
+class Decoder:
+    """Per-frame decoder (mp3d_decode_frame), one per stream."""
+
+    def __init__(self, device=None):
+        L = lib()
+        h = ctypes.c_void_p()
+        if device is None:
+            _check(L.mp3d_dec_create(ctypes.byref(h)))
+        else:
+            _check(L.mp3d_dec_create_on(int(device), ctypes.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().mp3d_dec_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def reset(self):
+        lib().mp3d_dec_reset(self._h)
+
+    def decode_frame(self, buf):
+        """Returns (samples_per_channel, pcm int16 [samples*channels], FrameInfo)."""
+        pcm = np.zeros(2304, np.int16)
+        info = FrameInfo()
+        buf = bytes(buf)
+        n = _check(lib().mp3d_decode_frame(self._h, buf, len(buf), pcm.ctypes.data, ctypes.byref(info)))
+        return n, pcm[: n * max(info.channels, 1)], info
+
+    def decode_stream(self, data):
+        """Decode a whole byte stream; returns int16 [channels, samples]."""
+        data = bytes(data)
+        pos, out, nch = 0, [], 0
+        while pos < len(data):
+            try:
+                n, pcm, info = self.decode_frame(data[pos:])
+            except MP3DError:
+                break
+            if info.frame_bytes <= 0:
+                break
+            pos += info.frame_bytes
+            if n:
+                nch = info.channels
+                out.append(pcm.reshape(n, nch))
+        if not out:
+            return np.zeros((0, 0), np.int16)
+        return np.concatenate(out).T.copy()
+
+
+class BatchDecoder:
+    """Batched decoder: per-stream state stays in HBM across calls."""
+
+    def __init__(self, max_streams, max_frames, device=0):
+        L = lib()
+        h = ctypes.c_void_p()
+        _check(L.mp3d_batch_create(int(device), int(max_streams), int(max_frames), ctypes.byref(h)))
+        self._h = h
+        self.device = device
+        self.max_streams, self.max_frames = max_streams, max_frames
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().mp3d_batch_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def reset(self):
+        _check(lib().mp3d_batch_reset(self._h))
+
+    def sync(self):
+        _check(lib().mp3d_batch_sync(self._h))
+
+    def set_timing(self, on=True):
+        _check(lib().mp3d_batch_set_timing(self._h, int(on)))
+
+    def kernel_times_us(self):
+        t = np.zeros(4, np.float32)
+        _check(lib().mp3d_batch_kernel_times(self._h, t.ctypes.data))
+        return dict(zip(("scan", "gather", "huffman", "synth"), t.tolist()))
+
+    @staticmethod
+    def _geom(offsets, sizes):
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        sz = np.ascontiguousarray(sizes, dtype=np.uint32)
+        if off.shape != sz.shape:
+            raise ValueError("offsets/sizes shape mismatch")
+        return off, sz
+
+    def decode(self, frames, offsets, sizes, frames_per_stream, pcm=None, infos=None, stream=None):
+        """frames: bytes/np.uint8/torch.uint8; pcm: None (allocate host) or
+        int16 array/tensor [n, F, 2304]; infos: None or FRAME_INFO_DT array /
+        int32 tensor [n, F, 6].  Returns (pcm, infos)."""
+        off, sz = self._geom(offsets, sizes)
+        n, F = off.size, int(frames_per_stream)
+        if pcm is None:
+            pcm = np.zeros((n, F, 2304), np.int16)
+        if infos is None:
+            infos = np.zeros((n, F), FRAME_INFO_DT)
+        fp, k1 = _ptr(frames)
+        pp, k2 = _ptr(pcm)
+        ip, k3 = _ptr(infos)
+        _check(lib().mp3d_batch_decode(self._h, fp, off.ctypes.data, sz.ctypes.data, n, F, pp, ip,
+                                       ctypes.c_void_p(stream) if stream else None))
+        return pcm, infos
+
+    def huffman_only(self, frames, offsets, sizes, frames_per_stream):
+        off, sz = self._geom(offsets, sizes)
+        n, F = off.size, int(frames_per_stream)
+        is_out = np.zeros((n, F, 2, 2, 576), np.int16)
+        sf_out = np.zeros((n, F, 2, 2, 40), np.uint8)
+        fp, k1 = _ptr(frames)
+        _check(lib().mp3d_batch_huffman_only(self._h, fp, off.ctypes.data, sz.ctypes.data, n, F,
+                                             is_out.ctypes.data, sf_out.ctypes.data, None))
+        return is_out, sf_out
+
+    def synth_only(self, xr, block_type, mixed, nch, hz, pcm=None, stream=None):
+        """xr f32 [n, F, 2, nch, 576]; block_type/mixed uint8 [n, F, 2, nch]."""
+        n, F = int(xr.shape[0]), int(xr.shape[1])
+        if pcm is None:
+            pcm = np.zeros((n, F, 2304), np.int16)
+        xp, k1 = _ptr(xr)
+        bp, k2 = _ptr(block_type)
+        mp, k3 = _ptr(mixed)
+        pp, k4 = _ptr(pcm)
+        _check(lib().mp3d_batch_synth_only(self._h, xp, bp, mp, n, F, int(nch), int(hz), pp,
+                                           ctypes.c_void_p(stream) if stream else None))
+        return pcm
+
+
+def pcm_to_planar(pcm_frames, infos):
+    """[F, 2304] int16 + infos [F] -> [channels, samples] for frames with audio."""
+    rows = []
+    nch = 0
+    for f in range(pcm_frames.shape[0]):
+        if infos[f]["samples"]:
+            nch = int(infos[f]["channels"])
+            rows.append(pcm_frames[f, : 1152 * nch].reshape(1152, nch))
+    if not rows:
+        return np.zeros((0, 0), np.int16)
+    return np.concatenate(rows).T.copy()

@@ -1,0 +1,626 @@
+/*
+ * mp3d_host.cpp -- host side of the MI355X MP3 decoder: the C ABI declared
+ * in include/mp3d.h, constant-table construction (ISO 11172-3 Annex B and
+ * 2.4.3.4 formulas), batch buffer management and kernel launches.
+ *
+ * No CPU decode path exists here: every frame is decoded by the HIP kernels
+ * in mp3d_kernels.hip; without a device the create calls fail.
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/mp3d.h"
+#include "mp3d_internal.h"
+#include "mp3d_tables.h"
+
+namespace mp3d {
+hipError_t upload_constants(const float *, const float *, const float *, const float *, const float *, const float *,
+                            const float *, const float *);
+void launch_scan(const uint8_t *, const uint64_t *, const uint32_t *, StreamState *, FrameRec *, int32_t *, void *, int,
+                 int, hipStream_t);
+void launch_gather(const uint8_t *, uint8_t *, const uint64_t *, StreamState *, const FrameRec *, const int32_t *, int,
+                   int, hipStream_t);
+void launch_huffman(const uint8_t *, const uint8_t *, const uint64_t *, const FrameRec *, const DevTables *, int16_t *,
+                    UnitMeta *, int, int, int, hipStream_t);
+void launch_synth(const FrameRec *, const int16_t *, const UnitMeta *, const DevTables *, StreamState *, int16_t *, int,
+                  int, hipStream_t);
+void launch_synth_xr(const float *, const uint8_t *, const uint8_t *, const DevTables *, StreamState *, int16_t *, int,
+                     int, int, int, hipStream_t);
+} // namespace mp3d
+
+using namespace mp3d;
+
+static thread_local int g_last_hip = 0;
+#define HIPCHK(x)                                                                                                      \
+    do {                                                                                                               \
+        hipError_t _e = (x);                                                                                           \
+        if (_e != hipSuccess) {                                                                                        \
+            g_last_hip = (int)_e;                                                                                      \
+            return _e == hipErrorOutOfMemory ? MP3D_E_NOMEM : MP3D_E_HIP;                                              \
+        }                                                                                                              \
+    } while (0)
+
+/* ------------------------------------------------------------------------ */
+/* Constant tables                                                          */
+/* ------------------------------------------------------------------------ */
+static void build_huffman_lut(DevTables &t) {
+    /* two-level LUT: first level min(8, maxlen) bits; codes longer than that
+     * go through one sub-table per 8-bit prefix (see mp3d_internal.h) */
+    std::vector<uint32_t> lut;
+    for (int ti = 0; ti < MP3D_LUT_TABLES; ti++) {
+        std::vector<uint32_t> code, len, val;
+        if (ti < MP3D_NUM_HTABS) {
+            int n = MP3D_HTAB_ROWLEN[ti];
+            for (int x = 0; x < n; x++)
+                for (int y = 0; y < n; y++) {
+                    code.push_back(MP3D_HTAB_CODES[ti][x * n + y]);
+                    len.push_back(MP3D_HTAB_LENS[ti][x * n + y]);
+                    val.push_back((uint32_t)(x << 4 | y));
+                }
+        } else {
+            for (int v = 0; v < 16; v++) {
+                code.push_back(MP3D_QUAD_CODE[0][v]);
+                len.push_back(MP3D_QUAD_LEN[0][v]);
+                val.push_back((uint32_t)v);
+            }
+        }
+        uint32_t maxlen = *std::max_element(len.begin(), len.end());
+        int b1 = (int)std::min<uint32_t>(8, maxlen);
+        size_t base = lut.size();
+        t.lut_hdr.base[ti] = (uint16_t)base;
+        t.lut_hdr.bits1[ti] = (uint8_t)b1;
+        lut.resize(base + (1u << b1), 0xFFFFFFFFu);
+        /* sub-table depth per prefix */
+        std::vector<int> subbits(1u << b1, 0);
+        for (size_t i = 0; i < code.size(); i++)
+            if ((int)len[i] > b1) {
+                uint32_t p = code[i] >> (len[i] - b1);
+                subbits[p] = std::max(subbits[p], (int)len[i] - b1);
+            }
+        for (uint32_t p = 0; p < (1u << b1); p++)
+            if (subbits[p]) {
+                size_t sb = lut.size();
+                lut.resize(sb + (1u << subbits[p]), 0xFFFFFFFFu);
+                lut[base + p] = 0x80000000u | ((uint32_t)subbits[p] << 16) | (uint32_t)sb;
+            }
+        for (size_t i = 0; i < code.size(); i++) {
+            uint32_t leaf = (len[i] << 8) | val[i];
+            if ((int)len[i] <= b1) {
+                uint32_t first = code[i] << (b1 - len[i]), cnt = 1u << (b1 - len[i]);
+                for (uint32_t k = 0; k < cnt; k++) lut[base + first + k] = leaf;
+            } else {
+                uint32_t p = code[i] >> (len[i] - b1);
+                uint32_t ptr = lut[base + p];
+                int nb = (int)((ptr >> 16) & 31);
+                uint32_t rest = code[i] & ((1u << (len[i] - b1)) - 1);
+                uint32_t first = rest << (nb - (len[i] - b1)), cnt = 1u << (nb - (len[i] - b1));
+                for (uint32_t k = 0; k < cnt; k++) lut[(ptr & 0xFFFF) + first + k] = leaf;
+            }
+        }
+    }
+    if (lut.size() > MP3D_LUT_MAX) {
+        fprintf(stderr, "mp3d: LUT overflow %zu\n", lut.size());
+        abort();
+    }
+    for (size_t i = 0; i < lut.size(); i++) t.lut[i] = lut[i] == 0xFFFFFFFFu ? (1u << 8) : lut[i];
+}
+
+static void build_tables(DevTables &t) {
+    memset(&t, 0, sizeof(t));
+    for (int i = 0; i < 8208; i++) t.pow43[i] = (float)pow((double)i, 4.0 / 3.0);
+    for (int m = 0; m < 32; m++)
+        for (int k = 0; k < 32; k++) t.dct_c[m][k] = (float)cos(m * (2 * k + 1) * M_PI / 64.0);
+    double D[512];
+    for (int i = 0; i <= 256; i++) {
+        double v = MP3D_SYNTH_WINDOW_Q16[i] / 65536.0;
+        D[i] = v;
+        if (i > 0) D[512 - i] = (i % 64) ? -v : v;
+    }
+    for (int j = 0; j < 32; j++) {
+        int a, sa, b, sbn = -1;
+        if (j < 16) { a = 16 + j; sa = 1; b = 16 - j; }
+        else if (j == 16) { a = 0; sa = 0; b = 0; }
+        else { a = 48 - j; sa = -1; b = j - 16; }
+        t.win_a[j] = (uint8_t)a;
+        t.win_b[j] = (uint8_t)b;
+        for (int i = 0; i < 8; i++) {
+            t.dwin[j][2 * i] = (float)(sa * D[64 * i + j]);
+            t.dwin[j][2 * i + 1] = (float)(sbn * D[64 * i + 32 + j]);
+        }
+    }
+    for (int sr = 0; sr < 3; sr++) {
+        int l = 0;
+        for (int b = 0; b < 22; b++)
+            for (int n = 0; n < MP3D_SFB_LONG_WIDTH[sr][b]; n++) t.long_sfb[sr][l++] = (uint8_t)b;
+        int p = 0;
+        for (int b = 0; b < 13; b++) {
+            int w = MP3D_SFB_SHORT_WIDTH[sr][b];
+            for (int off = 0; off < 3 * w; off++) {
+                int f = off / 3, win = off % 3;
+                t.short_src[sr][p + off] = (uint16_t)(p + win * w + f);
+                t.bs_band[sr][p + off] = (uint8_t)b;
+                t.bs_win[sr][p + off] = (uint8_t)(off / w);
+            }
+            p += 3 * w;
+        }
+    }
+    build_huffman_lut(t);
+}
+
+static int upload_symbols() {
+    float imdct36[18][18], imdct12[6][6], win36[4][36], win12[12], cs[8], ca[8], isr[7][2], p2q[4];
+    for (int k = 0; k < 18; k++)
+        for (int o = 0; o < 18; o++) {
+            int i = o < 9 ? o : 18 + (o - 9);
+            imdct36[k][o] = (float)cos(M_PI / 72.0 * (2 * i + 19) * (2 * k + 1));
+        }
+    for (int k = 0; k < 6; k++)
+        for (int o = 0; o < 6; o++) {
+            int i = o < 3 ? o : 6 + (o - 3);
+            imdct12[k][o] = (float)cos(M_PI / 24.0 * (2 * i + 7) * (2 * k + 1));
+        }
+    for (int i = 0; i < 36; i++) {
+        win36[0][i] = (float)sin(M_PI / 36.0 * (i + 0.5));
+        win36[1][i] = (float)(i < 18 ? sin(M_PI / 36.0 * (i + 0.5)) : i < 24 ? 1.0 : i < 30 ? sin(M_PI / 12.0 * (i - 18 + 0.5)) : 0.0);
+        win36[3][i] = (float)(i < 6 ? 0.0 : i < 12 ? sin(M_PI / 12.0 * (i - 6 + 0.5)) : i < 18 ? 1.0 : sin(M_PI / 36.0 * (i + 0.5)));
+        win36[2][i] = win36[0][i]; /* unused: short blocks use win12 */
+    }
+    for (int i = 0; i < 12; i++) win12[i] = (float)sin(M_PI / 12.0 * (i + 0.5));
+    for (int i = 0; i < 8; i++) {
+        double c = MP3D_ALIAS_C[i], d = sqrt(1.0 + c * c);
+        cs[i] = (float)(1.0 / d);
+        ca[i] = (float)(c / d);
+    }
+    for (int p = 0; p < 7; p++) {
+        if (p == 6) { isr[p][0] = 1.f; isr[p][1] = 0.f; continue; }
+        double tn = tan(p * M_PI / 12.0);
+        isr[p][0] = (float)(tn / (1.0 + tn));
+        isr[p][1] = (float)(1.0 / (1.0 + tn));
+    }
+    for (int i = 0; i < 4; i++) p2q[i] = (float)pow(2.0, i / 4.0);
+    HIPCHK(upload_constants(&imdct36[0][0], &imdct12[0][0], &win36[0][0], win12, cs, ca, &isr[0][0], p2q));
+    return MP3D_OK;
+}
+
+/* per-device one-time init: constant symbols + table buffer */
+struct DeviceCtx {
+    bool ready = false;
+    DevTables *tables = nullptr;
+    int n_cu = 256;
+};
+static std::mutex g_mu;
+static DeviceCtx g_dev[64];
+
+static int device_init(int device) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MP3D_E_NO_DEVICE;
+    if (device < 0 || device >= n || device >= 64) return MP3D_E_NO_DEVICE;
+    DeviceCtx &c = g_dev[device];
+    HIPCHK(hipSetDevice(device));
+    if (c.ready) return MP3D_OK;
+    int r = upload_symbols();
+    if (r) return r;
+    static DevTables host_tables;
+    static bool built = false;
+    if (!built) {
+        build_tables(host_tables);
+        built = true;
+    }
+    HIPCHK(hipMalloc(&c.tables, sizeof(DevTables)));
+    HIPCHK(hipMemcpy(c.tables, &host_tables, sizeof(DevTables), hipMemcpyHostToDevice));
+    (void)hipDeviceGetAttribute(&c.n_cu, hipDeviceAttributeMultiprocessorCount, device);
+    c.ready = true;
+    return MP3D_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Batch                                                                    */
+/* ------------------------------------------------------------------------ */
+struct mp3d_batch {
+    int device = 0, max_streams = 0, max_frames = 0;
+    hipStream_t own = nullptr;
+    StreamState *st = nullptr;
+    FrameRec *rec = nullptr;
+    int16_t *is_buf = nullptr;
+    UnitMeta *meta = nullptr;
+    int32_t *carry = nullptr;
+    uint64_t *d_in_off = nullptr, *d_md_off = nullptr;
+    uint32_t *d_in_len = nullptr;
+    mp3d_frame_info *d_infos = nullptr;
+    uint8_t *md = nullptr;
+    size_t md_cap = 0;
+    uint8_t *d_in = nullptr; /* staging for host input */
+    size_t in_cap = 0;
+    int16_t *d_pcm = nullptr; /* staging for host output */
+    size_t pcm_cap = 0;
+    float *d_xr = nullptr;
+    uint8_t *d_bt = nullptr, *d_mx = nullptr;
+    size_t xr_cap = 0;
+    std::vector<uint64_t> last_off, md_off_host;
+    std::vector<uint32_t> last_len;
+    int last_n = -1;
+    bool timing = false;
+    hipEvent_t ev[5] = {};
+    float times[4] = {0, 0, 0, 0};
+};
+
+static bool is_device_ptr(const void *p) {
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+static int grow(void **p, size_t *cap, size_t need) {
+    if (need <= *cap) return MP3D_OK;
+    if (*p) HIPCHK(hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    HIPCHK(hipMalloc(p, need));
+    *cap = need;
+    return MP3D_OK;
+}
+
+extern "C" int mp3d_batch_create(int device, int max_streams, int max_frames, mp3d_batch **out) {
+    if (!out || max_streams <= 0 || max_frames <= 0) return MP3D_E_ARG;
+    *out = nullptr;
+    int r = device_init(device);
+    if (r) return r;
+    mp3d_batch *b = new (std::nothrow) mp3d_batch;
+    if (!b) return MP3D_E_NOMEM;
+    b->device = device;
+    b->max_streams = max_streams;
+    b->max_frames = max_frames;
+    size_t units = (size_t)max_streams * max_frames * 4;
+#define BALLOC(ptr, bytes)                                                                                             \
+    do {                                                                                                               \
+        hipError_t _e = hipMalloc((void **)&(ptr), (bytes));                                                           \
+        if (_e != hipSuccess) {                                                                                        \
+            g_last_hip = (int)_e;                                                                                      \
+            mp3d_batch_destroy(b);                                                                                     \
+            return MP3D_E_NOMEM;                                                                                       \
+        }                                                                                                              \
+    } while (0)
+    BALLOC(b->st, sizeof(StreamState) * max_streams);
+    BALLOC(b->rec, sizeof(FrameRec) * (size_t)max_streams * max_frames);
+    BALLOC(b->is_buf, sizeof(int16_t) * 576 * units);
+    BALLOC(b->meta, sizeof(UnitMeta) * units);
+    BALLOC(b->carry, sizeof(int32_t) * 2 * max_streams);
+    BALLOC(b->d_in_off, sizeof(uint64_t) * max_streams);
+    BALLOC(b->d_md_off, sizeof(uint64_t) * max_streams);
+    BALLOC(b->d_in_len, sizeof(uint32_t) * max_streams);
+    BALLOC(b->d_infos, sizeof(mp3d_frame_info) * (size_t)max_streams * max_frames);
+#undef BALLOC
+    if (hipStreamCreateWithFlags(&b->own, hipStreamNonBlocking) != hipSuccess) {
+        mp3d_batch_destroy(b);
+        return MP3D_E_HIP;
+    }
+    for (int i = 0; i < 5; i++) (void)hipEventCreate(&b->ev[i]);
+    if (hipMemset(b->st, 0, sizeof(StreamState) * max_streams) != hipSuccess) {
+        mp3d_batch_destroy(b);
+        return MP3D_E_HIP;
+    }
+    *out = b;
+    return MP3D_OK;
+}
+
+extern "C" void mp3d_batch_destroy(mp3d_batch *b) {
+    if (!b) return;
+    (void)hipSetDevice(b->device);
+    if (b->own) (void)hipStreamSynchronize(b->own);
+    void *ptrs[] = {b->st, b->rec, b->is_buf, b->meta, b->carry, b->d_in_off, b->d_md_off, b->d_in_len,
+                    b->d_infos, b->md, b->d_in, b->d_pcm, b->d_xr, b->d_bt, b->d_mx};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
+    for (int i = 0; i < 5; i++)
+        if (b->ev[i]) (void)hipEventDestroy(b->ev[i]);
+    if (b->own) (void)hipStreamDestroy(b->own);
+    delete b;
+}
+
+extern "C" int mp3d_batch_reset(mp3d_batch *b) {
+    if (!b) return MP3D_E_ARG;
+    HIPCHK(hipSetDevice(b->device));
+    HIPCHK(hipMemsetAsync(b->st, 0, sizeof(StreamState) * b->max_streams, b->own));
+    HIPCHK(hipStreamSynchronize(b->own));
+    return MP3D_OK;
+}
+
+extern "C" int mp3d_batch_sync(mp3d_batch *b) {
+    if (!b) return MP3D_E_ARG;
+    HIPCHK(hipSetDevice(b->device));
+    HIPCHK(hipStreamSynchronize(b->own));
+    HIPCHK(hipDeviceSynchronize());
+    return MP3D_OK;
+}
+
+extern "C" int mp3d_batch_set_timing(mp3d_batch *b, int enable) {
+    if (!b) return MP3D_E_ARG;
+    b->timing = enable != 0;
+    return MP3D_OK;
+}
+
+extern "C" int mp3d_batch_kernel_times(mp3d_batch *b, float *us4) {
+    if (!b || !us4) return MP3D_E_ARG;
+    if (!b->timing) return MP3D_E_ARG;
+    HIPCHK(hipEventSynchronize(b->ev[4]));
+    for (int i = 0; i < 4; i++) {
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, b->ev[i], b->ev[i + 1]));
+        us4[i] = ms * 1000.f;
+    }
+    return MP3D_OK;
+}
+
+/* Upload stream geometry (cached when unchanged) and size the md region. */
+static int prepare_geometry(mp3d_batch *b, const uint64_t *offsets, const uint32_t *sizes, int n, hipStream_t s) {
+    bool same = b->last_n == n && !memcmp(b->last_off.data(), offsets, sizeof(uint64_t) * n) &&
+                !memcmp(b->last_len.data(), sizes, sizeof(uint32_t) * n);
+    if (same) return MP3D_OK;
+    b->last_off.assign(offsets, offsets + n);
+    b->last_len.assign(sizes, sizes + n);
+    b->md_off_host.resize(n);
+    size_t o = 0;
+    for (int i = 0; i < n; i++) {
+        b->md_off_host[i] = o;
+        o += ((size_t)sizes[i] + MP3D_RES_BYTES + 16 + 15) & ~(size_t)15;
+    }
+    int r = grow((void **)&b->md, &b->md_cap, o + 8192);
+    if (r) return r;
+    HIPCHK(hipMemcpyAsync(b->d_in_off, offsets, sizeof(uint64_t) * n, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(b->d_in_len, sizes, sizeof(uint32_t) * n, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(b->d_md_off, b->md_off_host.data(), sizeof(uint64_t) * n, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s)); /* host vectors must outlive the copies */
+    b->last_n = n;
+    return MP3D_OK;
+}
+
+/* Front half shared by decode and huffman_only: input staging + k_scan,
+ * k_gather, k_huffman. */
+static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets, const uint32_t *sizes, int n,
+                     int F, hipStream_t s, bool *sync_needed) {
+    if (!b || !frames || !offsets || !sizes || n <= 0 || F <= 0) return MP3D_E_ARG;
+    if (n > b->max_streams || F > b->max_frames) return MP3D_E_CAPACITY;
+    HIPCHK(hipSetDevice(b->device));
+    uint64_t total = 0;
+    for (int i = 0; i < n; i++) total = std::max<uint64_t>(total, offsets[i] + sizes[i]);
+    const uint8_t *din = frames;
+    if (!is_device_ptr(frames)) {
+        int r = grow((void **)&b->d_in, &b->in_cap, total + 64);
+        if (r) return r;
+        HIPCHK(hipMemcpyAsync(b->d_in, frames, total, hipMemcpyHostToDevice, s));
+        din = b->d_in;
+        *sync_needed = true;
+    }
+    int r = prepare_geometry(b, offsets, sizes, n, s);
+    if (r) return r;
+    DeviceCtx &dc = g_dev[b->device];
+    if (b->timing) HIPCHK(hipEventRecord(b->ev[0], s));
+    launch_scan(din, b->d_in_off, b->d_in_len, b->st, b->rec, b->carry, b->d_infos, n, F, s);
+    if (b->timing) HIPCHK(hipEventRecord(b->ev[1], s));
+    launch_gather(din, b->md, b->d_md_off, b->st, b->rec, b->carry, n, F, s);
+    if (b->timing) HIPCHK(hipEventRecord(b->ev[2], s));
+    launch_huffman(din, b->md, b->d_md_off, b->rec, dc.tables, b->is_buf, b->meta, n, F, dc.n_cu, s);
+    if (b->timing) HIPCHK(hipEventRecord(b->ev[3], s));
+    HIPCHK(hipGetLastError());
+    return MP3D_OK;
+}
+
+extern "C" int mp3d_batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets, const uint32_t *sizes,
+                                 int n, int F, int16_t *pcm, mp3d_frame_info *infos, void *hip_stream) {
+    if (!b || !pcm) return MP3D_E_ARG;
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : b->own;
+    bool sync_needed = false;
+    int r = run_front(b, frames, offsets, sizes, n, F, s, &sync_needed);
+    if (r) return r;
+    size_t pcm_bytes = (size_t)n * F * 2304 * sizeof(int16_t);
+    int16_t *dpcm = pcm;
+    bool pcm_host = !is_device_ptr(pcm);
+    if (pcm_host) {
+        r = grow((void **)&b->d_pcm, &b->pcm_cap, pcm_bytes);
+        if (r) return r;
+        dpcm = b->d_pcm;
+        /* frames without audio leave the caller's PCM untouched */
+        HIPCHK(hipMemcpyAsync(dpcm, pcm, pcm_bytes, hipMemcpyHostToDevice, s));
+    }
+    DeviceCtx &dc = g_dev[b->device];
+    launch_synth(b->rec, b->is_buf, b->meta, dc.tables, b->st, dpcm, n, F, s);
+    if (b->timing) HIPCHK(hipEventRecord(b->ev[4], s));
+    HIPCHK(hipGetLastError());
+    if (pcm_host) {
+        HIPCHK(hipMemcpyAsync(pcm, dpcm, pcm_bytes, hipMemcpyDeviceToHost, s));
+        sync_needed = true;
+    }
+    if (infos) {
+        size_t ib = sizeof(mp3d_frame_info) * (size_t)n * F;
+        if (is_device_ptr(infos)) {
+            HIPCHK(hipMemcpyAsync(infos, b->d_infos, ib, hipMemcpyDeviceToDevice, s));
+        } else {
+            HIPCHK(hipMemcpyAsync(infos, b->d_infos, ib, hipMemcpyDeviceToHost, s));
+            sync_needed = true;
+        }
+    }
+    if (sync_needed) HIPCHK(hipStreamSynchronize(s));
+    return MP3D_OK;
+}
+
+extern "C" int mp3d_batch_huffman_only(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets,
+                                       const uint32_t *sizes, int n, int F, int16_t *is_out, uint8_t *sf_out,
+                                       void *hip_stream) {
+    if (!b) return MP3D_E_ARG;
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : b->own;
+    bool sync_needed = false;
+    int r = run_front(b, frames, offsets, sizes, n, F, s, &sync_needed);
+    if (r) return r;
+    size_t units = (size_t)n * F * 4;
+    if (is_out) {
+        hipMemcpyKind k = is_device_ptr(is_out) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+        HIPCHK(hipMemcpyAsync(is_out, b->is_buf, units * 576 * sizeof(int16_t), k, s));
+        sync_needed |= k == hipMemcpyDeviceToHost;
+    }
+    if (sf_out) {
+        bool dev = is_device_ptr(sf_out);
+        HIPCHK(hipMemcpy2DAsync(sf_out, 40, b->meta, sizeof(UnitMeta), 40, units,
+                                dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
+        sync_needed |= !dev;
+    }
+    if (sync_needed) HIPCHK(hipStreamSynchronize(s));
+    return MP3D_OK;
+}
+
+extern "C" int mp3d_batch_synth_only(mp3d_batch *b, const float *xr, const uint8_t *block_type, const uint8_t *mixed,
+                                     int n, int F, int nch, int hz, int16_t *pcm, void *hip_stream) {
+    if (!b || !xr || !block_type || !mixed || !pcm || n <= 0 || F <= 0 || (nch != 1 && nch != 2)) return MP3D_E_ARG;
+    if (n > b->max_streams || F > b->max_frames) return MP3D_E_CAPACITY;
+    int sr = hz == 44100 ? 0 : hz == 48000 ? 1 : hz == 32000 ? 2 : -1;
+    if (sr < 0) return MP3D_E_ARG;
+    HIPCHK(hipSetDevice(b->device));
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : b->own;
+    bool sync_needed = false;
+    size_t nx = (size_t)n * F * 2 * nch;
+    const float *dxr = xr;
+    const uint8_t *dbt = block_type, *dmx = mixed;
+    if (!is_device_ptr(xr) || !is_device_ptr(block_type) || !is_device_ptr(mixed)) {
+        size_t need = nx * 576 * sizeof(float) + 2 * nx + 64;
+        int r = grow((void **)&b->d_xr, &b->xr_cap, need);
+        if (r) return r;
+        uint8_t *base = (uint8_t *)b->d_xr;
+        HIPCHK(hipMemcpyAsync(base, xr, nx * 576 * sizeof(float), hipMemcpyDefault, s));
+        HIPCHK(hipMemcpyAsync(base + nx * 576 * sizeof(float), block_type, nx, hipMemcpyDefault, s));
+        HIPCHK(hipMemcpyAsync(base + nx * 576 * sizeof(float) + nx, mixed, nx, hipMemcpyDefault, s));
+        dxr = (const float *)base;
+        dbt = base + nx * 576 * sizeof(float);
+        dmx = dbt + nx;
+        sync_needed = true;
+    }
+    size_t pcm_bytes = (size_t)n * F * 2304 * sizeof(int16_t);
+    int16_t *dpcm = pcm;
+    bool pcm_host = !is_device_ptr(pcm);
+    if (pcm_host) {
+        int r = grow((void **)&b->d_pcm, &b->pcm_cap, pcm_bytes);
+        if (r) return r;
+        dpcm = b->d_pcm;
+    }
+    DeviceCtx &dc = g_dev[b->device];
+    if (b->timing) {
+        for (int i = 0; i < 4; i++) HIPCHK(hipEventRecord(b->ev[i], s));
+    }
+    launch_synth_xr(dxr, dbt, dmx, dc.tables, b->st, dpcm, n, F, nch, sr, s);
+    if (b->timing) HIPCHK(hipEventRecord(b->ev[4], s));
+    HIPCHK(hipGetLastError());
+    if (pcm_host) {
+        HIPCHK(hipMemcpyAsync(pcm, dpcm, pcm_bytes, hipMemcpyDeviceToHost, s));
+        sync_needed = true;
+    }
+    if (sync_needed) HIPCHK(hipStreamSynchronize(s));
+    return MP3D_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Per-frame decoder                                                         */
+/* ------------------------------------------------------------------------ */
+struct mp3d_dec {
+    mp3d_batch *b = nullptr;
+    long frames = 0;
+};
+
+extern "C" int mp3d_dec_create_on(int device, mp3d_dec **out) {
+    if (!out) return MP3D_E_ARG;
+    *out = nullptr;
+    mp3d_dec *d = new (std::nothrow) mp3d_dec;
+    if (!d) return MP3D_E_NOMEM;
+    int r = mp3d_batch_create(device, 1, 1, &d->b);
+    if (r) {
+        delete d;
+        return r;
+    }
+    *out = d;
+    return MP3D_OK;
+}
+
+extern "C" int mp3d_dec_create(mp3d_dec **out) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    return mp3d_dec_create_on(dev, out);
+}
+
+extern "C" void mp3d_dec_destroy(mp3d_dec *d) {
+    if (!d) return;
+    mp3d_batch_destroy(d->b);
+    delete d;
+}
+
+extern "C" void mp3d_dec_reset(mp3d_dec *d) {
+    if (!d) return;
+    (void)mp3d_batch_reset(d->b);
+    d->frames = 0;
+}
+
+static int host_frame_bytes(const uint8_t *p) {
+    if (p[0] != 0xFF || (p[1] & 0xFE) != 0xFA) return -1;
+    int bi = p[2] >> 4, si = (p[2] >> 2) & 3;
+    if (bi == 0 || bi == 15 || si == 3) return -1;
+    return 144000 * (int)MP3D_BITRATE_L3[bi] / (int)MP3D_SAMPLE_RATE[si] + ((p[2] >> 1) & 1);
+}
+
+extern "C" int mp3d_decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, int16_t *pcm,
+                                 mp3d_frame_info *info) {
+    if (!d || !buf) return MP3D_E_ARG;
+    mp3d_frame_info tmp;
+    if (!info) info = &tmp;
+    memset(info, 0, sizeof(*info));
+    size_t pos = 0;
+    if (d->frames == 0 && bytes >= 10 && buf[0] == 'I' && buf[1] == 'D' && buf[2] == '3') {
+        size_t sz = ((size_t)(buf[6] & 0x7F) << 21) | ((size_t)(buf[7] & 0x7F) << 14) | ((size_t)(buf[8] & 0x7F) << 7) |
+                    (buf[9] & 0x7F);
+        pos = 10 + sz + ((buf[5] & 0x10) ? 10 : 0);
+    }
+    int fb = -1;
+    while (pos + 4 <= bytes) {
+        fb = host_frame_bytes(buf + pos);
+        if (fb > 0) break;
+        pos++;
+    }
+    if (fb <= 0 || pos + (size_t)fb > bytes) {
+        info->frame_bytes = (int)std::min<size_t>(pos, bytes);
+        return info->frame_bytes ? 0 : MP3D_E_NEED_MORE;
+    }
+    uint64_t off = 0;
+    uint32_t sz = (uint32_t)fb;
+    int16_t out[2304];
+    mp3d_frame_info fi;
+    int r = mp3d_batch_decode(d->b, buf + pos, &off, &sz, 1, 1, out, &fi, nullptr);
+    if (r) return r;
+    d->frames++;
+    *info = fi;
+    info->frame_bytes = (int)pos + fi.frame_bytes;
+    if (fi.samples && pcm) memcpy(pcm, out, sizeof(int16_t) * 1152 * fi.channels);
+    return fi.samples;
+}
+
+/* ------------------------------------------------------------------------ */
+extern "C" const char *mp3d_strerror(int e) {
+    switch (e) {
+    case MP3D_OK: return "ok";
+    case MP3D_E_ARG: return "bad argument";
+    case MP3D_E_NO_DEVICE: return "no usable HIP device (MI355X required; no CPU fallback)";
+    case MP3D_E_HIP: return "HIP runtime error";
+    case MP3D_E_NOMEM: return "out of memory";
+    case MP3D_E_CAPACITY: return "batch exceeds handle capacity";
+    case MP3D_E_NEED_MORE: return "no complete frame in buffer";
+    default: return "unknown error";
+    }
+}
+extern "C" int mp3d_last_hip_error(void) { return g_last_hip; }
+extern "C" int mp3d_abi_version(void) { return MP3D_ABI_VERSION; }

@@ -1,0 +1,90 @@
+/*
+ * mp3d_internal.h -- device data layout shared by the HIP kernels
+ * (mp3d_kernels.hip) and the host library (mp3d_host.cpp).
+ *
+ * HBM layout of one batch (SoA, one process per GPU):
+ *   input   : caller's frame bytes, stream s at in_off[s] (u64), in_len[s]
+ *   rec     : FrameRec[n_streams * F]         (k_scan, 32 B per frame)
+ *   md      : per-stream main-data byte region (carry-in + payloads),
+ *             stream s at md_off[s] (16-B aligned), read as big-endian words
+ *   is_buf  : int16 [n_streams * F * 4][576]  (k_huffman -> k_synth)
+ *   meta    : UnitMeta[n_streams * F * 4]    (scalefactors + gains)
+ *   state   : StreamState[max_streams]        (reservoir, overlap, V FIFO)
+ *   pcm     : int16 [n_streams * F][1152 * 2] (interleaved L/R; mono: 1152)
+ * Unit index u = ((s * F + f) * 2 + gr) * 2 + ch.
+ */
+#ifndef MP3D_INTERNAL_H
+#define MP3D_INTERNAL_H
+
+#include <stdint.h>
+
+#define MP3D_RES_BYTES 512       /* carried main-data history per stream   */
+#define MP3D_FIFO_SLOTS 15       /* synthesis history slots carried        */
+#define MP3D_MAX_FRAME_BYTES 1441
+
+/* Per-frame record written by k_scan. */
+struct FrameRec {
+    uint64_t frame_off;  /* byte offset of the frame header in input        */
+    uint32_t md_bit;     /* bit offset of main-data start inside md region   */
+    uint32_t payload_md; /* byte offset of this frame's payload in md region */
+    uint16_t frame_bytes;/* 0: no frame (stream ended / invalid)             */
+    uint16_t payload_len;
+    uint8_t hdr1, hdr2, hdr3; /* header bytes 1..3                           */
+    uint8_t nch;
+    uint8_t side_off;    /* 4 or 6 (CRC)                                     */
+    uint8_t first_gr;    /* first decoded granule (reservoir underflow)      */
+    uint8_t sr_idx;
+    uint8_t pad_;
+};
+
+/* Per-unit side information + scalefactors, written by k_huffman. */
+struct __attribute__((aligned(8))) UnitMeta {
+    uint8_t sf[40];
+    uint8_t global_gain;
+    uint8_t block_type;  /* 0 unless window switching                      */
+    uint8_t mixed;
+    uint8_t scalefac_scale;
+    uint8_t preflag;
+    uint8_t sbg[3];
+    uint16_t nz_end;     /* lines produced by big_values + count1          */
+    uint16_t part2_3_length;
+    uint16_t used_bits;  /* bits consumed (== part2_3_length when valid)   */
+    uint16_t pad_;
+};
+
+/* Persistent per-stream decoder state. */
+struct StreamState {
+    uint8_t res[MP3D_RES_BYTES];           /* main-data carry (oldest first) */
+    int32_t res_len;                       /* bytes valid in res             */
+    int32_t frames;                        /* frames decoded so far          */
+    int32_t pad_[2];
+    float overlap[2][32][18];              /* IMDCT overlap                  */
+    float fifo[2][MP3D_FIFO_SLOTS][32];    /* last 15 matrixing outputs X    */
+};
+
+/* Huffman LUT layout (u32 entries, two levels, first level 8 bits or fewer).
+ * leaf:    bit31 = 0, bits 8..12 code length, bits 4..7 x, bits 0..3 y
+ * pointer: bit31 = 1, bits 16..20 sub-index bits, bits 0..15 absolute base */
+#define MP3D_LUT_TABLES 16 /* 15 big_values code tables + count1 table A   */
+#define MP3D_LUT_MAX 7168
+struct HuffLutHeader {
+    uint16_t base[MP3D_LUT_TABLES];
+    uint8_t bits1[MP3D_LUT_TABLES];
+};
+
+/* Constant tables uploaded once per batch (built on the host). */
+struct DevTables {
+    float pow43[8208];         /* |is|^(4/3), |is| <= 8206               */
+    float dct_c[32][32];       /* C[m][sb] = cos(m (2 sb + 1) pi / 64)  */
+    float dwin[32][16];        /* per output j: signed window taps       */
+    uint8_t long_sfb[3][576];  /* line -> long band                      */
+    uint16_t short_src[3][576];/* reordered line -> bitstream line       */
+    uint8_t bs_band[3][576];   /* bitstream line (short) -> short band   */
+    uint8_t bs_win[3][576];    /* bitstream line (short) -> window       */
+    uint8_t win_a[32];         /* V[j] = sgn * X[a[j]]                   */
+    uint8_t win_b[32];         /* V[32 + j] = sgn * X[b[j]]              */
+    uint32_t lut[MP3D_LUT_MAX];
+    struct HuffLutHeader lut_hdr;
+};
+
+#endif

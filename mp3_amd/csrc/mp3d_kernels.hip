@@ -1,0 +1,815 @@
+/*
+ * mp3d_kernels.hip -- MI355X (gfx950) kernels of the batched MPEG-1 Layer III
+ * decode hot path (ISO/IEC 11172-3 clause per
+ * kernel).  The reference (lxm0851/mp3) has no decoder source: its player's
+ * decode loop (REF/README.md:2-3) is the path these kernels replace.
+ *
+ * Pipeline for one batch call (all on one HIP stream, state resident in HBM):
+ *   k_scan     thread / stream  : header + side-info walk, bit-reservoir map
+ *   k_gather   block  / stream  : main-data bytes -> contiguous md region
+ *   k_huffman  thread / unit    : scalefactors + Huffman (LDS LUT) -> is[576]
+ *   k_synth    wave   / stream  : requantise, stereo, alias, IMDCT, overlap,
+ *                                 32-band matrixing + 512-tap window -> PCM
+ * A unit is one (frame, granule, channel).  Streams are independent, so the
+ * batch is embarrassingly parallel over streams; frames of one stream are
+ * walked in order inside k_scan / k_synth, which keep the per-stream state
+ * (reservoir, overlap, synthesis FIFO) in registers / LDS between frames.
+ */
+#include <hip/hip_runtime.h>
+
+#include "mp3d_internal.h"
+#include "mp3d_tables.h"
+
+namespace mp3d {
+
+/* ------------------------------------------------------------------------ */
+/* Constant-memory tables (uniform access -> scalar loads)                   */
+/* ------------------------------------------------------------------------ */
+__constant__ float c_imdct36[18][18]; /* [k][o]: o<9 -> out o, o>=9 -> out 18+(o-9) */
+__constant__ float c_imdct12[6][6];   /* [k][o]: o<3 -> out o, o>=3 -> out 6+(o-3)   */
+__constant__ float c_win36[4][36];
+__constant__ float c_win12[12];
+__constant__ float c_alias_cs[8];
+__constant__ float c_alias_ca[8];
+__constant__ float c_is_ratio[7][2];  /* MPEG-1 intensity: k/(1+k), 1/(1+k) */
+__constant__ float c_pow2q[4];        /* 2^(i/4) */
+
+struct DevInfo { /* mirrors mp3d_frame_info (include/mp3d.h) */
+    int32_t frame_bytes, channels, hz, layer, bitrate_kbps, samples;
+};
+
+#define REC_TAG 0x80 /* FrameRec.first_gr high bit: Xing/Info tag frame   */
+#define REC_DROP 0x40 /* invalid side info (big_values > 288): dropped      */
+
+/* ------------------------------------------------------------------------ */
+/* Header / side-info helpers (ISO 2.4.1.3, 2.4.1.7)                          */
+/* ------------------------------------------------------------------------ */
+__device__ __forceinline__ uint32_t ld_be32(const uint8_t *p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+/* bits [pos, pos+n) of a byte array, n <= 24 */
+__device__ __forceinline__ uint32_t bits_at(const uint8_t *p, uint32_t pos, int n) {
+    uint32_t w = ld_be32(p + (pos >> 3));
+    return (w << (pos & 7)) >> (32 - n);
+}
+
+__device__ __forceinline__ int hdr_frame_bytes(uint8_t b1, uint8_t b2) {
+    if ((b1 & 0xFE) != 0xFA) return -1;
+    int bi = b2 >> 4, si = (b2 >> 2) & 3;
+    if (bi == 0 || bi == 15 || si == 3) return -1;
+    return 144000 * (int)MP3D_BITRATE_L3[bi] / (int)MP3D_SAMPLE_RATE[si] + ((b2 >> 1) & 1);
+}
+
+/* bit offset of unit (gr, ch) inside the side info */
+__device__ __forceinline__ uint32_t side_unit_bit(int nch, int gr, int ch) {
+    return 9 + (nch == 1 ? 5 : 3) + 4 * nch + 59 * (gr * nch + ch);
+}
+
+/* ------------------------------------------------------------------------ */
+/* k_scan: one thread per stream.  Walks the stream's frames (ISO 2.4.1.3), */
+/* maps each frame's main data into the stream's md region (bit reservoir, */
+/* ISO 2.4.3.4 main_data_begin; FFmpeg's underflow rule), records results. */
+/* ------------------------------------------------------------------------ */
+__global__ void __launch_bounds__(256) k_scan(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
+                                              const uint32_t *__restrict__ in_len, StreamState *__restrict__ st,
+                                              FrameRec *__restrict__ rec, int32_t *__restrict__ carry,
+                                              DevInfo *__restrict__ infos, int n_streams, int F) {
+    int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n_streams) return;
+    const uint8_t *p0 = in + in_off[s];
+    uint32_t len = in_len[s];
+    uint32_t cur = 0;
+    const int carry_in = st[s].res_len;
+    const int stream_start = st[s].frames == 0;
+    uint32_t P = (uint32_t)carry_in; /* md position of the next payload         */
+    int avail = carry_in;            /* bytes after the previous main-data end */
+    if (stream_start && len >= 10 && p0[0] == 'I' && p0[1] == 'D' && p0[2] == '3') {
+        uint32_t sz = ((uint32_t)(p0[6] & 0x7F) << 21) | ((uint32_t)(p0[7] & 0x7F) << 14) |
+                      ((uint32_t)(p0[8] & 0x7F) << 7) | (p0[9] & 0x7F);
+        cur = 10 + sz + ((p0[5] & 0x10) ? 10 : 0);
+    }
+    int decoded = 0;
+    for (int f = 0; f < F; f++) {
+        FrameRec r;
+        r.frame_off = 0; r.md_bit = 0; r.payload_md = P; r.frame_bytes = 0; r.payload_len = 0;
+        r.hdr1 = r.hdr2 = r.hdr3 = 0; r.nch = 0; r.side_off = 4; r.first_gr = 0; r.sr_idx = 0; r.pad_ = 0;
+        DevInfo inf = {0, 0, 0, 0, 0, 0};
+        int fb = -1;
+        while (cur + 4 <= len) {
+            if (p0[cur] == 0xFF) {
+                fb = hdr_frame_bytes(p0[cur + 1], p0[cur + 2]);
+                if (fb > 0) break;
+            }
+            cur++;
+        }
+        if (fb > 0 && cur + (uint32_t)fb <= len) {
+            const uint8_t *fp = p0 + cur;
+            int nch = (fp[3] >> 6) == 3 ? 1 : 2;
+            int crc = (fp[1] & 1) ? 0 : 2;
+            int side_bytes = nch == 1 ? 17 : 32;
+            int plen = fb - 4 - crc - side_bytes;
+            const uint8_t *side = fp + 4 + crc;
+            r.frame_off = in_off[s] + cur;
+            r.frame_bytes = (uint16_t)fb;
+            r.payload_len = (uint16_t)(plen > 0 ? plen : 0);
+            r.hdr1 = fp[1]; r.hdr2 = fp[2]; r.hdr3 = fp[3];
+            r.nch = (uint8_t)nch;
+            r.side_off = (uint8_t)(4 + crc);
+            r.sr_idx = (uint8_t)((fp[2] >> 2) & 3);
+            inf.frame_bytes = fb; inf.channels = nch; inf.hz = (int)MP3D_SAMPLE_RATE[r.sr_idx];
+            inf.layer = 3; inf.bitrate_kbps = MP3D_BITRATE_L3[fp[2] >> 4];
+            const uint8_t *tg = side + side_bytes;
+            bool tag = stream_start && f == 0 && plen >= 4 &&
+                       ((tg[0] == 'X' && tg[1] == 'i' && tg[2] == 'n' && tg[3] == 'g') ||
+                        (tg[0] == 'I' && tg[1] == 'n' && tg[2] == 'f' && tg[3] == 'o'));
+            int mdb = (int)bits_at(side, 0, 9);
+            int p23[2][2] = {{0, 0}, {0, 0}};
+            bool bad = plen < 0;
+            for (int gr = 0; gr < 2; gr++)
+                for (int ch = 0; ch < nch; ch++) {
+                    uint32_t b = side_unit_bit(nch, gr, ch);
+                    p23[gr][ch] = (int)bits_at(side, b, 12);
+                    if (bits_at(side, b + 12, 9) > 288) bad = true; /* SURVEY A.9 (5) */
+                }
+            if (tag) {
+                r.first_gr = REC_TAG;
+            } else if (bad) {
+                /* FFmpeg drops the frame; its reservoir restarts from the frame tail */
+                r.first_gr = REC_DROP;
+                avail = plen > 0 ? (plen < MP3D_RES_BYTES ? plen : MP3D_RES_BYTES) : 0;
+                P += (uint32_t)r.payload_len;
+            } else {
+                int gr0 = 0;
+                uint32_t mdbit;
+                if (mdb <= avail) {
+                    mdbit = (P - (uint32_t)mdb) * 8u;
+                } else {
+                    uint32_t bits = (uint32_t)avail * 8u;
+                    while (gr0 < 2 && (int)(bits >> 3) < mdb) {
+                        for (int ch = 0; ch < nch; ch++) bits += (uint32_t)p23[gr0][ch];
+                        gr0++;
+                    }
+                    mdbit = (P - (uint32_t)avail) * 8u + bits - 8u * (uint32_t)mdb;
+                }
+                uint32_t end = mdbit;
+                for (int gr = gr0; gr < 2; gr++)
+                    for (int ch = 0; ch < nch; ch++) end += (uint32_t)p23[gr][ch];
+                r.md_bit = mdbit;
+                r.first_gr = (uint8_t)gr0;
+                P += (uint32_t)plen;
+                int64_t after = (int64_t)P - (int64_t)((end + 7u) >> 3);
+                avail = after < 0 ? 0 : (int)after;
+                inf.samples = 1152;
+                decoded++;
+            }
+            cur += (uint32_t)fb;
+        } else {
+            cur = len;
+        }
+        rec[(size_t)s * F + f] = r;
+        if (infos) infos[(size_t)s * F + f] = inf;
+    }
+    int c = avail < MP3D_RES_BYTES ? avail : MP3D_RES_BYTES;
+    if ((uint32_t)c > P) c = (int)P;
+    carry[2 * s] = c;
+    carry[2 * s + 1] = (int)P;
+    st[s].frames += decoded;
+}
+
+/* ------------------------------------------------------------------------ */
+/* k_gather: one block per stream.  md region = [carry-in][payload 0][...]  */
+/* then the last `carry` bytes become the next call's carry-in.             */
+/* ------------------------------------------------------------------------ */
+__global__ void __launch_bounds__(256) k_gather(const uint8_t *__restrict__ in, uint8_t *__restrict__ md,
+                                                const uint64_t *__restrict__ md_off, StreamState *__restrict__ st,
+                                                const FrameRec *__restrict__ rec, const int32_t *__restrict__ carry,
+                                                int F) {
+    int s = blockIdx.x;
+    uint8_t *dst = md + md_off[s];
+    const int cin = st[s].res_len;
+    for (int i = threadIdx.x; i < cin; i += blockDim.x) dst[i] = st[s].res[i];
+    for (int f = 0; f < F; f++) {
+        const FrameRec &r = rec[(size_t)s * F + f];
+        if (!r.frame_bytes || (r.first_gr & REC_TAG)) continue;
+        const uint8_t *src = in + r.frame_off + r.side_off + (r.nch == 1 ? 17 : 32);
+        uint8_t *d = dst + r.payload_md;
+        for (int i = threadIdx.x; i < r.payload_len; i += blockDim.x) d[i] = src[i];
+    }
+    __syncthreads();
+    const int cout = carry[2 * s], pend = carry[2 * s + 1];
+    for (int i = threadIdx.x; i < cout; i += blockDim.x) st[s].res[i] = dst[pend - cout + i];
+    if (threadIdx.x == 0) st[s].res_len = cout;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Bit reader over a big-endian byte region read as 32-bit words.           */
+/* ------------------------------------------------------------------------ */
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+struct BitReader {
+    const uint32_t *w;
+    uint32_t pos, cw, a, b;
+    __device__ __forceinline__ void seek(uint32_t p) {
+        pos = p;
+        cw = p >> 5;
+        a = bswap32(w[cw]);
+        b = bswap32(w[cw + 1]);
+    }
+    __device__ __forceinline__ uint32_t peek() const {
+        uint32_t sh = pos & 31;
+        return sh ? __builtin_amdgcn_alignbit(a, b, 32 - sh) : a;
+    }
+    __device__ __forceinline__ void skip(uint32_t n) {
+        pos += n;
+        uint32_t nw = pos >> 5;
+        if (nw != cw) {
+            if (nw == cw + 1) {
+                a = b;
+                b = bswap32(w[nw + 1]);
+            } else {
+                a = bswap32(w[nw]);
+                b = bswap32(w[nw + 1]);
+            }
+            cw = nw;
+        }
+    }
+    __device__ __forceinline__ uint32_t get(int n) { /* 0 <= n <= 24 */
+        uint32_t v = n ? peek() >> (32 - n) : 0u;
+        skip((uint32_t)n);
+        return v;
+    }
+};
+
+struct UnitSide {
+    int part2_3_length, big_values, global_gain, scalefac_compress, ws, block_type, mixed;
+    int table_select[3], sbg[3], region0_count, region1_count, preflag, scalefac_scale, c1sel;
+};
+
+__device__ __forceinline__ void parse_unit(const uint8_t *side, int nch, int gr, int ch, UnitSide &u) {
+    uint32_t b = side_unit_bit(nch, gr, ch);
+    u.part2_3_length = (int)bits_at(side, b, 12);
+    u.big_values = (int)bits_at(side, b + 12, 9);
+    u.global_gain = (int)bits_at(side, b + 21, 8);
+    u.scalefac_compress = (int)bits_at(side, b + 29, 4);
+    u.ws = (int)bits_at(side, b + 33, 1);
+    if (u.ws) {
+        u.block_type = (int)bits_at(side, b + 34, 2);
+        u.mixed = (int)bits_at(side, b + 36, 1);
+        u.table_select[0] = (int)bits_at(side, b + 37, 5);
+        u.table_select[1] = (int)bits_at(side, b + 42, 5);
+        u.table_select[2] = 0;
+        u.sbg[0] = (int)bits_at(side, b + 47, 3);
+        u.sbg[1] = (int)bits_at(side, b + 50, 3);
+        u.sbg[2] = (int)bits_at(side, b + 53, 3);
+        u.region0_count = u.region1_count = 0;
+    } else {
+        u.block_type = 0;
+        u.mixed = 0;
+        u.table_select[0] = (int)bits_at(side, b + 34, 5);
+        u.table_select[1] = (int)bits_at(side, b + 39, 5);
+        u.table_select[2] = (int)bits_at(side, b + 44, 5);
+        u.region0_count = (int)bits_at(side, b + 49, 4);
+        u.region1_count = (int)bits_at(side, b + 53, 3);
+        u.sbg[0] = u.sbg[1] = u.sbg[2] = 0;
+    }
+    u.preflag = (int)bits_at(side, b + 56, 1);
+    u.scalefac_scale = (int)bits_at(side, b + 57, 1);
+    u.c1sel = (int)bits_at(side, b + 58, 1);
+}
+
+/* Scalefactors (part 2), ISO 2.4.2.7; layout as UnitMeta.sf. */
+__device__ __forceinline__ void read_scalefactors(BitReader &br, const UnitSide &u, int scfsi, const uint8_t *sf0,
+                                                  uint8_t *sf) {
+    int slen1 = MP3D_SLEN[0][u.scalefac_compress], slen2 = MP3D_SLEN[1][u.scalefac_compress];
+    for (int i = 0; i < 40; i++) sf[i] = 0;
+    int j = 0;
+    if (u.ws && u.block_type == 2) {
+        int n = u.mixed ? 17 : 18;
+        for (int i = 0; i < n; i++) sf[j++] = (uint8_t)br.get(slen1);
+        for (int i = 0; i < 18; i++) sf[j++] = (uint8_t)br.get(slen2);
+    } else {
+        for (int k = 0; k < 4; k++) {
+            int n = k == 0 ? 6 : 5;
+            int slen = k < 2 ? slen1 : slen2;
+            if (scfsi & (8 >> k)) {
+                for (int i = 0; i < n; i++, j++) sf[j] = sf0[j];
+            } else {
+                for (int i = 0; i < n; i++) sf[j++] = (uint8_t)br.get(slen);
+            }
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* k_huffman: one thread per unit (ISO 2.4.2.7 + Annex B).  Two-level LUT   */
+/* for the 15 code tables + count1 table A staged in LDS once per block;    */
+/* grid-strided so the 27 KB LUT is loaded ~2k times, not once per 256 u.  */
+/* ------------------------------------------------------------------------ */
+#define HUFF_BLOCK 256
+__global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restrict__ in, const uint8_t *__restrict__ md,
+                                                        const uint64_t *__restrict__ md_off,
+                                                        const FrameRec *__restrict__ rec,
+                                                        const DevTables *__restrict__ tab, int16_t *__restrict__ is_buf,
+                                                        UnitMeta *__restrict__ meta, int n_units, int F) {
+    __shared__ uint32_t s_lut[MP3D_LUT_MAX];
+    __shared__ uint8_t s_sf[HUFF_BLOCK][40];
+    __shared__ uint8_t s_sf0[HUFF_BLOCK][40];
+    const int lut_n = tab->lut_hdr.base[MP3D_LUT_TABLES - 1] + (1 << tab->lut_hdr.bits1[MP3D_LUT_TABLES - 1]);
+    for (int i = threadIdx.x; i < lut_n; i += blockDim.x) s_lut[i] = tab->lut[i];
+    __syncthreads();
+    uint8_t *sf = s_sf[threadIdx.x];
+    uint8_t *sf0 = s_sf0[threadIdx.x];
+    for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < n_units; u += gridDim.x * blockDim.x) {
+        const int fr = u >> 2, gr = (u >> 1) & 1, ch = u & 1;
+        const FrameRec r = rec[fr];
+        if (!r.frame_bytes || (r.first_gr & (REC_TAG | REC_DROP)) || ch >= r.nch) continue;
+        const int s = fr / F;
+        const int nch = r.nch;
+        const uint8_t *side = in + r.frame_off + r.side_off;
+        UnitSide us;
+        parse_unit(side, nch, gr, ch, us);
+        int16_t *out = is_buf + (size_t)u * 576;
+        UnitMeta m;
+        const int first_gr = r.first_gr;
+        uint32_t start = r.md_bit;
+        for (int g = first_gr; g < 2; g++)
+            for (int c = 0; c < nch; c++)
+                if (g < gr || (g == gr && c < ch)) start += bits_at(side, side_unit_bit(nch, g, c), 12);
+        BitReader br;
+        br.w = (const uint32_t *)(md + md_off[s]);
+        int nz_end = 0;
+        uint32_t used = 0;
+        if (gr < first_gr) {
+            for (int i = 0; i < 40; i++) sf[i] = 0;
+        } else {
+            int scfsi = gr == 1 ? (int)bits_at(side, 9 + (nch == 1 ? 5 : 3) + 4 * ch, 4) : 0;
+            bool long_blk = !(us.ws && us.block_type == 2);
+            if (scfsi && long_blk && first_gr == 0) {
+                /* scfsi reuse: decode granule 0's scalefactors of this channel */
+                UnitSide u0;
+                parse_unit(side, nch, 0, ch, u0);
+                uint32_t s0 = r.md_bit;
+                for (int c = 0; c < ch; c++) s0 += bits_at(side, side_unit_bit(nch, 0, c), 12);
+                br.seek(s0);
+                read_scalefactors(br, u0, 0, sf0, sf0);
+            } else {
+                for (int i = 0; i < 40; i++) sf0[i] = 0;
+            }
+            br.seek(start);
+            read_scalefactors(br, us, long_blk ? scfsi : 0, sf0, sf);
+            /* big_values: region boundaries (ISO 2.4.2.7; FFmpeg clamp) */
+            const int bv2 = us.big_values * 2;
+            int r1, r2;
+            if (us.ws) {
+                r1 = 36;
+                r2 = 576;
+            } else {
+                int b1 = us.region0_count + 1, b2 = us.region0_count + us.region1_count + 2;
+                if (b2 > 22) b2 = 22;
+                r1 = 0;
+                for (int i = 0; i < b1; i++) r1 += MP3D_SFB_LONG_WIDTH[r.sr_idx][i];
+                r2 = 0;
+                for (int i = 0; i < b2; i++) r2 += MP3D_SFB_LONG_WIDTH[r.sr_idx][i];
+            }
+            r1 = r1 < bv2 ? r1 : bv2;
+            r2 = r2 < bv2 ? r2 : bv2;
+            int k = 0;
+            for (int reg = 0; reg < 3; reg++) {
+                const int end = reg == 0 ? r1 : reg == 1 ? r2 : bv2;
+                const int sel = us.table_select[reg];
+                const int t = MP3D_HTAB_OF_SELECT[sel];
+                const int lin = MP3D_LINBITS[sel];
+                if (t < 0) {
+                    for (; k < end; k += 2) *(uint32_t *)(out + k) = 0u;
+                    continue;
+                }
+                const uint32_t base = tab->lut_hdr.base[t];
+                const int b1 = tab->lut_hdr.bits1[t];
+                for (; k < end; k += 2) {
+                    uint32_t pk = br.peek();
+                    uint32_t e = s_lut[base + (pk >> (32 - b1))];
+                    if (e >> 31) {
+                        uint32_t nb = (e >> 16) & 31;
+                        e = s_lut[(e & 0xFFFFu) + ((pk << b1) >> (32 - nb))];
+                    }
+                    int x = (e >> 4) & 15, y = e & 15;
+                    br.skip((e >> 8) & 31);
+                    if (lin) {
+                        if (x == 15) x += (int)br.get(lin);
+                        if (x && br.get(1)) x = -x;
+                        if (y == 15) y += (int)br.get(lin);
+                        if (y && br.get(1)) y = -y;
+                    } else {
+                        /* no linbits: both sign bits are adjacent */
+                        int nsb = (x != 0) + (y != 0);
+                        uint32_t sb = br.get(nsb);
+                        if (y && (sb & 1)) y = -y;
+                        if (x && ((sb >> (y != 0)) & 1)) x = -x;
+                    }
+                    *(uint32_t *)(out + k) = (uint32_t)(uint16_t)x | ((uint32_t)(uint16_t)y << 16);
+                }
+            }
+            /* count1 quadruples until part2_3 end; a quadruple that overreads
+             * it is discarded (FFmpeg huffman_decode) */
+            const uint32_t end_bit = start + (uint32_t)us.part2_3_length;
+            const uint32_t qbase = tab->lut_hdr.base[MP3D_LUT_TABLES - 1];
+            const int qb1 = tab->lut_hdr.bits1[MP3D_LUT_TABLES - 1];
+            while (k <= 572 && br.pos < end_bit) {
+                const uint32_t save = br.pos;
+                uint32_t pk = br.peek();
+                int v, len;
+                if (us.c1sel) {
+                    v = 15 - (int)(pk >> 28);
+                    len = 4;
+                } else {
+                    uint32_t e = s_lut[qbase + (pk >> (32 - qb1))];
+                    v = e & 15;
+                    len = (e >> 8) & 31;
+                }
+                br.skip((uint32_t)len);
+                int q0 = (v >> 3) & 1, q1 = (v >> 2) & 1, q2 = (v >> 1) & 1, q3 = v & 1;
+                int ns = q0 + q1 + q2 + q3;
+                uint32_t sb = br.get(ns);
+                int bit = ns;
+                if (q0) { bit--; if ((sb >> bit) & 1) q0 = -1; }
+                if (q1) { bit--; if ((sb >> bit) & 1) q1 = -1; }
+                if (q2) { bit--; if ((sb >> bit) & 1) q2 = -1; }
+                if (q3) { bit--; if ((sb >> bit) & 1) q3 = -1; }
+                if (br.pos > end_bit) {
+                    br.seek(save);
+                    break;
+                }
+                *(uint2 *)(out + k) = make_uint2((uint32_t)(uint16_t)q0 | ((uint32_t)(uint16_t)q1 << 16),
+                                                 (uint32_t)(uint16_t)q2 | ((uint32_t)(uint16_t)q3 << 16));
+                k += 4;
+            }
+            nz_end = k;
+            used = br.pos - start;
+        }
+        /* rzero */
+        int k0 = nz_end;
+        for (; k0 < 576 && (k0 & 7); k0 += 2) *(uint32_t *)(out + k0) = 0u;
+        for (; k0 < 576; k0 += 8) *(uint4 *)(out + k0) = make_uint4(0, 0, 0, 0);
+        for (int i = 0; i < 40; i++) m.sf[i] = sf[i];
+        m.global_gain = (uint8_t)us.global_gain;
+        m.block_type = (uint8_t)(us.ws ? us.block_type : 0);
+        m.mixed = (uint8_t)(us.ws && us.block_type == 2 ? us.mixed : 0);
+        m.scalefac_scale = (uint8_t)us.scalefac_scale;
+        m.preflag = (uint8_t)us.preflag;
+        m.sbg[0] = (uint8_t)us.sbg[0];
+        m.sbg[1] = (uint8_t)us.sbg[1];
+        m.sbg[2] = (uint8_t)us.sbg[2];
+        m.nz_end = (uint16_t)nz_end;
+        m.part2_3_length = (uint16_t)(gr < first_gr ? 0 : us.part2_3_length);
+        m.used_bits = (uint16_t)used;
+        m.pad_ = (uint16_t)(gr < first_gr);
+        meta[u] = m;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* k_synth: one wave (64 lanes) per stream, frames in order.                */
+/*  Phase R, lane = (ch, sb): requantise (ISO 2.4.3.4), joint stereo, short */
+/*   reorder, alias reduction (lane shuffles), IMDCT 36 / 3x12 + window +   */
+/*   overlap (in registers) + frequency inversion -> S[ch][slot][sb] (LDS)  */
+/*  Phase S, lane = (ch, m): per slot, 32-point matrixing X = C.S (ISO Annex*/
+/*   A, as the 32x32 DCT-II half of N[64][32]), X ring in LDS, then lane   */
+/*   (ch, j) applies the 512-tap window D over 16 slots -> int16 PCM.      */
+/* Template SRC_XR: config-2 entry (spectra given as f32 xr, after stereo). */
+/* ------------------------------------------------------------------------ */
+__device__ __forceinline__ float exp2q(int q) { /* 2^(q/4) exactly rounded once */
+    return ldexpf(c_pow2q[q & 3], q >> 2);
+}
+
+template <bool SRC_XR>
+__global__ void __launch_bounds__(64) k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf,
+                                              const UnitMeta *__restrict__ meta, const float *__restrict__ xr_in,
+                                              const uint8_t *__restrict__ xr_bt, const uint8_t *__restrict__ xr_mixed,
+                                              const DevTables *__restrict__ tab, StreamState *__restrict__ st,
+                                              int16_t *__restrict__ pcm, int F, int xr_nch, int xr_sr) {
+    __shared__ float sS[2][18][32];
+    __shared__ float sB[2][576];
+    __shared__ float sX[2][32][32];
+    __shared__ UnitMeta sM[2];
+    const int s = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int ch = lane >> 5;
+    const int sb = lane & 31; /* Phase R: subband; Phase S: m / j */
+
+    /* constants in registers */
+    float C[32];
+#pragma unroll
+    for (int k = 0; k < 32; k++) C[k] = tab->dct_c[sb][k];
+    float Dw[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) Dw[i] = tab->dwin[sb][i];
+    const int wa = tab->win_a[sb], wb = tab->win_b[sb];
+
+    /* state in */
+    StreamState &S = st[s];
+    float ov[18];
+#pragma unroll
+    for (int i = 0; i < 18; i++) ov[i] = S.overlap[ch][sb][i];
+    for (int t = 0; t < MP3D_FIFO_SLOTS; t++) sX[ch][(t - MP3D_FIFO_SLOTS) & 31][sb] = S.fifo[ch][t][sb];
+    int pos = 0;
+    __syncthreads();
+
+    for (int f = 0; f < F; f++) {
+        int nch, sr, mode = 0, mext = 0;
+        size_t fr = (size_t)s * F + f;
+        if (SRC_XR) {
+            nch = xr_nch;
+            sr = xr_sr;
+        } else {
+            const FrameRec r = rec[fr];
+            if (!r.frame_bytes || (r.first_gr & (REC_TAG | REC_DROP))) continue;
+            nch = r.nch;
+            sr = r.sr_idx;
+            mode = r.hdr3 >> 6;
+            mext = (r.hdr3 >> 4) & 3;
+        }
+        const bool active = ch < nch;
+        int16_t *out = pcm + fr * 2304;
+        for (int gr = 0; gr < 2; gr++) {
+            const size_t u = (fr * 2 + gr) * 2 + ch;
+            int bt, mixed;
+            float x[18];
+            if (SRC_XR) {
+                const size_t ux = (fr * 2 + gr) * (size_t)nch + (active ? ch : 0);
+                bt = xr_bt[ux];
+                mixed = bt == 2 ? xr_mixed[ux] : 0;
+                const float *src = xr_in + ux * 576;
+#pragma unroll
+                for (int i = 0; i < 18; i++) {
+                    int rl = 18 * sb + i;
+                    int sl = (bt == 2 && !(mixed && rl < 36)) ? tab->short_src[sr][rl] : rl;
+                    x[i] = active ? src[sl] : 0.f;
+                }
+            } else {
+                if (lane < 2 * (int)(sizeof(UnitMeta) / 4)) {
+                    int c = lane / (sizeof(UnitMeta) / 4), wi = lane % (sizeof(UnitMeta) / 4);
+                    if (c < nch)
+                        ((uint32_t *)&sM[c])[wi] = ((const uint32_t *)&meta[(fr * 2 + gr) * 2 + c])[wi];
+                }
+                __syncthreads();
+                const UnitMeta &M = sM[active ? ch : 0];
+                bt = M.block_type;
+                mixed = M.mixed;
+                const int gain = (int)M.global_gain - 210;
+                const int shift = M.scalefac_scale + 1;
+                const int16_t *isrow = is_buf + u * 576;
+                /* requantise in bitstream order: lane (ch, sb) owns lines
+                 * 18 sb .. 18 sb + 17 (coalesced is[] reads).  nzmask: bit b
+                 * (long band b) / bit 22 + 13 w + b (short band b, window w)
+                 * set where this channel has a nonzero line (IS detection). */
+                uint64_t nzmask = 0;
+                int vv[18];
+                if (active) {
+                    const uint32_t *row32 = (const uint32_t *)(isrow + 18 * sb);
+#pragma unroll
+                    for (int i = 0; i < 9; i++) {
+                        uint32_t w2 = row32[i];
+                        vv[2 * i] = (int16_t)(w2 & 0xFFFFu);
+                        vv[2 * i + 1] = (int16_t)(w2 >> 16);
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 18; i++) vv[i] = 0;
+                }
+#pragma unroll
+                for (int i = 0; i < 18; i++) {
+                    const int l = 18 * sb + i;
+                    const bool sh = bt == 2 && !(mixed && l < 36);
+                    int q, band, w = 0;
+                    if (sh) {
+                        band = tab->bs_band[sr][l];
+                        w = tab->bs_win[sr][l];
+                        int k = mixed ? 8 + 3 * (band - 3) + w : 3 * band + w;
+                        q = gain - 8 * M.sbg[w] - (M.sf[k] << shift);
+                    } else {
+                        band = tab->long_sfb[sr][l];
+                        int pre = M.preflag ? MP3D_PRETAB[band] : 0;
+                        q = gain - ((M.sf[band] + pre) << shift);
+                    }
+                    const int v = vv[i];
+                    const int a = v < 0 ? -v : v;
+                    const float mag = tab->pow43[a] * exp2q(q);
+                    x[i] = v < 0 ? -mag : (v ? mag : 0.f);
+                    if (v) nzmask |= sh ? (1ull << (22 + 13 * w + band)) : (1ull << band);
+                }
+                /* joint stereo (ISO 2.4.3.4): MPEG-1 intensity + M/S, paired by
+                 * bitstream line; the right channel's block structure decides
+                 * the IS bands (FFmpeg compute_stereo) */
+                if (mode == 1 && nch == 2 && mext) {
+                    uint64_t rm = ch ? nzmask : 0ull;
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) rm |= __shfl_xor(rm, o);
+                    const UnitMeta &MR = sM[1];
+                    const float isq = 0.70710678118654752f;
+                    const bool short_nz = (rm >> 22) != 0ull;
+#pragma unroll
+                    for (int i = 0; i < 18; i++) {
+                        const float other = __shfl_xor(x[i], 32);
+                        const float lv = ch ? other : x[i], rv = ch ? x[i] : other;
+                        const int l = 18 * sb + i;
+                        bool do_is = false;
+                        int ipos = 7;
+                        if (mext & 1) {
+                            const bool shR = MR.block_type == 2 && !(MR.mixed && l < 36);
+                            if (shR) {
+                                const int band = tab->bs_band[sr][l], w = tab->bs_win[sr][l];
+                                const uint32_t wm = (uint32_t)(rm >> (22 + 13 * w)) & 0x1FFFu;
+                                const int kb = band == 12 ? 11 : band;
+                                ipos = MR.sf[MR.mixed ? 8 + 3 * (kb - 3) + w : 3 * kb + w];
+                                do_is = (wm >> band) == 0u && ipos < 7;
+                            } else {
+                                const int band = tab->long_sfb[sr][l];
+                                const uint32_t lm = (uint32_t)(rm & 0x3FFFFFull);
+                                ipos = MR.sf[band == 21 ? 20 : band];
+                                do_is = !short_nz && (lm >> band) == 0u && ipos < 7;
+                            }
+                        }
+                        if (do_is) x[i] = lv * c_is_ratio[ipos][ch];
+                        else if (mext & 2) x[i] = ch ? (lv - rv) * isq : (lv + rv) * isq;
+                    }
+                }
+                /* short-block reorder through LDS (window-grouped bands ->
+                 * (freq, window) interleave), only where this channel is short */
+                if (bt == 2) {
+#pragma unroll
+                    for (int i = 0; i < 18; i++) sB[ch][18 * sb + i] = x[i];
+                }
+                __syncthreads();
+                if (bt == 2) {
+#pragma unroll
+                    for (int i = 0; i < 18; i++) {
+                        const int rl = 18 * sb + i;
+                        x[i] = (mixed && rl < 36) ? x[i] : sB[ch][tab->short_src[sr][rl]];
+                    }
+                }
+            }
+            /* alias reduction (ISO 2.4.3.4): butterflies across the 31 subband
+             * boundaries (long), the first one only (mixed), none (short) */
+            {
+                const bool upper = active && ((bt != 2 && sb >= 1) || (bt == 2 && mixed && sb == 1));
+                const bool lower = active && ((bt != 2 && sb <= 30) || (bt == 2 && mixed && sb == 0));
+                float up[8], dn[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    up[k] = __shfl_up(x[17 - k], 1); /* lane sb-1's x[17-k] */
+                    dn[k] = __shfl_down(x[k], 1);    /* lane sb+1's x[k]    */
+                }
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    float lo = x[17 - k], hi = x[k];
+                    if (upper) x[k] = hi * c_alias_cs[k] + up[k] * c_alias_ca[k];
+                    if (lower) x[17 - k] = lo * c_alias_cs[k] - dn[k] * c_alias_ca[k];
+                }
+            }
+            /* IMDCT + window + overlap-add + frequency inversion */
+            {
+                float z[36];
+                const bool long_imdct = bt != 2 || (mixed && sb < 2);
+                if (long_imdct) {
+                    const int wt = (bt == 2) ? 0 : bt;
+                    float h[18];
+#pragma unroll
+                    for (int o = 0; o < 18; o++) {
+                        float acc = 0.f;
+#pragma unroll
+                        for (int k = 0; k < 18; k++) acc = fmaf(x[k], c_imdct36[k][o], acc);
+                        h[o] = acc;
+                    }
+#pragma unroll
+                    for (int i = 0; i < 9; i++) {
+                        z[i] = h[i];
+                        z[17 - i] = -h[i];
+                        z[18 + i] = h[9 + i];
+                        z[35 - i] = h[9 + i];
+                    }
+#pragma unroll
+                    for (int i = 0; i < 36; i++) z[i] *= c_win36[wt][i];
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 36; i++) z[i] = 0.f;
+#pragma unroll
+                    for (int w = 0; w < 3; w++) {
+                        float h[6];
+#pragma unroll
+                        for (int o = 0; o < 6; o++) {
+                            float acc = 0.f;
+#pragma unroll
+                            for (int k = 0; k < 6; k++) acc = fmaf(x[3 * k + w], c_imdct12[k][o], acc);
+                            h[o] = acc;
+                        }
+                        float y[12];
+#pragma unroll
+                        for (int i = 0; i < 3; i++) {
+                            y[i] = h[i];
+                            y[5 - i] = -h[i];
+                            y[6 + i] = h[3 + i];
+                            y[11 - i] = h[3 + i];
+                        }
+#pragma unroll
+                        for (int i = 0; i < 12; i++) z[6 * w + 6 + i] += y[i] * c_win12[i];
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < 18; i++) {
+                    float v = z[i] + ov[i];
+                    ov[i] = active ? z[18 + i] : ov[i];
+                    if ((sb & 1) && (i & 1)) v = -v;
+                    sS[ch][i][sb] = v;
+                }
+            }
+            __syncthreads();
+            /* Phase S: matrixing + windowing, 18 slots */
+            for (int t = 0; t < 18; t++) {
+                const float4 *row = (const float4 *)&sS[ch][t][0];
+                float acc = 0.f;
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    float4 v4 = row[q];
+                    acc = fmaf(C[4 * q + 0], v4.x, acc);
+                    acc = fmaf(C[4 * q + 1], v4.y, acc);
+                    acc = fmaf(C[4 * q + 2], v4.z, acc);
+                    acc = fmaf(C[4 * q + 3], v4.w, acc);
+                }
+                const int cur = (pos + t) & 31;
+                sX[ch][cur][sb] = acc;
+                __syncthreads();
+                float o = 0.f;
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    o = fmaf(Dw[2 * i], sX[ch][(cur - 2 * i) & 31][wa], o);
+                    o = fmaf(Dw[2 * i + 1], sX[ch][(cur - 2 * i - 1) & 31][wb], o);
+                }
+                if (active) {
+                    float pv = rintf(o * 32768.f);
+                    pv = fminf(fmaxf(pv, -32768.f), 32767.f);
+                    out[(gr * 576 + t * 32 + sb) * nch + ch] = (int16_t)pv;
+                }
+            }
+            pos = (pos + 18) & 31;
+            __syncthreads();
+        }
+    }
+    /* state out */
+#pragma unroll
+    for (int i = 0; i < 18; i++) S.overlap[ch][sb][i] = ov[i];
+    for (int t = 0; t < MP3D_FIFO_SLOTS; t++) S.fifo[ch][t][sb] = sX[ch][(pos - MP3D_FIFO_SLOTS + t) & 31][sb];
+}
+
+/* ------------------------------------------------------------------------ */
+/* Host-side launchers                                                       */
+/* ------------------------------------------------------------------------ */
+hipError_t upload_constants(const float *imdct36, const float *imdct12, const float *win36, const float *win12,
+                            const float *alias_cs, const float *alias_ca, const float *is_ratio, const float *pow2q) {
+    hipError_t e;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_imdct36), imdct36, sizeof(float) * 18 * 18))) return e;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_imdct12), imdct12, sizeof(float) * 6 * 6))) return e;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_win36), win36, sizeof(float) * 4 * 36))) return e;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_win12), win12, sizeof(float) * 12))) return e;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_alias_cs), alias_cs, sizeof(float) * 8))) return e;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_alias_ca), alias_ca, sizeof(float) * 8))) return e;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_is_ratio), is_ratio, sizeof(float) * 14))) return e;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_pow2q), pow2q, sizeof(float) * 4))) return e;
+    return hipSuccess;
+}
+
+void launch_scan(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len, StreamState *st, FrameRec *rec,
+                 int32_t *carry, void *infos, int n_streams, int F, hipStream_t strm) {
+    hipLaunchKernelGGL(k_scan, dim3((n_streams + 255) / 256), dim3(256), 0, strm, in, in_off, in_len, st, rec, carry,
+                       (DevInfo *)infos, n_streams, F);
+}
+
+void launch_gather(const uint8_t *in, uint8_t *md, const uint64_t *md_off, StreamState *st, const FrameRec *rec,
+                   const int32_t *carry, int n_streams, int F, hipStream_t strm) {
+    hipLaunchKernelGGL(k_gather, dim3(n_streams), dim3(256), 0, strm, in, md, md_off, st, rec, carry, F);
+}
+
+void launch_huffman(const uint8_t *in, const uint8_t *md, const uint64_t *md_off, const FrameRec *rec,
+                    const DevTables *tab, int16_t *is_buf, UnitMeta *meta, int n_streams, int F, int n_cu,
+                    hipStream_t strm) {
+    int n_units = n_streams * F * 4;
+    int blocks = (n_units + HUFF_BLOCK - 1) / HUFF_BLOCK;
+    int cap = n_cu * 8;
+    if (blocks > cap) blocks = cap;
+    hipLaunchKernelGGL(k_huffman, dim3(blocks), dim3(HUFF_BLOCK), 0, strm, in, md, md_off, rec, tab, is_buf, meta,
+                       n_units, F);
+}
+
+void launch_synth(const FrameRec *rec, const int16_t *is_buf, const UnitMeta *meta, const DevTables *tab,
+                  StreamState *st, int16_t *pcm, int n_streams, int F, hipStream_t strm) {
+    hipLaunchKernelGGL(k_synth<false>, dim3(n_streams), dim3(64), 0, strm, rec, is_buf, meta, (const float *)nullptr,
+                       (const uint8_t *)nullptr, (const uint8_t *)nullptr, tab, st, pcm, F, 2, 0);
+}
+
+void launch_synth_xr(const float *xr, const uint8_t *bt, const uint8_t *mixed, const DevTables *tab, StreamState *st,
+                     int16_t *pcm, int n_streams, int F, int nch, int sr, hipStream_t strm) {
+    hipLaunchKernelGGL(k_synth<true>, dim3(n_streams), dim3(64), 0, strm, (const FrameRec *)nullptr,
+                       (const int16_t *)nullptr, (const UnitMeta *)nullptr, xr, bt, mixed, tab, st, pcm, F, nch, sr);
+}
+
+} // namespace mp3d

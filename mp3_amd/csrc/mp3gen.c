@@ -426,7 +426,11 @@ GEN_API long mp3gen_stream(const gen_cfg *cfg, uint64_t seed, int n_frames, uint
             for (int gr = 0; gr < 2; gr++)
                 for (int ch = 0; ch < nch; ch++) if (U[gr][ch].part2_3_length > 4095) bad = 1;
             if (!bad && used >= 1 && lo <= hi && total_bits <= target + 400) unit_bytes_ok = 1;
-            else scale *= 0.8;
+            else {
+                /* shrink toward the target in proportion to the overshoot */
+                double ratio = total_bits > 0 ? 0.95 * (double)target / (double)total_bits : 0.5;
+                scale *= ratio < 0.8 ? (ratio > 0.1 ? ratio : 0.1) : 0.8;
+            }
         }
         if (!unit_bytes_ok) { /* fall back to silence units */
             total_bits = 0;

@@ -8,3 +8,7 @@ sys.path.insert(0, str(HERE.parent))
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box via gpurun)")
+
+
+def pytest_collection_modifyitems(config, items):
+    pass
