@@ -52,8 +52,9 @@ static thread_local int g_last_hip = 0;
 /* ------------------------------------------------------------------------ */
 static void build_huffman_lut(DevTables &t) {
     /* two-level LUT: first level min(8, maxlen) bits; codes longer than that
-     * go through one sub-table per 8-bit prefix (see mp3d_internal.h) */
-    std::vector<uint32_t> lut;
+     * go through one sub-table per first-level prefix (mp3d_internal.h) */
+    std::vector<uint16_t> lut;
+    const uint16_t UNUSED = 0xFFFF;
     for (int ti = 0; ti < MP3D_LUT_TABLES; ti++) {
         std::vector<uint32_t> code, len, val;
         if (ti < MP3D_NUM_HTABS) {
@@ -73,35 +74,41 @@ static void build_huffman_lut(DevTables &t) {
         }
         uint32_t maxlen = *std::max_element(len.begin(), len.end());
         int b1 = (int)std::min<uint32_t>(8, maxlen);
+        if (lut.size() & 1) lut.push_back(UNUSED);
         size_t base = lut.size();
         t.lut_hdr.base[ti] = (uint16_t)base;
         t.lut_hdr.bits1[ti] = (uint8_t)b1;
-        lut.resize(base + (1u << b1), 0xFFFFFFFFu);
-        /* sub-table depth per prefix */
+        lut.resize(base + (1u << b1), UNUSED);
         std::vector<int> subbits(1u << b1, 0);
         for (size_t i = 0; i < code.size(); i++)
             if ((int)len[i] > b1) {
                 uint32_t p = code[i] >> (len[i] - b1);
                 subbits[p] = std::max(subbits[p], (int)len[i] - b1);
             }
+        std::vector<size_t> subbase(1u << b1, 0);
         for (uint32_t p = 0; p < (1u << b1); p++)
             if (subbits[p]) {
-                size_t sb = lut.size();
-                lut.resize(sb + (1u << subbits[p]), 0xFFFFFFFFu);
-                lut[base + p] = 0x80000000u | ((uint32_t)subbits[p] << 16) | (uint32_t)sb;
+                if (lut.size() & 1) lut.push_back(UNUSED);
+                size_t rel = lut.size() - base;
+                if (rel / 2 > 0x7FF || subbits[p] > 15) {
+                    fprintf(stderr, "mp3d: LUT pointer overflow\n");
+                    abort();
+                }
+                subbase[p] = lut.size();
+                lut.resize(lut.size() + (1u << subbits[p]), UNUSED);
+                lut[base + p] = (uint16_t)(0x8000u | ((uint32_t)subbits[p] << 11) | (uint32_t)(rel / 2));
             }
         for (size_t i = 0; i < code.size(); i++) {
-            uint32_t leaf = (len[i] << 8) | val[i];
+            uint16_t leaf = (uint16_t)((len[i] << 8) | val[i]);
             if ((int)len[i] <= b1) {
                 uint32_t first = code[i] << (b1 - len[i]), cnt = 1u << (b1 - len[i]);
                 for (uint32_t k = 0; k < cnt; k++) lut[base + first + k] = leaf;
             } else {
                 uint32_t p = code[i] >> (len[i] - b1);
-                uint32_t ptr = lut[base + p];
-                int nb = (int)((ptr >> 16) & 31);
+                int nb = subbits[p];
                 uint32_t rest = code[i] & ((1u << (len[i] - b1)) - 1);
                 uint32_t first = rest << (nb - (len[i] - b1)), cnt = 1u << (nb - (len[i] - b1));
-                for (uint32_t k = 0; k < cnt; k++) lut[(ptr & 0xFFFF) + first + k] = leaf;
+                for (uint32_t k = 0; k < cnt; k++) lut[subbase[p] + first + k] = leaf;
             }
         }
     }
@@ -109,7 +116,7 @@ static void build_huffman_lut(DevTables &t) {
         fprintf(stderr, "mp3d: LUT overflow %zu\n", lut.size());
         abort();
     }
-    for (size_t i = 0; i < lut.size(); i++) t.lut[i] = lut[i] == 0xFFFFFFFFu ? (1u << 8) : lut[i];
+    for (size_t i = 0; i < lut.size(); i++) t.lut[i] = lut[i] == UNUSED ? (uint16_t)(1u << 8) : lut[i];
 }
 
 static void build_tables(DevTables &t) {
@@ -150,6 +157,17 @@ static void build_tables(DevTables &t) {
             }
             p += 3 * w;
         }
+    }
+    for (int k = 0; k < 18; k++)
+        for (int o = 0; o < 18; o++) {
+            int i = o < 9 ? o : 18 + (o - 9);
+            t.imdct36[k][o] = (float)cos(M_PI / 72.0 * (2 * i + 19) * (2 * k + 1));
+        }
+    for (int i = 0; i < 36; i++) {
+        t.win36[0][i] = (float)sin(M_PI / 36.0 * (i + 0.5));
+        t.win36[1][i] = (float)(i < 18 ? sin(M_PI / 36.0 * (i + 0.5)) : i < 24 ? 1.0 : i < 30 ? sin(M_PI / 12.0 * (i - 18 + 0.5)) : 0.0);
+        t.win36[3][i] = (float)(i < 6 ? 0.0 : i < 12 ? sin(M_PI / 12.0 * (i - 6 + 0.5)) : i < 18 ? 1.0 : sin(M_PI / 36.0 * (i + 0.5)));
+        t.win36[2][i] = t.win36[0][i];
     }
     build_huffman_lut(t);
 }

@@ -62,9 +62,10 @@ struct StreamState {
     float fifo[2][MP3D_FIFO_SLOTS][32];    /* last 15 matrixing outputs X    */
 };
 
-/* Huffman LUT layout (u32 entries, two levels, first level 8 bits or fewer).
- * leaf:    bit31 = 0, bits 8..12 code length, bits 4..7 x, bits 0..3 y
- * pointer: bit31 = 1, bits 16..20 sub-index bits, bits 0..15 absolute base */
+/* Huffman LUT layout (u16 entries, two levels, first level <= 8 bits):
+ * leaf:    bit15 = 0, bits 8..12 code length, bits 4..7 x, bits 0..3 y
+ * pointer: bit15 = 1, bits 11..14 sub-index bits, bits 0..10 sub-table
+ *          offset / 2 relative to the table's first-level base          */
 #define MP3D_LUT_TABLES 16 /* 15 big_values code tables + count1 table A   */
 #define MP3D_LUT_MAX 7168
 struct HuffLutHeader {
@@ -76,6 +77,8 @@ struct HuffLutHeader {
 struct DevTables {
     float pow43[8208];         /* |is|^(4/3), |is| <= 8206               */
     float dct_c[32][32];       /* C[m][sb] = cos(m (2 sb + 1) pi / 64)  */
+    float imdct36[18][20];     /* [k][o] 36-point IMDCT, 18 unique outs */
+    float win36[4][36];        /* long / start / (unused) / stop windows */
     float dwin[32][16];        /* per output j: signed window taps       */
     uint8_t long_sfb[3][576];  /* line -> long band                      */
     uint16_t short_src[3][576];/* reordered line -> bitstream line       */
@@ -83,7 +86,7 @@ struct DevTables {
     uint8_t bs_win[3][576];    /* bitstream line (short) -> window       */
     uint8_t win_a[32];         /* V[j] = sgn * X[a[j]]                   */
     uint8_t win_b[32];         /* V[32 + j] = sgn * X[b[j]]              */
-    uint32_t lut[MP3D_LUT_MAX];
+    uint16_t lut[MP3D_LUT_MAX];
     struct HuffLutHeader lut_hdr;
 };
 

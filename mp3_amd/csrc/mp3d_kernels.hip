@@ -208,13 +208,16 @@ __global__ void __launch_bounds__(256) k_gather(const uint8_t *__restrict__ in, 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
 struct BitReader {
+    /* 96-bit window a:b:c of big-endian words; c is prefetched one word
+     * ahead so a refill's load latency hides behind ~32 bits of decode */
     const uint32_t *w;
-    uint32_t pos, cw, a, b;
+    uint32_t pos, cw, a, b, c;
     __device__ __forceinline__ void seek(uint32_t p) {
         pos = p;
         cw = p >> 5;
         a = bswap32(w[cw]);
         b = bswap32(w[cw + 1]);
+        c = bswap32(w[cw + 2]);
     }
     __device__ __forceinline__ uint32_t peek() const {
         uint32_t sh = pos & 31;
@@ -226,10 +229,12 @@ struct BitReader {
         if (nw != cw) {
             if (nw == cw + 1) {
                 a = b;
-                b = bswap32(w[nw + 1]);
+                b = c;
+                c = bswap32(w[nw + 2]);
             } else {
-                a = bswap32(w[nw]);
+                a = nw == cw + 2 ? c : bswap32(w[nw]);
                 b = bswap32(w[nw + 1]);
+                c = bswap32(w[nw + 2]);
             }
             cw = nw;
         }
@@ -278,33 +283,67 @@ __device__ __forceinline__ void parse_unit(const uint8_t *side, int nch, int gr,
     u.c1sel = (int)bits_at(side, b + 58, 1);
 }
 
-/* Scalefactors (part 2), ISO 2.4.2.7; layout as UnitMeta.sf. */
-__device__ __forceinline__ void read_scalefactors(BitReader &br, const UnitSide &u, int scfsi, const uint8_t *sf0,
-                                                  uint8_t *sf) {
+/* Scalefactors (part 2), ISO 2.4.2.7, read in place: bands whose scfsi bit
+ * is set keep the granule-0 values already in sf (layout as UnitMeta.sf). */
+__device__ __forceinline__ void read_scalefactors(BitReader &br, const UnitSide &u, int scfsi, uint8_t *sf) {
     int slen1 = MP3D_SLEN[0][u.scalefac_compress], slen2 = MP3D_SLEN[1][u.scalefac_compress];
-    for (int i = 0; i < 40; i++) sf[i] = 0;
     int j = 0;
     if (u.ws && u.block_type == 2) {
         int n = u.mixed ? 17 : 18;
         for (int i = 0; i < n; i++) sf[j++] = (uint8_t)br.get(slen1);
         for (int i = 0; i < 18; i++) sf[j++] = (uint8_t)br.get(slen2);
+        for (; j < 40; j++) sf[j] = 0;
     } else {
         for (int k = 0; k < 4; k++) {
             int n = k == 0 ? 6 : 5;
             int slen = k < 2 ? slen1 : slen2;
             if (scfsi & (8 >> k)) {
-                for (int i = 0; i < n; i++, j++) sf[j] = sf0[j];
+                j += n;
             } else {
                 for (int i = 0; i < n; i++) sf[j++] = (uint8_t)br.get(slen);
             }
         }
+        for (; j < 40; j++) sf[j] = 0;
     }
 }
 
+/* is[] row writer: words (2 x int16) are shifted through 4 registers and
+ * stored 16 B at a time (one dwordx4 per 8 lines instead of 4 dword stores) */
+struct RowWriter {
+    int16_t *out;
+    uint32_t w0, w1, w2, w3;
+    int nw; /* words pushed */
+    __device__ __forceinline__ void push(uint32_t v) {
+        w0 = w1;
+        w1 = w2;
+        w2 = w3;
+        w3 = v;
+        nw++;
+        if ((nw & 3) == 0) *(uint4 *)(out + 2 * (nw - 4)) = make_uint4(w0, w1, w2, w3);
+    }
+    __device__ __forceinline__ void finish() { /* flush + rzero to 576 lines */
+        int r = nw & 3, k = 2 * (nw - r);
+        if (r == 3) {
+            *(uint32_t *)(out + k) = w1;
+            *(uint32_t *)(out + k + 2) = w2;
+            *(uint32_t *)(out + k + 4) = w3;
+            *(uint32_t *)(out + k + 6) = 0u;
+        } else if (r == 2) {
+            *(uint2 *)(out + k) = make_uint2(w2, w3);
+            *(uint2 *)(out + k + 4) = make_uint2(0u, 0u);
+        } else if (r == 1) {
+            *(uint32_t *)(out + k) = w3;
+            *(uint32_t *)(out + k + 2) = 0u;
+            *(uint2 *)(out + k + 4) = make_uint2(0u, 0u);
+        }
+        for (int kk = k + (r ? 8 : 0); kk < 576; kk += 8) *(uint4 *)(out + kk) = make_uint4(0, 0, 0, 0);
+    }
+};
+
 /* ------------------------------------------------------------------------ */
-/* k_huffman: one thread per unit (ISO 2.4.2.7 + Annex B).  Two-level LUT   */
-/* for the 15 code tables + count1 table A staged in LDS once per block;    */
-/* grid-strided so the 27 KB LUT is loaded ~2k times, not once per 256 u.  */
+/* k_huffman: one thread per unit (ISO 2.4.2.7 + Annex B).  Two-level u16   */
+/* LUT (15 code tables + count1 table A, 14 KB) staged in LDS once per     */
+/* block; grid-strided so it is loaded ~2k times per call, not per 256 u. */
 /* ------------------------------------------------------------------------ */
 #define HUFF_BLOCK 256
 __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restrict__ in, const uint8_t *__restrict__ md,
@@ -312,14 +351,13 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                                                         const FrameRec *__restrict__ rec,
                                                         const DevTables *__restrict__ tab, int16_t *__restrict__ is_buf,
                                                         UnitMeta *__restrict__ meta, int n_units, int F) {
-    __shared__ uint32_t s_lut[MP3D_LUT_MAX];
+    __shared__ uint16_t s_lut[MP3D_LUT_MAX];
     __shared__ uint8_t s_sf[HUFF_BLOCK][40];
-    __shared__ uint8_t s_sf0[HUFF_BLOCK][40];
     const int lut_n = tab->lut_hdr.base[MP3D_LUT_TABLES - 1] + (1 << tab->lut_hdr.bits1[MP3D_LUT_TABLES - 1]);
-    for (int i = threadIdx.x; i < lut_n; i += blockDim.x) s_lut[i] = tab->lut[i];
+    for (int i = threadIdx.x; i < (lut_n + 1) / 2; i += blockDim.x)
+        ((uint32_t *)s_lut)[i] = ((const uint32_t *)tab->lut)[i];
     __syncthreads();
     uint8_t *sf = s_sf[threadIdx.x];
-    uint8_t *sf0 = s_sf0[threadIdx.x];
     for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < n_units; u += gridDim.x * blockDim.x) {
         const int fr = u >> 2, gr = (u >> 1) & 1, ch = u & 1;
         const FrameRec r = rec[fr];
@@ -329,8 +367,10 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
         const uint8_t *side = in + r.frame_off + r.side_off;
         UnitSide us;
         parse_unit(side, nch, gr, ch, us);
-        int16_t *out = is_buf + (size_t)u * 576;
-        UnitMeta m;
+        RowWriter rw;
+        rw.out = is_buf + (size_t)u * 576;
+        rw.nw = 0;
+        rw.w0 = rw.w1 = rw.w2 = rw.w3 = 0u;
         const int first_gr = r.first_gr;
         uint32_t start = r.md_bit;
         for (int g = first_gr; g < 2; g++)
@@ -338,26 +378,27 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                 if (g < gr || (g == gr && c < ch)) start += bits_at(side, side_unit_bit(nch, g, c), 12);
         BitReader br;
         br.w = (const uint32_t *)(md + md_off[s]);
-        int nz_end = 0;
         uint32_t used = 0;
         if (gr < first_gr) {
             for (int i = 0; i < 40; i++) sf[i] = 0;
         } else {
             int scfsi = gr == 1 ? (int)bits_at(side, 9 + (nch == 1 ? 5 : 3) + 4 * ch, 4) : 0;
-            bool long_blk = !(us.ws && us.block_type == 2);
-            if (scfsi && long_blk && first_gr == 0) {
-                /* scfsi reuse: decode granule 0's scalefactors of this channel */
+            const bool long_blk = !(us.ws && us.block_type == 2);
+            if (!long_blk) scfsi = 0;
+            if (scfsi && first_gr == 0) {
+                /* scfsi reuse: decode granule 0's scalefactors of this channel
+                 * into sf first, then read granule 1's over them in place */
                 UnitSide u0;
                 parse_unit(side, nch, 0, ch, u0);
                 uint32_t s0 = r.md_bit;
                 for (int c = 0; c < ch; c++) s0 += bits_at(side, side_unit_bit(nch, 0, c), 12);
                 br.seek(s0);
-                read_scalefactors(br, u0, 0, sf0, sf0);
-            } else {
-                for (int i = 0; i < 40; i++) sf0[i] = 0;
+                read_scalefactors(br, u0, 0, sf);
+            } else if (scfsi) {
+                for (int i = 0; i < 40; i++) sf[i] = 0;
             }
             br.seek(start);
-            read_scalefactors(br, us, long_blk ? scfsi : 0, sf0, sf);
+            read_scalefactors(br, us, scfsi, sf);
             /* big_values: region boundaries (ISO 2.4.2.7; FFmpeg clamp) */
             const int bv2 = us.big_values * 2;
             int r1, r2;
@@ -381,20 +422,20 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                 const int t = MP3D_HTAB_OF_SELECT[sel];
                 const int lin = MP3D_LINBITS[sel];
                 if (t < 0) {
-                    for (; k < end; k += 2) *(uint32_t *)(out + k) = 0u;
+                    for (; k < end; k += 2) rw.push(0u);
                     continue;
                 }
                 const uint32_t base = tab->lut_hdr.base[t];
                 const int b1 = tab->lut_hdr.bits1[t];
                 for (; k < end; k += 2) {
-                    uint32_t pk = br.peek();
+                    const uint32_t pk = br.peek();
                     uint32_t e = s_lut[base + (pk >> (32 - b1))];
-                    if (e >> 31) {
-                        uint32_t nb = (e >> 16) & 31;
-                        e = s_lut[(e & 0xFFFFu) + ((pk << b1) >> (32 - nb))];
+                    if (e & 0x8000u) {
+                        const uint32_t nb = (e >> 11) & 15u;
+                        e = s_lut[base + ((e & 0x7FFu) << 1) + ((pk << b1) >> (32 - nb))];
                     }
                     int x = (e >> 4) & 15, y = e & 15;
-                    br.skip((e >> 8) & 31);
+                    br.skip((e >> 8) & 31u);
                     if (lin) {
                         if (x == 15) x += (int)br.get(lin);
                         if (x && br.get(1)) x = -x;
@@ -402,12 +443,12 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                         if (y && br.get(1)) y = -y;
                     } else {
                         /* no linbits: both sign bits are adjacent */
-                        int nsb = (x != 0) + (y != 0);
-                        uint32_t sb = br.get(nsb);
+                        const int nsb = (x != 0) + (y != 0);
+                        const uint32_t sb = br.get(nsb);
                         if (y && (sb & 1)) y = -y;
                         if (x && ((sb >> (y != 0)) & 1)) x = -x;
                     }
-                    *(uint32_t *)(out + k) = (uint32_t)(uint16_t)x | ((uint32_t)(uint16_t)y << 16);
+                    rw.push((uint32_t)(uint16_t)x | ((uint32_t)(uint16_t)y << 16));
                 }
             }
             /* count1 quadruples until part2_3 end; a quadruple that overreads
@@ -417,41 +458,39 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
             const int qb1 = tab->lut_hdr.bits1[MP3D_LUT_TABLES - 1];
             while (k <= 572 && br.pos < end_bit) {
                 const uint32_t save = br.pos;
-                uint32_t pk = br.peek();
+                const uint32_t pk = br.peek();
                 int v, len;
                 if (us.c1sel) {
                     v = 15 - (int)(pk >> 28);
                     len = 4;
                 } else {
-                    uint32_t e = s_lut[qbase + (pk >> (32 - qb1))];
+                    const uint32_t e = s_lut[qbase + (pk >> (32 - qb1))];
                     v = e & 15;
                     len = (e >> 8) & 31;
                 }
-                br.skip((uint32_t)len);
-                int q0 = (v >> 3) & 1, q1 = (v >> 2) & 1, q2 = (v >> 1) & 1, q3 = v & 1;
-                int ns = q0 + q1 + q2 + q3;
-                uint32_t sb = br.get(ns);
+                /* the code and its sign bits are both inside the 32-bit peek
+                 * window (<= 6 + 4 bits), so decode signs without refills */
+                const int ns = __builtin_popcount(v);
+                const uint32_t sb = (pk << len) >> (32 - (ns ? ns : 1));
                 int bit = ns;
+                int q0 = (v >> 3) & 1, q1 = (v >> 2) & 1, q2 = (v >> 1) & 1, q3 = v & 1;
                 if (q0) { bit--; if ((sb >> bit) & 1) q0 = -1; }
                 if (q1) { bit--; if ((sb >> bit) & 1) q1 = -1; }
                 if (q2) { bit--; if ((sb >> bit) & 1) q2 = -1; }
                 if (q3) { bit--; if ((sb >> bit) & 1) q3 = -1; }
-                if (br.pos > end_bit) {
-                    br.seek(save);
-                    break;
-                }
-                *(uint2 *)(out + k) = make_uint2((uint32_t)(uint16_t)q0 | ((uint32_t)(uint16_t)q1 << 16),
-                                                 (uint32_t)(uint16_t)q2 | ((uint32_t)(uint16_t)q3 << 16));
+                if (save + (uint32_t)(len + ns) > end_bit) break; /* overread: discard */
+                br.skip((uint32_t)(len + ns));
+                rw.push((uint32_t)(uint16_t)q0 | ((uint32_t)(uint16_t)q1 << 16));
+                rw.push((uint32_t)(uint16_t)q2 | ((uint32_t)(uint16_t)q3 << 16));
                 k += 4;
             }
-            nz_end = k;
             used = br.pos - start;
         }
-        /* rzero */
-        int k0 = nz_end;
-        for (; k0 < 576 && (k0 & 7); k0 += 2) *(uint32_t *)(out + k0) = 0u;
-        for (; k0 < 576; k0 += 8) *(uint4 *)(out + k0) = make_uint4(0, 0, 0, 0);
-        for (int i = 0; i < 40; i++) m.sf[i] = sf[i];
+        const int nz_end = 2 * rw.nw;
+        rw.finish();
+        UnitMeta m;
+#pragma unroll
+        for (int i = 0; i < 10; i++) ((uint32_t *)m.sf)[i] = ((const uint32_t *)sf)[i];
         m.global_gain = (uint8_t)us.global_gain;
         m.block_type = (uint8_t)(us.ws ? us.block_type : 0);
         m.mixed = (uint8_t)(us.ws && us.block_type == 2 ? us.mixed : 0);
@@ -470,11 +509,12 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
 
 /* ------------------------------------------------------------------------ */
 /* k_synth: one wave (64 lanes) per stream, frames in order.                */
-/*  Phase R, lane = (ch, sb): requantise (ISO 2.4.3.4), joint stereo, short */
-/*   reorder, alias reduction (lane shuffles), IMDCT 36 / 3x12 + window +   */
-/*   overlap (in registers) + frequency inversion -> S[ch][slot][sb] (LDS)  */
-/*  Phase S, lane = (ch, m): per slot, 32-point matrixing X = C.S (ISO Annex*/
-/*   A, as the 32x32 DCT-II half of N[64][32]), X ring in LDS, then lane   */
+/*  Phase R, lane = (ch, sb): requantise (ISO 2.4.3.4) + joint stereo in   */
+/*   bitstream order, short reorder (LDS), alias reduction (lane shuffles), */
+/*   IMDCT 36 / 3x12 + window + overlap (registers) + frequency inversion  */
+/*   -> S[ch][slot][sb] (LDS)                                              */
+/*  Phase S, lane = (ch, m): 32-point matrixing X = C.S for all 18 slots   */
+/*   (18 independent accumulators), X ring (33 slots, LDS); then lane      */
 /*   (ch, j) applies the 512-tap window D over 16 slots -> int16 PCM.      */
 /* Template SRC_XR: config-2 entry (spectra given as f32 xr, after stereo). */
 /* ------------------------------------------------------------------------ */
@@ -482,42 +522,53 @@ __device__ __forceinline__ float exp2q(int q) { /* 2^(q/4) exactly rounded once 
     return ldexpf(c_pow2q[q & 3], q >> 2);
 }
 
+#define XRING 33 /* 15 history + 18 new slots                            */
+#define SROW 33  /* LDS row stride (floats) of S and X: bank-conflict pad */
+__device__ __forceinline__ int ring(int i) { return i >= XRING ? i - XRING : i; }
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
 template <bool SRC_XR>
 __global__ void __launch_bounds__(64) k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf,
                                               const UnitMeta *__restrict__ meta, const float *__restrict__ xr_in,
                                               const uint8_t *__restrict__ xr_bt, const uint8_t *__restrict__ xr_mixed,
                                               const DevTables *__restrict__ tab, StreamState *__restrict__ st,
                                               int16_t *__restrict__ pcm, int F, int xr_nch, int xr_sr) {
-    __shared__ float sS[2][18][32];
-    __shared__ float sB[2][576];
-    __shared__ float sX[2][32][32];
+    __shared__ float sS[2][18 * SROW];   /* reorder buffer, then S[ch][t][sb] */
+    __shared__ float sX[2][XRING][SROW]; /* matrixing outputs X, 33-slot ring */
+    __shared__ float sI[18][20];         /* IMDCT-36 kernel [k][o]            */
+    __shared__ float sW[4][36];          /* long windows                       */
     __shared__ UnitMeta sM[2];
     const int s = blockIdx.x;
     const int lane = threadIdx.x;
     const int ch = lane >> 5;
-    const int sb = lane & 31; /* Phase R: subband; Phase S: m / j */
+    const int sb = lane & 31; /* Phase R: subband; window: output j */
 
-    /* constants in registers */
-    float C[32];
+    for (int i = lane; i < 18 * 20; i += 64) (&sI[0][0])[i] = (&tab->imdct36[0][0])[i];
+    for (int i = lane; i < 4 * 36; i += 64) (&sW[0][0])[i] = (&tab->win36[0][0])[i];
+    /* MFMA A fragments: C[16 mt + (l & 15)][4 ks + (l >> 4)] */
+    float Af[2][8];
 #pragma unroll
-    for (int k = 0; k < 32; k++) C[k] = tab->dct_c[sb][k];
+    for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+        for (int ks = 0; ks < 8; ks++) Af[mt][ks] = tab->dct_c[16 * mt + (lane & 15)][4 * ks + (lane >> 4)];
     float Dw[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) Dw[i] = tab->dwin[sb][i];
     const int wa = tab->win_a[sb], wb = tab->win_b[sb];
 
-    /* state in */
     StreamState &S = st[s];
     float ov[18];
 #pragma unroll
     for (int i = 0; i < 18; i++) ov[i] = S.overlap[ch][sb][i];
-    for (int t = 0; t < MP3D_FIFO_SLOTS; t++) sX[ch][(t - MP3D_FIFO_SLOTS) & 31][sb] = S.fifo[ch][t][sb];
-    int pos = 0;
+    /* history: ring slots 0..14 hold slots pos-15 .. pos-1 */
+    int pos = MP3D_FIFO_SLOTS;
+    for (int t = 0; t < MP3D_FIFO_SLOTS; t++) sX[ch][t][sb] = S.fifo[ch][t][sb];
     __syncthreads();
 
     for (int f = 0; f < F; f++) {
         int nch, sr, mode = 0, mext = 0;
-        size_t fr = (size_t)s * F + f;
+        const size_t fr = (size_t)s * F + f;
         if (SRC_XR) {
             nch = xr_nch;
             sr = xr_sr;
@@ -539,13 +590,9 @@ __global__ void __launch_bounds__(64) k_synth(const FrameRec *__restrict__ rec, 
                 const size_t ux = (fr * 2 + gr) * (size_t)nch + (active ? ch : 0);
                 bt = xr_bt[ux];
                 mixed = bt == 2 ? xr_mixed[ux] : 0;
-                const float *src = xr_in + ux * 576;
+                const float *src = xr_in + ux * 576 + 18 * sb;
 #pragma unroll
-                for (int i = 0; i < 18; i++) {
-                    int rl = 18 * sb + i;
-                    int sl = (bt == 2 && !(mixed && rl < 36)) ? tab->short_src[sr][rl] : rl;
-                    x[i] = active ? src[sl] : 0.f;
-                }
+                for (int i = 0; i < 18; i++) x[i] = active ? src[i] : 0.f;
             } else {
                 if (lane < 2 * (int)(sizeof(UnitMeta) / 4)) {
                     int c = lane / (sizeof(UnitMeta) / 4), wi = lane % (sizeof(UnitMeta) / 4);
@@ -558,18 +605,17 @@ __global__ void __launch_bounds__(64) k_synth(const FrameRec *__restrict__ rec, 
                 mixed = M.mixed;
                 const int gain = (int)M.global_gain - 210;
                 const int shift = M.scalefac_scale + 1;
-                const int16_t *isrow = is_buf + u * 576;
                 /* requantise in bitstream order: lane (ch, sb) owns lines
                  * 18 sb .. 18 sb + 17 (coalesced is[] reads).  nzmask: bit b
                  * (long band b) / bit 22 + 13 w + b (short band b, window w)
-                 * set where this channel has a nonzero line (IS detection). */
+                 * where this channel has a nonzero line (IS detection). */
                 uint64_t nzmask = 0;
                 int vv[18];
                 if (active) {
-                    const uint32_t *row32 = (const uint32_t *)(isrow + 18 * sb);
+                    const uint32_t *row32 = (const uint32_t *)(is_buf + u * 576 + 18 * sb);
 #pragma unroll
                     for (int i = 0; i < 9; i++) {
-                        uint32_t w2 = row32[i];
+                        const uint32_t w2 = row32[i];
                         vv[2 * i] = (int16_t)(w2 & 0xFFFFu);
                         vv[2 * i + 1] = (int16_t)(w2 >> 16);
                     }
@@ -585,16 +631,17 @@ __global__ void __launch_bounds__(64) k_synth(const FrameRec *__restrict__ rec, 
                     if (sh) {
                         band = tab->bs_band[sr][l];
                         w = tab->bs_win[sr][l];
-                        int k = mixed ? 8 + 3 * (band - 3) + w : 3 * band + w;
+                        const int k = mixed ? 8 + 3 * (band - 3) + w : 3 * band + w;
                         q = gain - 8 * M.sbg[w] - (M.sf[k] << shift);
                     } else {
                         band = tab->long_sfb[sr][l];
-                        int pre = M.preflag ? MP3D_PRETAB[band] : 0;
+                        const int pre = M.preflag ? MP3D_PRETAB[band] : 0;
                         q = gain - ((M.sf[band] + pre) << shift);
                     }
                     const int v = vv[i];
-                    const int a = v < 0 ? -v : v;
-                    const float mag = tab->pow43[a] * exp2q(q);
+                    const float a = (float)(v < 0 ? -v : v);
+                    /* |is|^(4/3) = a * cbrt(a) via v_log/v_exp (rel. err ~1e-7) */
+                    const float mag = a * __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(a) * (1.0f / 3.0f)) * exp2q(q);
                     x[i] = v < 0 ? -mag : (v ? mag : 0.f);
                     if (v) nzmask |= sh ? (1ull << (22 + 13 * w + band)) : (1ull << band);
                 }
@@ -634,19 +681,19 @@ __global__ void __launch_bounds__(64) k_synth(const FrameRec *__restrict__ rec, 
                         else if (mext & 2) x[i] = ch ? (lv - rv) * isq : (lv + rv) * isq;
                     }
                 }
-                /* short-block reorder through LDS (window-grouped bands ->
-                 * (freq, window) interleave), only where this channel is short */
-                if (bt == 2) {
+            }
+            /* short-block reorder through LDS (window-grouped bands ->
+             * (freq, window) interleave), only where this channel is short */
+            if (bt == 2) {
 #pragma unroll
-                    for (int i = 0; i < 18; i++) sB[ch][18 * sb + i] = x[i];
-                }
-                __syncthreads();
-                if (bt == 2) {
+                for (int i = 0; i < 18; i++) sS[ch][18 * sb + i] = x[i];
+            }
+            __syncthreads();
+            if (bt == 2) {
 #pragma unroll
-                    for (int i = 0; i < 18; i++) {
-                        const int rl = 18 * sb + i;
-                        x[i] = (mixed && rl < 36) ? x[i] : sB[ch][tab->short_src[sr][rl]];
-                    }
+                for (int i = 0; i < 18; i++) {
+                    const int rl = 18 * sb + i;
+                    x[i] = (mixed && rl < 36) ? x[i] : sS[ch][tab->short_src[sr][rl]];
                 }
             }
             /* alias reduction (ISO 2.4.3.4): butterflies across the 31 subband
@@ -662,37 +709,54 @@ __global__ void __launch_bounds__(64) k_synth(const FrameRec *__restrict__ rec, 
                 }
 #pragma unroll
                 for (int k = 0; k < 8; k++) {
-                    float lo = x[17 - k], hi = x[k];
+                    const float lo = x[17 - k], hi = x[k];
                     if (upper) x[k] = hi * c_alias_cs[k] + up[k] * c_alias_ca[k];
                     if (lower) x[17 - k] = lo * c_alias_cs[k] - dn[k] * c_alias_ca[k];
                 }
             }
-            /* IMDCT + window + overlap-add + frequency inversion */
+            /* IMDCT + window + overlap-add + frequency inversion; out[] is
+             * formed directly from the 18 unique IMDCT outputs (no z[36]) */
+            float o18[18];
             {
-                float z[36];
                 const bool long_imdct = bt != 2 || (mixed && sb < 2);
                 if (long_imdct) {
                     const int wt = (bt == 2) ? 0 : bt;
                     float h[18];
 #pragma unroll
-                    for (int o = 0; o < 18; o++) {
-                        float acc = 0.f;
+                    for (int o = 0; o < 18; o++) h[o] = 0.f;
 #pragma unroll
-                        for (int k = 0; k < 18; k++) acc = fmaf(x[k], c_imdct36[k][o], acc);
-                        h[o] = acc;
+                    for (int k = 0; k < 18; k++) {
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            const float4 c4 = *(const float4 *)&sI[k][4 * q];
+                            h[4 * q + 0] = fmaf(x[k], c4.x, h[4 * q + 0]);
+                            h[4 * q + 1] = fmaf(x[k], c4.y, h[4 * q + 1]);
+                            h[4 * q + 2] = fmaf(x[k], c4.z, h[4 * q + 2]);
+                            h[4 * q + 3] = fmaf(x[k], c4.w, h[4 * q + 3]);
+                        }
+                        const float2 c2 = *(const float2 *)&sI[k][16];
+                        h[16] = fmaf(x[k], c2.x, h[16]);
+                        h[17] = fmaf(x[k], c2.y, h[17]);
+                    }
+                    /* z[i] = h[i], z[17-i] = -h[i], z[18+i] = z[35-i] = h[9+i] */
+                    const float *wv = sW[wt];
+#pragma unroll
+                    for (int i = 0; i < 9; i++) {
+                        o18[i] = fmaf(h[i], wv[i], ov[i]);
+                        o18[17 - i] = fmaf(-h[i], wv[17 - i], ov[17 - i]);
                     }
 #pragma unroll
                     for (int i = 0; i < 9; i++) {
-                        z[i] = h[i];
-                        z[17 - i] = -h[i];
-                        z[18 + i] = h[9 + i];
-                        z[35 - i] = h[9 + i];
+                        const float n0 = h[9 + i] * wv[18 + i];
+                        const float n1 = h[9 + i] * wv[35 - i];
+                        ov[i] = active ? n0 : ov[i];
+                        ov[17 - i] = active ? n1 : ov[17 - i];
                     }
-#pragma unroll
-                    for (int i = 0; i < 36; i++) z[i] *= c_win36[wt][i];
                 } else {
+                    /* z[6w+6+i] += y_w[i] * win12[i], w = 0..2, i = 0..11 */
+                    float z[24]; /* z[6..29] */
 #pragma unroll
-                    for (int i = 0; i < 36; i++) z[i] = 0.f;
+                    for (int i = 0; i < 24; i++) z[i] = 0.f;
 #pragma unroll
                     for (int w = 0; w < 3; w++) {
                         float h[6];
@@ -703,62 +767,100 @@ __global__ void __launch_bounds__(64) k_synth(const FrameRec *__restrict__ rec, 
                             for (int k = 0; k < 6; k++) acc = fmaf(x[3 * k + w], c_imdct12[k][o], acc);
                             h[o] = acc;
                         }
-                        float y[12];
 #pragma unroll
                         for (int i = 0; i < 3; i++) {
-                            y[i] = h[i];
-                            y[5 - i] = -h[i];
-                            y[6 + i] = h[3 + i];
-                            y[11 - i] = h[3 + i];
+                            z[6 * w + i] = fmaf(h[i], c_win12[i], z[6 * w + i]);
+                            z[6 * w + 5 - i] = fmaf(-h[i], c_win12[5 - i], z[6 * w + 5 - i]);
+                            z[6 * w + 6 + i] = fmaf(h[3 + i], c_win12[6 + i], z[6 * w + 6 + i]);
+                            z[6 * w + 11 - i] = fmaf(h[3 + i], c_win12[11 - i], z[6 * w + 11 - i]);
                         }
+                    }
 #pragma unroll
-                        for (int i = 0; i < 12; i++) z[6 * w + 6 + i] += y[i] * c_win12[i];
+                    for (int i = 0; i < 18; i++) o18[i] = (i < 6 ? 0.f : z[i - 6]) + ov[i];
+#pragma unroll
+                    for (int i = 0; i < 18; i++) {
+                        const float n = i < 12 ? z[12 + i] : 0.f;
+                        ov[i] = active ? n : ov[i];
                     }
                 }
+            }
+            __syncthreads(); /* reorder reads of sS done before S overwrite */
 #pragma unroll
-                for (int i = 0; i < 18; i++) {
-                    float v = z[i] + ov[i];
-                    ov[i] = active ? z[18 + i] : ov[i];
-                    if ((sb & 1) && (i & 1)) v = -v;
-                    sS[ch][i][sb] = v;
+            for (int i = 0; i < 18; i++) {
+                float v = o18[i];
+                if ((sb & 1) && (i & 1)) v = -v;
+                sS[ch][i * SROW + sb] = v;
+            }
+            __syncthreads();
+            /* Phase S (a): matrixing X[ch, t][m] = sum_sb C[m][sb] S[ch][t][sb]
+             * on the matrix cores: v_mfma_f32_16x16x4_f32, rows = m (2 tiles),
+             * cols = (ch, t) pairs (36 -> 3 tiles of 16), K = sb (8 steps).
+             * A = C fragments (registers), B = S columns (LDS, padded rows). */
+            {
+                f32x4 acc[2][3];
+#pragma unroll
+                for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+                    for (int nt = 0; nt < 3; nt++) acc[mt][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int nt = 0; nt < 3; nt++) {
+                    int c = 16 * nt + (lane & 15);
+                    c = c < 36 ? c : 35;
+                    const int cch = c >= 18 ? 1 : 0, ct = c - 18 * cch;
+                    const float *col = &sS[cch][ct * SROW + (lane >> 4)];
+#pragma unroll
+                    for (int ks = 0; ks < 8; ks++) {
+                        const float bv = col[4 * ks];
+                        acc[0][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[0][ks], bv, acc[0][nt], 0, 0, 0);
+                        acc[1][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[1][ks], bv, acc[1][nt], 0, 0, 0);
+                    }
+                }
+                /* D[row = 4 (l >> 4) + r][col = l & 15] -> X ring */
+#pragma unroll
+                for (int nt = 0; nt < 3; nt++) {
+                    const int c = 16 * nt + (lane & 15);
+                    if (c < 36) {
+                        const int cch = c >= 18 ? 1 : 0, ct = c - 18 * cch;
+                        float *xrow = &sX[cch][ring(pos + ct)][0];
+#pragma unroll
+                        for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+                            for (int r = 0; r < 4; r++) xrow[16 * mt + 4 * (lane >> 4) + r] = acc[mt][nt][r];
+                    }
                 }
             }
             __syncthreads();
-            /* Phase S: matrixing + windowing, 18 slots */
-            for (int t = 0; t < 18; t++) {
-                const float4 *row = (const float4 *)&sS[ch][t][0];
-                float acc = 0.f;
+            /* Phase S (b): 512-tap window over 16 slots, lane (ch, j = sb) */
+            if (active) {
 #pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    float4 v4 = row[q];
-                    acc = fmaf(C[4 * q + 0], v4.x, acc);
-                    acc = fmaf(C[4 * q + 1], v4.y, acc);
-                    acc = fmaf(C[4 * q + 2], v4.z, acc);
-                    acc = fmaf(C[4 * q + 3], v4.w, acc);
-                }
-                const int cur = (pos + t) & 31;
-                sX[ch][cur][sb] = acc;
-                __syncthreads();
-                float o = 0.f;
+                for (int t = 0; t < 18; t++) {
+                    const int cur = pos + t; /* < 2 * XRING */
+                    float o = 0.f;
 #pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    o = fmaf(Dw[2 * i], sX[ch][(cur - 2 * i) & 31][wa], o);
-                    o = fmaf(Dw[2 * i + 1], sX[ch][(cur - 2 * i - 1) & 31][wb], o);
-                }
-                if (active) {
+                    for (int i = 0; i < 8; i++) {
+                        int ia = cur - 2 * i, ib = cur - 2 * i - 1;
+                        ia = ia >= XRING ? ia - XRING : (ia < 0 ? ia + XRING : ia);
+                        ib = ib >= XRING ? ib - XRING : (ib < 0 ? ib + XRING : ib);
+                        o = fmaf(Dw[2 * i], sX[ch][ia][wa], o);
+                        o = fmaf(Dw[2 * i + 1], sX[ch][ib][wb], o);
+                    }
                     float pv = rintf(o * 32768.f);
                     pv = fminf(fmaxf(pv, -32768.f), 32767.f);
                     out[(gr * 576 + t * 32 + sb) * nch + ch] = (int16_t)pv;
                 }
             }
-            pos = (pos + 18) & 31;
+            pos = ring(pos + 18);
             __syncthreads();
         }
     }
     /* state out */
 #pragma unroll
     for (int i = 0; i < 18; i++) S.overlap[ch][sb][i] = ov[i];
-    for (int t = 0; t < MP3D_FIFO_SLOTS; t++) S.fifo[ch][t][sb] = sX[ch][(pos - MP3D_FIFO_SLOTS + t) & 31][sb];
+    for (int t = 0; t < MP3D_FIFO_SLOTS; t++) {
+        int k = pos - MP3D_FIFO_SLOTS + t;
+        k = k < 0 ? k + XRING : k;
+        S.fifo[ch][t][sb] = sX[ch][k][sb];
+    }
 }
 
 /* ------------------------------------------------------------------------ */
