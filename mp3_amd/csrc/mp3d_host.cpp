@@ -22,7 +22,7 @@
 
 namespace mp3d {
 hipError_t upload_constants(const float *, const float *, const float *, const float *, const float *, const float *,
-                            const float *, const float *);
+                            const float *);
 void launch_scan(const uint8_t *, const uint64_t *, const uint32_t *, StreamState *, FrameRec *, int32_t *, void *, int,
                  int, hipStream_t);
 void launch_gather(const uint8_t *, uint8_t *, const uint64_t *, StreamState *, const FrameRec *, const int32_t *, int,
@@ -145,51 +145,41 @@ static void build_tables(DevTables &t) {
     for (int sr = 0; sr < 3; sr++) {
         int l = 0;
         for (int b = 0; b < 22; b++)
-            for (int n = 0; n < MP3D_SFB_LONG_WIDTH[sr][b]; n++) t.long_sfb[sr][l++] = (uint8_t)b;
+            for (int n = 0; n < MP3D_SFB_LONG_WIDTH[sr][b]; n++) t.linfo[sr][l++] = (uint32_t)b;
         int p = 0;
         for (int b = 0; b < 13; b++) {
             int w = MP3D_SFB_SHORT_WIDTH[sr][b];
             for (int off = 0; off < 3 * w; off++) {
-                int f = off / 3, win = off % 3;
-                t.short_src[sr][p + off] = (uint16_t)(p + win * w + f);
-                t.bs_band[sr][p + off] = (uint8_t)b;
-                t.bs_win[sr][p + off] = (uint8_t)(off / w);
+                int win = off / w, f = off % w;
+                t.linfo[sr][p + off] |= ((uint32_t)b << 5) | ((uint32_t)win << 9) | ((uint32_t)(p + 3 * f + win) << 11);
             }
             p += 3 * w;
         }
-    }
-    for (int k = 0; k < 18; k++)
-        for (int o = 0; o < 18; o++) {
-            int i = o < 9 ? o : 18 + (o - 9);
-            t.imdct36[k][o] = (float)cos(M_PI / 72.0 * (2 * i + 19) * (2 * k + 1));
-        }
-    for (int i = 0; i < 36; i++) {
-        t.win36[0][i] = (float)sin(M_PI / 36.0 * (i + 0.5));
-        t.win36[1][i] = (float)(i < 18 ? sin(M_PI / 36.0 * (i + 0.5)) : i < 24 ? 1.0 : i < 30 ? sin(M_PI / 12.0 * (i - 18 + 0.5)) : 0.0);
-        t.win36[3][i] = (float)(i < 6 ? 0.0 : i < 12 ? sin(M_PI / 12.0 * (i - 6 + 0.5)) : i < 18 ? 1.0 : sin(M_PI / 36.0 * (i + 0.5)));
-        t.win36[2][i] = t.win36[0][i];
     }
     build_huffman_lut(t);
 }
 
 static int upload_symbols() {
-    float imdct36[18][18], imdct12[6][6], win36[4][36], win12[12], cs[8], ca[8], isr[7][2], p2q[4];
-    for (int k = 0; k < 18; k++)
-        for (int o = 0; o < 18; o++) {
-            int i = o < 9 ? o : 18 + (o - 9);
-            imdct36[k][o] = (float)cos(M_PI / 72.0 * (2 * i + 19) * (2 * k + 1));
-        }
+    float imdct12[6][6], win36[4][36], win12[12], cs[8], ca[8], isr[7][2], p2q[4];
     for (int k = 0; k < 6; k++)
         for (int o = 0; o < 6; o++) {
             int i = o < 3 ? o : 6 + (o - 3);
             imdct12[k][o] = (float)cos(M_PI / 24.0 * (2 * i + 7) * (2 * k + 1));
         }
-    for (int i = 0; i < 36; i++) {
-        win36[0][i] = (float)sin(M_PI / 36.0 * (i + 0.5));
-        win36[1][i] = (float)(i < 18 ? sin(M_PI / 36.0 * (i + 0.5)) : i < 24 ? 1.0 : i < 30 ? sin(M_PI / 12.0 * (i - 18 + 0.5)) : 0.0);
-        win36[3][i] = (float)(i < 6 ? 0.0 : i < 12 ? sin(M_PI / 12.0 * (i - 6 + 0.5)) : i < 18 ? 1.0 : sin(M_PI / 36.0 * (i + 0.5)));
-        win36[2][i] = win36[0][i]; /* unused: short blocks use win12 */
-    }
+    /* long windows (block types 0, 1, 3) with the fast IMDCT's output
+     * scale s_n = 1 / (2 cos(pi (2n+1) / 72)) and signs folded in
+     * (mp3d_kernels.hip imdct36_w): out i<9 uses y_(9+i), i in 9..17 -y_(26-i),
+     * 18..26 -y_(26-i), 27..35 -y_(i-27)                                   */
+    for (int bt = 0; bt < 4; bt++)
+        for (int i = 0; i < 36; i++) {
+            double w;
+            if (bt == 0 || bt == 2) w = sin(M_PI / 36.0 * (i + 0.5));
+            else if (bt == 1) w = i < 18 ? sin(M_PI / 36.0 * (i + 0.5)) : i < 24 ? 1.0 : i < 30 ? sin(M_PI / 12.0 * (i - 18 + 0.5)) : 0.0;
+            else w = i < 6 ? 0.0 : i < 12 ? sin(M_PI / 12.0 * (i - 6 + 0.5)) : i < 18 ? 1.0 : sin(M_PI / 36.0 * (i + 0.5));
+            int n = i < 9 ? 9 + i : i < 27 ? 26 - i : i - 27;
+            double sc = 1.0 / (2.0 * cos(M_PI * (2 * n + 1) / 72.0));
+            win36[bt][i] = (float)((i < 9 ? 1.0 : -1.0) * w * sc);
+        }
     for (int i = 0; i < 12; i++) win12[i] = (float)sin(M_PI / 12.0 * (i + 0.5));
     for (int i = 0; i < 8; i++) {
         double c = MP3D_ALIAS_C[i], d = sqrt(1.0 + c * c);
@@ -203,7 +193,7 @@ static int upload_symbols() {
         isr[p][1] = (float)(1.0 / (1.0 + tn));
     }
     for (int i = 0; i < 4; i++) p2q[i] = (float)pow(2.0, i / 4.0);
-    HIPCHK(upload_constants(&imdct36[0][0], &imdct12[0][0], &win36[0][0], win12, cs, ca, &isr[0][0], p2q));
+    HIPCHK(upload_constants(&imdct12[0][0], &win36[0][0], win12, cs, ca, &isr[0][0], p2q));
     return MP3D_OK;
 }
 

@@ -77,13 +77,10 @@ struct HuffLutHeader {
 struct DevTables {
     float pow43[8208];         /* |is|^(4/3), |is| <= 8206               */
     float dct_c[32][32];       /* C[m][sb] = cos(m (2 sb + 1) pi / 64)  */
-    float imdct36[18][20];     /* [k][o] 36-point IMDCT, 18 unique outs */
-    float win36[4][36];        /* long / start / (unused) / stop windows */
     float dwin[32][16];        /* per output j: signed window taps       */
-    uint8_t long_sfb[3][576];  /* line -> long band                      */
-    uint16_t short_src[3][576];/* reordered line -> bitstream line       */
-    uint8_t bs_band[3][576];   /* bitstream line (short) -> short band   */
-    uint8_t bs_win[3][576];    /* bitstream line (short) -> window       */
+    /* per (sample-rate, bitstream line): bits 0..4 long band, 5..8 short
+     * band, 9..10 short window, 11..20 reordered (short) position      */
+    uint32_t linfo[3][576];
     uint8_t win_a[32];         /* V[j] = sgn * X[a[j]]                   */
     uint8_t win_b[32];         /* V[32 + j] = sgn * X[b[j]]              */
     uint16_t lut[MP3D_LUT_MAX];

@@ -25,9 +25,8 @@ namespace mp3d {
 /* ------------------------------------------------------------------------ */
 /* Constant-memory tables (uniform access -> scalar loads)                   */
 /* ------------------------------------------------------------------------ */
-__constant__ float c_imdct36[18][18]; /* [k][o]: o<9 -> out o, o>=9 -> out 18+(o-9) */
 __constant__ float c_imdct12[6][6];   /* [k][o]: o<3 -> out o, o>=3 -> out 6+(o-3)   */
-__constant__ float c_win36[4][36];
+__constant__ float c_win36[4][36];    /* long windows x IMDCT output scale (imdct36_w) */
 __constant__ float c_win12[12];
 __constant__ float c_alias_cs[8];
 __constant__ float c_alias_ca[8];
@@ -507,63 +506,133 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
     }
 }
 
-/* ------------------------------------------------------------------------ */
-/* k_synth: one wave (64 lanes) per stream, frames in order.                */
-/*  Phase R, lane = (ch, sb): requantise (ISO 2.4.3.4) + joint stereo in   */
-/*   bitstream order, short reorder (LDS), alias reduction (lane shuffles), */
-/*   IMDCT 36 / 3x12 + window + overlap (registers) + frequency inversion  */
-/*   -> S[ch][slot][sb] (LDS)                                              */
-/*  Phase S, lane = (ch, m): 32-point matrixing X = C.S for all 18 slots   */
-/*   (18 independent accumulators), X ring (33 slots, LDS); then lane      */
-/*   (ch, j) applies the 512-tap window D over 16 slots -> int16 PCM.      */
-/* Template SRC_XR: config-2 entry (spectra given as f32 xr, after stereo). */
-/* ------------------------------------------------------------------------ */
-__device__ __forceinline__ float exp2q(int q) { /* 2^(q/4) exactly rounded once */
-    return ldexpf(c_pow2q[q & 3], q >> 2);
+/* 9-point DCT-III: v[n] = sum_m a[m] cos(pi m (2n+1) / 18), n = 0..8, via the
+ * symmetry v[8-n] = sum_m (-1)^m a[m] cos(...): even / odd m partial sums */
+__device__ __forceinline__ void dct3_9(const float *a, float *v) {
+    const float C10 = 9.848077530e-01f; /* cos(10 deg) */
+    const float C20 = 9.396926208e-01f; /* cos(20 deg) */
+    const float C30 = 8.660254038e-01f; /* cos(30 deg) */
+    const float C40 = 7.660444431e-01f; /* cos(40 deg) */
+    const float C50 = 6.427876097e-01f; /* cos(50 deg) */
+    const float C70 = 3.420201433e-01f; /* cos(70 deg) */
+    const float C80 = 1.736481777e-01f; /* cos(80 deg) */
+    const float ev0 = fmaf(a[8], C80, fmaf(a[6], 0.5f, fmaf(a[4], C40, fmaf(a[2], C20, a[0]))));
+    const float od0 = fmaf(a[7], C70, fmaf(a[5], C50, fmaf(a[3], C30, a[1] * C10)));
+    v[0] = ev0 + od0;
+    v[8] = ev0 - od0;
+    const float ev1 = fmaf(a[8], -0.5f, (fmaf(a[4], -0.5f, fmaf(a[2], 0.5f, a[0])) - a[6]));
+    const float od1 = fmaf(a[7], -C30, fmaf(a[5], -C30, a[1] * C30));
+    v[1] = ev1 + od1;
+    v[7] = ev1 - od1;
+    const float ev2 = fmaf(a[8], C40, fmaf(a[6], 0.5f, fmaf(a[4], -C20, fmaf(a[2], -C80, a[0]))));
+    const float od2 = fmaf(a[7], C10, fmaf(a[5], -C70, fmaf(a[3], -C30, a[1] * C50)));
+    v[2] = ev2 + od2;
+    v[6] = ev2 - od2;
+    const float ev3 = fmaf(a[8], -C20, fmaf(a[6], 0.5f, fmaf(a[4], C80, fmaf(a[2], -C40, a[0]))));
+    const float od3 = fmaf(a[7], -C50, fmaf(a[5], C10, fmaf(a[3], -C30, a[1] * C70)));
+    v[3] = ev3 + od3;
+    v[5] = ev3 - od3;
+    v[4] = a[0] - a[2] + a[4] - a[6] + a[8];
 }
 
-#define XRING 33 /* 15 history + 18 new slots                            */
-#define SROW 33  /* LDS row stride (floats) of S and X: bank-conflict pad */
-__device__ __forceinline__ int ring(int i) { return i >= XRING ? i - XRING : i; }
+
+/* 36-point IMDCT of one subband's 18 lines (ISO 2.4.3.4) without the 18x36
+ * matrix: x_i = y_(i+9) / -y_(26-i) / -y_(i-27) with y the 18-point DCT-IV
+ * of X; y_n = w_n / (2 cos(pi (2n+1) / 72)) (scale folded into c_win36), w
+ * the 18-point DCT-III of Z_k = X_k + X_(k-1), split into the 9-point
+ * DCT-III of Z_2m (even) and of Z_(2m+1) + Z_(2m-1) (odd, scaled by
+ * 1 / (2 cos(pi (2n+1) / 36))).  ~150 flops instead of 324 FMAs.        */
+__device__ __forceinline__ void imdct36_w(const float *X, float *w) {
+    float e[9], p[9], E[9], P[9];
+    float zprev = 0.f;
+#pragma unroll
+    for (int m = 0; m < 9; m++) {
+        e[m] = m ? X[2 * m] + X[2 * m - 1] : X[0];
+        const float zo = X[2 * m + 1] + X[2 * m];
+        p[m] = zo + zprev;
+        zprev = zo;
+    }
+    dct3_9(e, E);
+    dct3_9(p, P);
+    const float K[9] = {5.019099188e-01f, 5.176380902e-01f, 5.516889595e-01f, 6.103872944e-01f, 7.071067812e-01f,
+                        8.717233978e-01f, 1.183100792e+00f, 1.931851653e+00f, 5.736856623e+00f};
+#pragma unroll
+    for (int n = 0; n < 9; n++) {
+        const float o = P[n] * K[n];
+        w[n] = E[n] + o;
+        w[17 - n] = E[n] - o;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* k_synth: one wave (64 lanes) per stream, frames and granules in order;   */
+/* every phase exchanges data through ONE 5 KB LDS buffer, so a wave holds  */
+/* only the per-stream state (IMDCT overlap, synthesis history) in VGPRs.   */
+/*  Q  lane = line (l = lane + 64 i): requantise both channels (ISO 2.4.3.4,*/
+/*     per-band 2^(q/4) precomputed by lane = band), joint stereo paired by */
+/*     bitstream line, scatter into LDS in short-block reordered position.  */
+/*  I  lane = (ch, sb): alias reduction (neighbours read from LDS), IMDCT   */
+/*     36 / 3x12 + window + overlap + frequency inversion -> S[ch,t][sb].   */
+/*  M  32-point matrixing X = C.S on the matrix cores (v_mfma_f32_16x16x4): */
+/*     rows m, cols (ch, t), K = sb; A = C fragments, B = S rows (LDS).     */
+/*  W  lane = (ch, j): 512-tap window over 16 slots; the 29 X values of the */
+/*     previous granule this lane needs live in registers -> int16 PCM.     */
+/* Template SRC_XR: config-2 entry (spectra given as f32 xr, after stereo). */
+/* ------------------------------------------------------------------------ */
+#define SROW 36      /* LDS row stride of S (floats): 16-B rows, few conflicts */
+#define SYN_BUF 1296 /* floats: max(xr 2x576, S 36x36, X 36x32)              */
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+/* Opaque copy of a loop-invariant LDS index: keeps the compiler from
+ * hoisting one address VGPR per unrolled access out of the frame loop
+ * (it would rather hold ~60 of them live than fold immediate offsets). */
+__device__ __forceinline__ int opaque(int v) {
+    __asm__ volatile("" : "+v"(v));
+    return v;
+}
+
+__device__ __forceinline__ float pow2_quarter(int q) { /* 2^(q/4), exact table */
+    const int r = q & 3;
+    const float f = r == 0 ? 1.0f : r == 1 ? 1.18920711500272106672f : r == 2 ? 1.41421356237309504880f
+                                                                              : 1.68179283050742908606f;
+    return ldexpf(f, q >> 2);
+}
+
 template <bool SRC_XR>
-__global__ void __launch_bounds__(64) k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8))) k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf,
                                               const UnitMeta *__restrict__ meta, const float *__restrict__ xr_in,
                                               const uint8_t *__restrict__ xr_bt, const uint8_t *__restrict__ xr_mixed,
                                               const DevTables *__restrict__ tab, StreamState *__restrict__ st,
                                               int16_t *__restrict__ pcm, int F, int xr_nch, int xr_sr) {
-    __shared__ float sS[2][18 * SROW];   /* reorder buffer, then S[ch][t][sb] */
-    __shared__ float sX[2][XRING][SROW]; /* matrixing outputs X, 33-slot ring */
-    __shared__ float sI[18][20];         /* IMDCT-36 kernel [k][o]            */
-    __shared__ float sW[4][36];          /* long windows                       */
+    __shared__ float sBuf[SYN_BUF];
+    __shared__ float sScale[2][64]; /* 2^(q/4) per (ch, band idx): long b | 22 + 3 b + w */
+    __shared__ uint8_t sIS[64];     /* intensity position per right-channel band idx, 0xFF none */
+    __shared__ float sP43[16];      /* |is|^(4/3) for |is| < 16                       */
+    __shared__ float sW[4][36];     /* long-block windows                             */
+    __shared__ float sISR[7][2];    /* MPEG-1 intensity ratios                        */
     __shared__ UnitMeta sM[2];
     const int s = blockIdx.x;
     const int lane = threadIdx.x;
     const int ch = lane >> 5;
-    const int sb = lane & 31; /* Phase R: subband; window: output j */
+    const int sb = lane & 31; /* phase I: subband; phase W: output j */
 
-    for (int i = lane; i < 18 * 20; i += 64) (&sI[0][0])[i] = (&tab->imdct36[0][0])[i];
-    for (int i = lane; i < 4 * 36; i += 64) (&sW[0][0])[i] = (&tab->win36[0][0])[i];
-    /* MFMA A fragments: C[16 mt + (l & 15)][4 ks + (l >> 4)] */
-    float Af[2][8];
-#pragma unroll
-    for (int mt = 0; mt < 2; mt++)
-#pragma unroll
-        for (int ks = 0; ks < 8; ks++) Af[mt][ks] = tab->dct_c[16 * mt + (lane & 15)][4 * ks + (lane >> 4)];
-    float Dw[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) Dw[i] = tab->dwin[sb][i];
-    const int wa = tab->win_a[sb], wb = tab->win_b[sb];
+    if (lane < 16) sP43[lane] = tab->pow43[lane];
+    if (lane < 14) (&sISR[0][0])[lane] = (&c_is_ratio[0][0])[lane];
+    for (int i = lane; i < 4 * 36; i += 64) (&sW[0][0])[i] = (&c_win36[0][0])[i];
 
     StreamState &S = st[s];
+    const int wa = tab->win_a[sb], wb = tab->win_b[sb];
     float ov[18];
 #pragma unroll
     for (int i = 0; i < 18; i++) ov[i] = S.overlap[ch][sb][i];
-    /* history: ring slots 0..14 hold slots pos-15 .. pos-1 */
-    int pos = MP3D_FIFO_SLOTS;
-    for (int t = 0; t < MP3D_FIFO_SLOTS; t++) sX[ch][t][sb] = S.fifo[ch][t][sb];
+    /* synthesis history: ha[k] = X_{k-14}[wa], hb[k] = X_{k-15}[wb] (slot
+     * index relative to the granule's first slot; fifo[t] = slot t - 15)  */
+    float ha[14], hb[15];
+#pragma unroll
+    for (int k = 0; k < 14; k++) ha[k] = S.fifo[ch][k + 1][wa];
+#pragma unroll
+    for (int k = 0; k < 15; k++) hb[k] = S.fifo[ch][k][wb];
     __syncthreads();
 
     for (int f = 0; f < F; f++) {
@@ -582,173 +651,187 @@ __global__ void __launch_bounds__(64) k_synth(const FrameRec *__restrict__ rec, 
         }
         const bool active = ch < nch;
         int16_t *out = pcm + fr * 2304;
+        const uint32_t *linfo = tab->linfo[sr];
         for (int gr = 0; gr < 2; gr++) {
-            const size_t u = (fr * 2 + gr) * 2 + ch;
-            int bt, mixed;
-            float x[18];
+            /* lane-derived indices are re-derived from an opaque copy each
+             * granule so they are not hoisted and held live across the loop */
+            const int lane = opaque((int)threadIdx.x);
+            const int ch = lane >> 5, sb = lane & 31;
+            /* block structure of both channels (uniform) */
+            int bt0, mx0, bt1 = 0, mx1 = 0;
+            /* ---------------- phase Q: requantise + stereo -> LDS ---------- */
             if (SRC_XR) {
-                const size_t ux = (fr * 2 + gr) * (size_t)nch + (active ? ch : 0);
-                bt = xr_bt[ux];
-                mixed = bt == 2 ? xr_mixed[ux] : 0;
-                const float *src = xr_in + ux * 576 + 18 * sb;
+                const size_t ux = (fr * 2 + gr) * (size_t)nch;
+                bt0 = xr_bt[ux];
+                mx0 = bt0 == 2 ? xr_mixed[ux] : 0;
+                if (nch == 2) {
+                    bt1 = xr_bt[ux + 1];
+                    mx1 = bt1 == 2 ? xr_mixed[ux + 1] : 0;
+                }
 #pragma unroll
-                for (int i = 0; i < 18; i++) x[i] = active ? src[i] : 0.f;
+                for (int i = 0; i < 9; i++) {
+                    const int l = lane + 64 * i;
+                    const uint32_t inf = linfo[l];
+                    const int dst = (int)(inf >> 11);
+                    const float x0 = xr_in[ux * 576 + l];
+                    sBuf[(bt0 == 2 && !(mx0 && l < 36)) ? dst : l] = x0;
+                    if (nch == 2) {
+                        const float x1 = xr_in[(ux + 1) * 576 + l];
+                        sBuf[576 + ((bt1 == 2 && !(mx1 && l < 36)) ? dst : l)] = x1;
+                    }
+                }
             } else {
+                const size_t u0 = (fr * 2 + gr) * 2;
                 if (lane < 2 * (int)(sizeof(UnitMeta) / 4)) {
-                    int c = lane / (sizeof(UnitMeta) / 4), wi = lane % (sizeof(UnitMeta) / 4);
-                    if (c < nch)
-                        ((uint32_t *)&sM[c])[wi] = ((const uint32_t *)&meta[(fr * 2 + gr) * 2 + c])[wi];
+                    const int c = lane / (int)(sizeof(UnitMeta) / 4), wi = lane % (int)(sizeof(UnitMeta) / 4);
+                    if (c < nch) ((uint32_t *)&sM[c])[wi] = ((const uint32_t *)&meta[u0 + c])[wi];
                 }
                 __syncthreads();
-                const UnitMeta &M = sM[active ? ch : 0];
-                bt = M.block_type;
-                mixed = M.mixed;
-                const int gain = (int)M.global_gain - 210;
-                const int shift = M.scalefac_scale + 1;
-                /* requantise in bitstream order: lane (ch, sb) owns lines
-                 * 18 sb .. 18 sb + 17 (coalesced is[] reads).  nzmask: bit b
-                 * (long band b) / bit 22 + 13 w + b (short band b, window w)
-                 * where this channel has a nonzero line (IS detection). */
-                uint64_t nzmask = 0;
-                int vv[18];
-                if (active) {
-                    const uint32_t *row32 = (const uint32_t *)(is_buf + u * 576 + 18 * sb);
-#pragma unroll
-                    for (int i = 0; i < 9; i++) {
-                        const uint32_t w2 = row32[i];
-                        vv[2 * i] = (int16_t)(w2 & 0xFFFFu);
-                        vv[2 * i + 1] = (int16_t)(w2 >> 16);
-                    }
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 18; i++) vv[i] = 0;
+                bt0 = sM[0].block_type;
+                mx0 = sM[0].mixed;
+                if (nch == 2) {
+                    bt1 = sM[1].block_type;
+                    mx1 = sM[1].mixed;
                 }
-#pragma unroll
-                for (int i = 0; i < 18; i++) {
-                    const int l = 18 * sb + i;
-                    const bool sh = bt == 2 && !(mixed && l < 36);
-                    int q, band, w = 0;
-                    if (sh) {
-                        band = tab->bs_band[sr][l];
-                        w = tab->bs_win[sr][l];
-                        const int k = mixed ? 8 + 3 * (band - 3) + w : 3 * band + w;
-                        q = gain - 8 * M.sbg[w] - (M.sf[k] << shift);
+                /* per-band scale, lane = band idx */
+                for (int c = 0; c < nch; c++) {
+                    const UnitMeta &M = sM[c];
+                    const int gain = (int)M.global_gain - 210, shift = M.scalefac_scale + 1;
+                    int q;
+                    if (lane < 22) {
+                        q = gain - ((M.sf[lane] + (M.preflag ? MP3D_PRETAB[lane] : 0)) << shift);
                     } else {
-                        band = tab->long_sfb[sr][l];
-                        const int pre = M.preflag ? MP3D_PRETAB[band] : 0;
-                        q = gain - ((M.sf[band] + pre) << shift);
+                        const int b = (lane - 22) / 3, w = lane - 22 - 3 * b;
+                        int k = M.mixed ? 8 + 3 * (b - 3) + w : 3 * b + w;
+                        k = k < 0 ? 0 : (k > 39 ? 39 : k);
+                        q = gain - 8 * M.sbg[w < 3 ? w : 0] - (M.sf[k] << shift);
                     }
-                    const int v = vv[i];
-                    const float a = (float)(v < 0 ? -v : v);
-                    /* |is|^(4/3) = a * cbrt(a) via v_log/v_exp (rel. err ~1e-7) */
-                    const float mag = a * __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(a) * (1.0f / 3.0f)) * exp2q(q);
-                    x[i] = v < 0 ? -mag : (v ? mag : 0.f);
-                    if (v) nzmask |= sh ? (1ull << (22 + 13 * w + band)) : (1ull << band);
+                    sScale[c][lane] = pow2_quarter(q);
+                }
+                __syncthreads();
+                float xv[2][9];
+                uint64_t nzR = 0;
+#pragma unroll
+                for (int i = 0; i < 9; i++) {
+                    const int l = lane + 64 * i;
+                    const uint32_t inf = linfo[l];
+                    const int lb = inf & 31, sbd = (inf >> 5) & 15, w = (inf >> 9) & 3;
+#pragma unroll
+                    for (int c = 0; c < 2; c++) {
+                        xv[c][i] = 0.f;
+                        if (c < nch) {
+                            const int bt = c ? bt1 : bt0, mx = c ? mx1 : mx0;
+                            const bool sh = bt == 2 && !(mx && l < 36);
+                            const int v = is_buf[(u0 + c) * 576 + l];
+                            const int a = v < 0 ? -v : v;
+                            float p = sP43[a < 16 ? a : 0];
+                            if (a >= 16) p = tab->pow43[a];
+                            const float mag = p * sScale[c][sh ? 22 + 3 * sbd + w : lb];
+                            xv[c][i] = v < 0 ? -mag : (v ? mag : 0.f);
+                            if (c == 1 && v) nzR |= sh ? (1ull << (22 + 13 * w + sbd)) : (1ull << lb);
+                        }
+                    }
                 }
                 /* joint stereo (ISO 2.4.3.4): MPEG-1 intensity + M/S, paired by
-                 * bitstream line; the right channel's block structure decides
-                 * the IS bands (FFmpeg compute_stereo) */
+                 * bitstream line; the right channel's block structure and its
+                 * highest nonzero band (per window) decide the IS bands
+                 * (FFmpeg compute_stereo; oracle/mp3_oracle.c orc_stereo) */
                 if (mode == 1 && nch == 2 && mext) {
-                    uint64_t rm = ch ? nzmask : 0ull;
+                    if (mext & 1) {
 #pragma unroll
-                    for (int o = 1; o < 64; o <<= 1) rm |= __shfl_xor(rm, o);
-                    const UnitMeta &MR = sM[1];
-                    const float isq = 0.70710678118654752f;
-                    const bool short_nz = (rm >> 22) != 0ull;
-#pragma unroll
-                    for (int i = 0; i < 18; i++) {
-                        const float other = __shfl_xor(x[i], 32);
-                        const float lv = ch ? other : x[i], rv = ch ? x[i] : other;
-                        const int l = 18 * sb + i;
-                        bool do_is = false;
-                        int ipos = 7;
-                        if (mext & 1) {
-                            const bool shR = MR.block_type == 2 && !(MR.mixed && l < 36);
-                            if (shR) {
-                                const int band = tab->bs_band[sr][l], w = tab->bs_win[sr][l];
-                                const uint32_t wm = (uint32_t)(rm >> (22 + 13 * w)) & 0x1FFFu;
-                                const int kb = band == 12 ? 11 : band;
-                                ipos = MR.sf[MR.mixed ? 8 + 3 * (kb - 3) + w : 3 * kb + w];
-                                do_is = (wm >> band) == 0u && ipos < 7;
-                            } else {
-                                const int band = tab->long_sfb[sr][l];
-                                const uint32_t lm = (uint32_t)(rm & 0x3FFFFFull);
-                                ipos = MR.sf[band == 21 ? 20 : band];
-                                do_is = !short_nz && (lm >> band) == 0u && ipos < 7;
+                        for (int o = 1; o < 64; o <<= 1) nzR |= __shfl_xor(nzR, o);
+                        const UnitMeta &R = sM[1];
+                        int ip = 0xFF;
+                        if (lane < 22) {
+                            if (bt1 != 2 || (mx1 && lane < 8)) {
+                                const int p = R.sf[lane == 21 ? 20 : lane];
+                                const bool short_nz = (nzR >> 22) != 0ull;
+                                if (!short_nz && ((uint32_t)(nzR & 0x3FFFFFull) >> lane) == 0u && p < 7) ip = p;
+                            }
+                        } else if (lane < 61 && bt1 == 2) {
+                            const int b = (lane - 22) / 3, w = lane - 22 - 3 * b;
+                            if (!mx1 || b >= 3) {
+                                const int kb = b == 12 ? 11 : b;
+                                const int p = R.sf[mx1 ? 8 + 3 * (kb - 3) + w : 3 * kb + w];
+                                const uint32_t wm = (uint32_t)(nzR >> (22 + 13 * w)) & 0x1FFFu;
+                                if ((wm >> b) == 0u && p < 7) ip = p;
                             }
                         }
-                        if (do_is) x[i] = lv * c_is_ratio[ipos][ch];
-                        else if (mext & 2) x[i] = ch ? (lv - rv) * isq : (lv + rv) * isq;
+                        sIS[lane] = (uint8_t)ip;
+                        __syncthreads();
+                    }
+                    const float isq = 0.70710678118654752f;
+#pragma unroll
+                    for (int i = 0; i < 9; i++) {
+                        const int l = lane + 64 * i;
+                        const float lv = xv[0][i], rv = xv[1][i];
+                        int ip = 0xFF;
+                        if (mext & 1) {
+                            const uint32_t inf = linfo[l];
+                            const bool shR = bt1 == 2 && !(mx1 && l < 36);
+                            ip = sIS[shR ? 22 + 3 * ((inf >> 5) & 15) + ((inf >> 9) & 3) : (inf & 31)];
+                        }
+                        if (ip != 0xFF) {
+                            xv[0][i] = lv * sISR[ip][0];
+                            xv[1][i] = lv * sISR[ip][1];
+                        } else if (mext & 2) {
+                            xv[0][i] = (lv + rv) * isq;
+                            xv[1][i] = (lv - rv) * isq;
+                        }
                     }
                 }
-            }
-            /* short-block reorder through LDS (window-grouped bands ->
-             * (freq, window) interleave), only where this channel is short */
-            if (bt == 2) {
 #pragma unroll
-                for (int i = 0; i < 18; i++) sS[ch][18 * sb + i] = x[i];
+                for (int i = 0; i < 9; i++) {
+                    const int l = lane + 64 * i;
+                    const int dst = (int)(linfo[l] >> 11);
+                    sBuf[(bt0 == 2 && !(mx0 && l < 36)) ? dst : l] = xv[0][i];
+                    if (nch == 2) sBuf[576 + ((bt1 == 2 && !(mx1 && l < 36)) ? dst : l)] = xv[1][i];
+                }
             }
             __syncthreads();
-            if (bt == 2) {
-#pragma unroll
-                for (int i = 0; i < 18; i++) {
-                    const int rl = 18 * sb + i;
-                    x[i] = (mixed && rl < 36) ? x[i] : sS[ch][tab->short_src[sr][rl]];
-                }
-            }
-            /* alias reduction (ISO 2.4.3.4): butterflies across the 31 subband
-             * boundaries (long), the first one only (mixed), none (short) */
+            /* ---------------- phase I: alias + IMDCT + overlap ------------ */
+            const int bt = ch ? bt1 : bt0, mixed = ch ? mx1 : mx0;
+            float o18[18];
             {
-                const bool upper = active && ((bt != 2 && sb >= 1) || (bt == 2 && mixed && sb == 1));
-                const bool lower = active && ((bt != 2 && sb <= 30) || (bt == 2 && mixed && sb == 0));
-                float up[8], dn[8];
+                const int base = ch * 576 + 18 * sb;
+                float x[18], up[8], dn[8];
 #pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    up[k] = __shfl_up(x[17 - k], 1); /* lane sb-1's x[17-k] */
-                    dn[k] = __shfl_down(x[k], 1);    /* lane sb+1's x[k]    */
+                for (int i = 0; i < 9; i++) {
+                    const float2 v = *(const float2 *)&sBuf[base + 2 * i];
+                    x[2 * i] = v.x;
+                    x[2 * i + 1] = v.y;
                 }
+                const int pb = sb ? base - 8 : base, nb = sb < 31 ? base + 18 : base;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const float2 p = *(const float2 *)&sBuf[pb + 2 * i];
+                    const float2 n = *(const float2 *)&sBuf[nb + 2 * i];
+                    up[7 - 2 * i] = p.x; /* up[k] = x_{sb-1}[17 - k] */
+                    up[6 - 2 * i] = p.y;
+                    dn[2 * i] = n.x;     /* dn[k] = x_{sb+1}[k]      */
+                    dn[2 * i + 1] = n.y;
+                }
+                /* alias reduction (ISO 2.4.3.4): all 31 boundaries (long),
+                 * the first one (mixed), none (short) */
+                const bool upper = (bt != 2 && sb >= 1) || (bt == 2 && mixed && sb == 1);
+                const bool lower = (bt != 2 && sb <= 30) || (bt == 2 && mixed && sb == 0);
 #pragma unroll
                 for (int k = 0; k < 8; k++) {
                     const float lo = x[17 - k], hi = x[k];
                     if (upper) x[k] = hi * c_alias_cs[k] + up[k] * c_alias_ca[k];
                     if (lower) x[17 - k] = lo * c_alias_cs[k] - dn[k] * c_alias_ca[k];
                 }
-            }
-            /* IMDCT + window + overlap-add + frequency inversion; out[] is
-             * formed directly from the 18 unique IMDCT outputs (no z[36]) */
-            float o18[18];
-            {
                 const bool long_imdct = bt != 2 || (mixed && sb < 2);
                 if (long_imdct) {
-                    const int wt = (bt == 2) ? 0 : bt;
-                    float h[18];
-#pragma unroll
-                    for (int o = 0; o < 18; o++) h[o] = 0.f;
-#pragma unroll
-                    for (int k = 0; k < 18; k++) {
-#pragma unroll
-                        for (int q = 0; q < 4; q++) {
-                            const float4 c4 = *(const float4 *)&sI[k][4 * q];
-                            h[4 * q + 0] = fmaf(x[k], c4.x, h[4 * q + 0]);
-                            h[4 * q + 1] = fmaf(x[k], c4.y, h[4 * q + 1]);
-                            h[4 * q + 2] = fmaf(x[k], c4.z, h[4 * q + 2]);
-                            h[4 * q + 3] = fmaf(x[k], c4.w, h[4 * q + 3]);
-                        }
-                        const float2 c2 = *(const float2 *)&sI[k][16];
-                        h[16] = fmaf(x[k], c2.x, h[16]);
-                        h[17] = fmaf(x[k], c2.y, h[17]);
-                    }
-                    /* z[i] = h[i], z[17-i] = -h[i], z[18+i] = z[35-i] = h[9+i] */
-                    const float *wv = sW[wt];
+                    const float *wv = sW[bt == 2 ? 0 : bt];
+                    float w[18];
+                    imdct36_w(x, w);
 #pragma unroll
                     for (int i = 0; i < 9; i++) {
-                        o18[i] = fmaf(h[i], wv[i], ov[i]);
-                        o18[17 - i] = fmaf(-h[i], wv[17 - i], ov[17 - i]);
-                    }
-#pragma unroll
-                    for (int i = 0; i < 9; i++) {
-                        const float n0 = h[9 + i] * wv[18 + i];
-                        const float n1 = h[9 + i] * wv[35 - i];
+                        o18[i] = fmaf(w[9 + i], wv[i], ov[i]);
+                        o18[17 - i] = fmaf(w[9 + i], wv[17 - i], ov[17 - i]);
+                        const float n0 = w[8 - i] * wv[18 + i];
+                        const float n1 = w[8 - i] * wv[35 - i];
                         ov[i] = active ? n0 : ov[i];
                         ov[17 - i] = active ? n1 : ov[17 - i];
                     }
@@ -784,92 +867,112 @@ __global__ void __launch_bounds__(64) k_synth(const FrameRec *__restrict__ rec, 
                     }
                 }
             }
-            __syncthreads(); /* reorder reads of sS done before S overwrite */
+            __syncthreads(); /* every lane has read its xr before S overwrites it */
+            {
+                const int sw = opaque(18 * ch * SROW + sb);
 #pragma unroll
-            for (int i = 0; i < 18; i++) {
-                float v = o18[i];
-                if ((sb & 1) && (i & 1)) v = -v;
-                sS[ch][i * SROW + sb] = v;
+                for (int t = 0; t < 18; t++) sBuf[sw + t * SROW] = ((sb & 1) && (t & 1)) ? -o18[t] : o18[t];
             }
             __syncthreads();
-            /* Phase S (a): matrixing X[ch, t][m] = sum_sb C[m][sb] S[ch][t][sb]
-             * on the matrix cores: v_mfma_f32_16x16x4_f32, rows = m (2 tiles),
-             * cols = (ch, t) pairs (36 -> 3 tiles of 16), K = sb (8 steps).
-             * A = C fragments (registers), B = S columns (LDS, padded rows). */
+            /* ---------------- phase M: matrixing on the matrix cores ------- */
             {
-                f32x4 acc[2][3];
+                const int q = lane >> 4, r16 = lane & 15;
+                /* k = 4 ks + q <-> sb = 8 q + ks: each lane's 8 B values are
+                 * one contiguous 32-B run of an S row */
+                float Af[2][8];
 #pragma unroll
-                for (int mt = 0; mt < 2; mt++)
-#pragma unroll
-                    for (int nt = 0; nt < 3; nt++) acc[mt][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int nt = 0; nt < 3; nt++) {
-                    int c = 16 * nt + (lane & 15);
-                    c = c < 36 ? c : 35;
-                    const int cch = c >= 18 ? 1 : 0, ct = c - 18 * cch;
-                    const float *col = &sS[cch][ct * SROW + (lane >> 4)];
-#pragma unroll
-                    for (int ks = 0; ks < 8; ks++) {
-                        const float bv = col[4 * ks];
-                        acc[0][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[0][ks], bv, acc[0][nt], 0, 0, 0);
-                        acc[1][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[1][ks], bv, acc[1][nt], 0, 0, 0);
-                    }
+                for (int mt = 0; mt < 2; mt++) {
+                    const float4 *src = (const float4 *)&tab->dct_c[16 * mt + r16][8 * q];
+                    const float4 a0 = src[0], a1 = src[1];
+                    Af[mt][0] = a0.x; Af[mt][1] = a0.y; Af[mt][2] = a0.z; Af[mt][3] = a0.w;
+                    Af[mt][4] = a1.x; Af[mt][5] = a1.y; Af[mt][6] = a1.z; Af[mt][7] = a1.w;
                 }
-                /* D[row = 4 (l >> 4) + r][col = l & 15] -> X ring */
+                float Bf[3][8];
 #pragma unroll
                 for (int nt = 0; nt < 3; nt++) {
-                    const int c = 16 * nt + (lane & 15);
-                    if (c < 36) {
-                        const int cch = c >= 18 ? 1 : 0, ct = c - 18 * cch;
-                        float *xrow = &sX[cch][ring(pos + ct)][0];
+                    int n = 16 * nt + r16;
+                    n = n < 36 ? n : 35;
+                    const float4 *src = (const float4 *)&sBuf[n * SROW + 8 * q];
+                    const float4 b0 = src[0], b1 = src[1];
+                    Bf[nt][0] = b0.x; Bf[nt][1] = b0.y; Bf[nt][2] = b0.z; Bf[nt][3] = b0.w;
+                    Bf[nt][4] = b1.x; Bf[nt][5] = b1.y; Bf[nt][6] = b1.z; Bf[nt][7] = b1.w;
+                }
+                f32x4 acc[3][2];
+#pragma unroll
+                for (int nt = 0; nt < 3; nt++)
+#pragma unroll
+                    for (int mt = 0; mt < 2; mt++) acc[nt][mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < 8; ks++)
+#pragma unroll
+                    for (int nt = 0; nt < 3; nt++)
 #pragma unroll
                         for (int mt = 0; mt < 2; mt++)
+                            acc[nt][mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[mt][ks], Bf[nt][ks], acc[nt][mt], 0, 0, 0);
+                __syncthreads(); /* all S reads retired before X overwrites them */
+                /* D[row m = 16 mt + 4 q + r][col n] -> X[n][m] */
 #pragma unroll
-                            for (int r = 0; r < 4; r++) xrow[16 * mt + 4 * (lane >> 4) + r] = acc[mt][nt][r];
-                    }
+                for (int nt = 0; nt < 3; nt++) {
+                    const int n = 16 * nt + r16;
+                    if (n < 36)
+#pragma unroll
+                        for (int mt = 0; mt < 2; mt++) *(f32x4 *)&sBuf[n * 32 + 16 * mt + 4 * q] = acc[nt][mt];
                 }
             }
             __syncthreads();
-            /* Phase S (b): 512-tap window over 16 slots, lane (ch, j = sb) */
-            if (active) {
+            /* ---------------- phase W: 512-tap window -> PCM --------------- */
+            {
+                float Dw[16];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const float4 d = ((const float4 *)tab->dwin[sb])[i];
+                    Dw[4 * i] = d.x; Dw[4 * i + 1] = d.y; Dw[4 * i + 2] = d.z; Dw[4 * i + 3] = d.w;
+                }
+                float xa[18], xb[18];
+                const int pa = opaque(18 * ch * 32 + wa), pb = opaque(18 * ch * 32 + wb);
 #pragma unroll
                 for (int t = 0; t < 18; t++) {
-                    const int cur = pos + t; /* < 2 * XRING */
+                    xa[t] = sBuf[pa + t * 32];
+                    xb[t] = sBuf[pb + t * 32];
+                }
+#pragma unroll
+                for (int t = 0; t < 18; t++) {
                     float o = 0.f;
 #pragma unroll
                     for (int i = 0; i < 8; i++) {
-                        int ia = cur - 2 * i, ib = cur - 2 * i - 1;
-                        ia = ia >= XRING ? ia - XRING : (ia < 0 ? ia + XRING : ia);
-                        ib = ib >= XRING ? ib - XRING : (ib < 0 ? ib + XRING : ib);
-                        o = fmaf(Dw[2 * i], sX[ch][ia][wa], o);
-                        o = fmaf(Dw[2 * i + 1], sX[ch][ib][wb], o);
+                        const int sa = t - 2 * i, sbb = t - 2 * i - 1;
+                        const float va = sa >= 0 ? xa[sa] : ha[sa + 14];
+                        const float vb = sbb >= 0 ? xb[sbb] : hb[sbb + 15];
+                        o = fmaf(Dw[2 * i], va, o);
+                        o = fmaf(Dw[2 * i + 1], vb, o);
                     }
                     float pv = rintf(o * 32768.f);
                     pv = fminf(fmaxf(pv, -32768.f), 32767.f);
-                    out[(gr * 576 + t * 32 + sb) * nch + ch] = (int16_t)pv;
+                    if (active) out[(gr * 576 + t * 32 + sb) * nch + ch] = (int16_t)pv;
                 }
+#pragma unroll
+                for (int k = 0; k < 14; k++) ha[k] = active ? xa[k + 4] : ha[k];
+#pragma unroll
+                for (int k = 0; k < 15; k++) hb[k] = active ? xb[k + 3] : hb[k];
             }
-            pos = ring(pos + 18);
-            __syncthreads();
+            __syncthreads(); /* X reads done before the next granule's xr */
         }
     }
     /* state out */
 #pragma unroll
     for (int i = 0; i < 18; i++) S.overlap[ch][sb][i] = ov[i];
-    for (int t = 0; t < MP3D_FIFO_SLOTS; t++) {
-        int k = pos - MP3D_FIFO_SLOTS + t;
-        k = k < 0 ? k + XRING : k;
-        S.fifo[ch][t][sb] = sX[ch][k][sb];
-    }
+#pragma unroll
+    for (int k = 0; k < 14; k++) S.fifo[ch][k + 1][wa] = ha[k];
+#pragma unroll
+    for (int k = 0; k < 15; k++) S.fifo[ch][k][wb] = hb[k];
 }
 
 /* ------------------------------------------------------------------------ */
 /* Host-side launchers                                                       */
 /* ------------------------------------------------------------------------ */
-hipError_t upload_constants(const float *imdct36, const float *imdct12, const float *win36, const float *win12,
+hipError_t upload_constants(const float *imdct12, const float *win36, const float *win12,
                             const float *alias_cs, const float *alias_ca, const float *is_ratio, const float *pow2q) {
     hipError_t e;
-    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_imdct36), imdct36, sizeof(float) * 18 * 18))) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_imdct12), imdct12, sizeof(float) * 6 * 6))) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_win36), win36, sizeof(float) * 4 * 36))) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_win12), win12, sizeof(float) * 12))) return e;
