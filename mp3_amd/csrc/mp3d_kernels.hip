@@ -599,23 +599,31 @@ __device__ __forceinline__ float pow2_quarter(int q) { /* 2^(q/4), exact table *
     return ldexpf(f, q >> 2);
 }
 
+/* One wave per workgroup: LDS operations of a wave complete in issue order,
+ * so a phase hand-off through LDS only needs the compiler not to reorder
+ * across it -- no s_barrier and, unlike __syncthreads(), no vmcnt(0) drain
+ * of the global loads (prefetches) and PCM stores still in flight.      */
+__device__ __forceinline__ void wave_sync() { __asm__ volatile("" ::: "memory"); }
+
 template <bool SRC_XR>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8))) k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf,
-                                              const UnitMeta *__restrict__ meta, const float *__restrict__ xr_in,
-                                              const uint8_t *__restrict__ xr_bt, const uint8_t *__restrict__ xr_mixed,
-                                              const DevTables *__restrict__ tab, StreamState *__restrict__ st,
-                                              int16_t *__restrict__ pcm, int F, int xr_nch, int xr_sr) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
+k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, const UnitMeta *__restrict__ meta,
+        const float *__restrict__ xr_in, const uint8_t *__restrict__ xr_bt, const uint8_t *__restrict__ xr_mixed,
+        const DevTables *__restrict__ tab, StreamState *__restrict__ st, int16_t *__restrict__ pcm, int F, int xr_nch,
+        int xr_sr) {
     __shared__ float sBuf[SYN_BUF];
-    __shared__ float sScale[2][64]; /* 2^(q/4) per (ch, band idx): long b | 22 + 3 b + w */
-    __shared__ uint8_t sIS[64];     /* intensity position per right-channel band idx, 0xFF none */
-    __shared__ float sP43[16];      /* |is|^(4/3) for |is| < 16                       */
-    __shared__ float sW[4][36];     /* long-block windows                             */
-    __shared__ float sISR[7][2];    /* MPEG-1 intensity ratios                        */
+    __shared__ uint32_t sLinfo[576]; /* tab->linfo[sr] of the current sample rate   */
+    __shared__ float sScale[2][64];  /* 2^(q/4) per (ch, band idx): long b | 22 + 3 b + w */
+    __shared__ uint8_t sIS[64];      /* intensity position per right-channel band idx, 0xFF none */
+    __shared__ float sP43[16];       /* |is|^(4/3) for |is| < 16                       */
+    __shared__ float sW[4][36];      /* long-block windows                             */
+    __shared__ float sISR[7][2];     /* MPEG-1 intensity ratios                        */
     __shared__ UnitMeta sM[2];
     const int s = blockIdx.x;
     const int lane = threadIdx.x;
     const int ch = lane >> 5;
     const int sb = lane & 31; /* phase I: subband; phase W: output j */
+    constexpr int MW = (int)(sizeof(UnitMeta) / 4); /* 14 words per unit */
 
     if (lane < 16) sP43[lane] = tab->pow43[lane];
     if (lane < 14) (&sISR[0][0])[lane] = (&c_is_ratio[0][0])[lane];
@@ -633,7 +641,23 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
     for (int k = 0; k < 14; k++) ha[k] = S.fifo[ch][k + 1][wa];
 #pragma unroll
     for (int k = 0; k < 15; k++) hb[k] = S.fifo[ch][k][wb];
-    __syncthreads();
+    int cur_sr = -1;
+
+    /* next granule's is[] words (lane owns lines 2 lane + 128 i, +1) and
+     * UnitMeta words, loaded one granule ahead of use (register prefetch) */
+    uint32_t nis[2][5], nmeta = 0;
+    size_t pre_up = ~(size_t)0;
+    auto prefetch = [&](size_t up) {
+        if (SRC_XR) return;
+        const uint32_t *row = (const uint32_t *)(is_buf + up * 2 * 576);
+#pragma unroll
+        for (int c = 0; c < 2; c++)
+#pragma unroll
+            for (int i = 0; i < 5; i++) nis[c][i] = (i < 4 || lane < 32) ? row[c * 288 + lane + 64 * i] : 0u;
+        nmeta = lane < 2 * MW ? ((const uint32_t *)&meta[up * 2])[lane] : 0u;
+        pre_up = up;
+    };
+    prefetch((size_t)s * F * 2);
 
     for (int f = 0; f < F; f++) {
         int nch, sr, mode = 0, mext = 0;
@@ -649,9 +673,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
             mode = r.hdr3 >> 6;
             mext = (r.hdr3 >> 4) & 3;
         }
+        if (sr != cur_sr) { /* line tables of this sample rate into LDS */
+            wave_sync();
+            for (int i = lane; i < 576; i += 64) sLinfo[i] = tab->linfo[sr][i];
+            cur_sr = sr;
+            wave_sync();
+        }
         const bool active = ch < nch;
         int16_t *out = pcm + fr * 2304;
-        const uint32_t *linfo = tab->linfo[sr];
         for (int gr = 0; gr < 2; gr++) {
             /* lane-derived indices are re-derived from an opaque copy each
              * granule so they are not hoisted and held live across the loop */
@@ -671,8 +700,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
 #pragma unroll
                 for (int i = 0; i < 9; i++) {
                     const int l = lane + 64 * i;
-                    const uint32_t inf = linfo[l];
-                    const int dst = (int)(inf >> 11);
+                    const int dst = (int)(sLinfo[l] >> 11);
                     const float x0 = xr_in[ux * 576 + l];
                     sBuf[(bt0 == 2 && !(mx0 && l < 36)) ? dst : l] = x0;
                     if (nch == 2) {
@@ -681,12 +709,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
                     }
                 }
             } else {
-                const size_t u0 = (fr * 2 + gr) * 2;
-                if (lane < 2 * (int)(sizeof(UnitMeta) / 4)) {
-                    const int c = lane / (int)(sizeof(UnitMeta) / 4), wi = lane % (int)(sizeof(UnitMeta) / 4);
-                    if (c < nch) ((uint32_t *)&sM[c])[wi] = ((const uint32_t *)&meta[u0 + c])[wi];
-                }
-                __syncthreads();
+                const size_t up = fr * 2 + gr;
+                if (pre_up != up) prefetch(up); /* a skipped frame broke the chain */
+                uint32_t cis[2][5];
+#pragma unroll
+                for (int c = 0; c < 2; c++)
+#pragma unroll
+                    for (int i = 0; i < 5; i++) cis[c][i] = nis[c][i];
+                if (lane < 2 * MW && lane / MW < nch) ((uint32_t *)&sM[0])[lane] = nmeta;
+                /* the next granule's loads fly during this one */
+                if (gr == 0) prefetch(up + 1);
+                else if (f + 1 < F) prefetch(up + 1);
+                wave_sync();
                 bt0 = sM[0].block_type;
                 mx0 = sM[0].mixed;
                 if (nch == 2) {
@@ -708,26 +742,31 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
                     }
                     sScale[c][lane] = pow2_quarter(q);
                 }
-                __syncthreads();
-                float xv[2][9];
+                wave_sync();
+                /* lane owns lines 2 lane + 128 i + e (e = 0, 1), i < 4, or i = 4
+                 * for lanes < 32; xv[c][2 i + e] */
+                float xv[2][10];
                 uint64_t nzR = 0;
 #pragma unroll
-                for (int i = 0; i < 9; i++) {
-                    const int l = lane + 64 * i;
-                    const uint32_t inf = linfo[l];
-                    const int lb = inf & 31, sbd = (inf >> 5) & 15, w = (inf >> 9) & 3;
+                for (int i = 0; i < 5; i++) {
+                    const int l0 = 2 * lane + 128 * i;
+                    const bool ok = i < 4 || lane < 32;
+                    const uint2 inf2 = ok ? *(const uint2 *)&sLinfo[l0] : make_uint2(0u, 0u);
 #pragma unroll
-                    for (int c = 0; c < 2; c++) {
-                        xv[c][i] = 0.f;
-                        if (c < nch) {
+                    for (int e = 0; e < 2; e++) {
+                        const int l = l0 + e;
+                        const uint32_t inf = e ? inf2.y : inf2.x;
+                        const int lb = inf & 31, sbd = (inf >> 5) & 15, w = (inf >> 9) & 3;
+#pragma unroll
+                        for (int c = 0; c < 2; c++) {
                             const int bt = c ? bt1 : bt0, mx = c ? mx1 : mx0;
                             const bool sh = bt == 2 && !(mx && l < 36);
-                            const int v = is_buf[(u0 + c) * 576 + l];
+                            const int v = (int)(int16_t)(e ? (cis[c][i] >> 16) : (cis[c][i] & 0xFFFFu));
                             const int a = v < 0 ? -v : v;
                             float p = sP43[a < 16 ? a : 0];
                             if (a >= 16) p = tab->pow43[a];
                             const float mag = p * sScale[c][sh ? 22 + 3 * sbd + w : lb];
-                            xv[c][i] = v < 0 ? -mag : (v ? mag : 0.f);
+                            xv[c][2 * i + e] = v < 0 ? -mag : (v ? mag : 0.f);
                             if (c == 1 && v) nzR |= sh ? (1ull << (22 + 13 * w + sbd)) : (1ull << lb);
                         }
                     }
@@ -758,37 +797,48 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
                             }
                         }
                         sIS[lane] = (uint8_t)ip;
-                        __syncthreads();
+                        wave_sync();
                     }
                     const float isq = 0.70710678118654752f;
 #pragma unroll
-                    for (int i = 0; i < 9; i++) {
-                        const int l = lane + 64 * i;
-                        const float lv = xv[0][i], rv = xv[1][i];
-                        int ip = 0xFF;
-                        if (mext & 1) {
-                            const uint32_t inf = linfo[l];
-                            const bool shR = bt1 == 2 && !(mx1 && l < 36);
-                            ip = sIS[shR ? 22 + 3 * ((inf >> 5) & 15) + ((inf >> 9) & 3) : (inf & 31)];
-                        }
-                        if (ip != 0xFF) {
-                            xv[0][i] = lv * sISR[ip][0];
-                            xv[1][i] = lv * sISR[ip][1];
-                        } else if (mext & 2) {
-                            xv[0][i] = (lv + rv) * isq;
-                            xv[1][i] = (lv - rv) * isq;
+                    for (int i = 0; i < 5; i++) {
+                        const int l0 = 2 * lane + 128 * i;
+#pragma unroll
+                        for (int e = 0; e < 2; e++) {
+                            const int l = l0 + e, k = 2 * i + e;
+                            const float lv = xv[0][k], rv = xv[1][k];
+                            int ip = 0xFF;
+                            if ((mext & 1) && (i < 4 || lane < 32)) {
+                                const uint32_t inf = sLinfo[l];
+                                const bool shR = bt1 == 2 && !(mx1 && l < 36);
+                                ip = sIS[shR ? 22 + 3 * ((inf >> 5) & 15) + ((inf >> 9) & 3) : (inf & 31)];
+                            }
+                            if (ip != 0xFF) {
+                                xv[0][k] = lv * sISR[ip][0];
+                                xv[1][k] = lv * sISR[ip][1];
+                            } else if (mext & 2) {
+                                xv[0][k] = (lv + rv) * isq;
+                                xv[1][k] = (lv - rv) * isq;
+                            }
                         }
                     }
                 }
 #pragma unroll
-                for (int i = 0; i < 9; i++) {
-                    const int l = lane + 64 * i;
-                    const int dst = (int)(linfo[l] >> 11);
-                    sBuf[(bt0 == 2 && !(mx0 && l < 36)) ? dst : l] = xv[0][i];
-                    if (nch == 2) sBuf[576 + ((bt1 == 2 && !(mx1 && l < 36)) ? dst : l)] = xv[1][i];
+                for (int i = 0; i < 5; i++) {
+                    if (i < 4 || lane < 32) {
+                        const int l0 = 2 * lane + 128 * i;
+                        const uint2 inf2 = *(const uint2 *)&sLinfo[l0];
+#pragma unroll
+                        for (int e = 0; e < 2; e++) {
+                            const int l = l0 + e;
+                            const int dst = (int)((e ? inf2.y : inf2.x) >> 11);
+                            sBuf[(bt0 == 2 && !(mx0 && l < 36)) ? dst : l] = xv[0][2 * i + e];
+                            if (nch == 2) sBuf[576 + ((bt1 == 2 && !(mx1 && l < 36)) ? dst : l)] = xv[1][2 * i + e];
+                        }
+                    }
                 }
             }
-            __syncthreads();
+            wave_sync();
             /* ---------------- phase I: alias + IMDCT + overlap ------------ */
             const int bt = ch ? bt1 : bt0, mixed = ch ? mx1 : mx0;
             float o18[18];
@@ -867,13 +917,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
                     }
                 }
             }
-            __syncthreads(); /* every lane has read its xr before S overwrites it */
+            wave_sync(); /* every lane has read its xr before S overwrites it */
             {
                 const int sw = opaque(18 * ch * SROW + sb);
 #pragma unroll
                 for (int t = 0; t < 18; t++) sBuf[sw + t * SROW] = ((sb & 1) && (t & 1)) ? -o18[t] : o18[t];
             }
-            __syncthreads();
+            wave_sync();
             /* ---------------- phase M: matrixing on the matrix cores ------- */
             {
                 const int q = lane >> 4, r16 = lane & 15;
@@ -909,7 +959,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
 #pragma unroll
                         for (int mt = 0; mt < 2; mt++)
                             acc[nt][mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[mt][ks], Bf[nt][ks], acc[nt][mt], 0, 0, 0);
-                __syncthreads(); /* all S reads retired before X overwrites them */
+                wave_sync(); /* all S reads retired before X overwrites them */
                 /* D[row m = 16 mt + 4 q + r][col n] -> X[n][m] */
 #pragma unroll
                 for (int nt = 0; nt < 3; nt++) {
@@ -919,7 +969,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
                         for (int mt = 0; mt < 2; mt++) *(f32x4 *)&sBuf[n * 32 + 16 * mt + 4 * q] = acc[nt][mt];
                 }
             }
-            __syncthreads();
+            wave_sync();
             /* ---------------- phase W: 512-tap window -> PCM --------------- */
             {
                 float Dw[16];
@@ -955,7 +1005,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
 #pragma unroll
                 for (int k = 0; k < 15; k++) hb[k] = active ? xb[k + 3] : hb[k];
             }
-            __syncthreads(); /* X reads done before the next granule's xr */
+            wave_sync(); /* X reads done before the next granule's xr */
         }
     }
     /* state out */
