@@ -23,11 +23,11 @@
 namespace mp3d {
 hipError_t upload_constants(const float *, const float *, const float *, const float *, const float *, const float *,
                             const float *);
-void launch_scan(const uint8_t *, const uint64_t *, const uint32_t *, StreamState *, FrameRec *, int32_t *, void *, int,
-                 int, hipStream_t);
+void launch_scan(const uint8_t *, const uint64_t *, const uint32_t *, StreamState *, FrameRec *, uint64_t *, int32_t *,
+                 void *, int, int, hipStream_t);
 void launch_gather(const uint8_t *, uint8_t *, const uint64_t *, StreamState *, const FrameRec *, const int32_t *, int,
                    int, hipStream_t);
-void launch_huffman(const uint8_t *, const uint8_t *, const uint64_t *, const FrameRec *, const DevTables *, int16_t *,
+void launch_huffman(const uint8_t *, const uint64_t *, const FrameRec *, const uint64_t *, const DevTables *, int16_t *,
                     UnitMeta *, int, int, int, hipStream_t);
 void launch_synth(const FrameRec *, const int16_t *, const UnitMeta *, const DevTables *, StreamState *, int16_t *, int,
                   int, hipStream_t);
@@ -237,6 +237,7 @@ struct mp3d_batch {
     hipStream_t own = nullptr;
     StreamState *st = nullptr;
     FrameRec *rec = nullptr;
+    uint64_t *sideu = nullptr; /* per-unit side info (k_scan -> k_huffman) */
     int16_t *is_buf = nullptr;
     UnitMeta *meta = nullptr;
     int32_t *carry = nullptr;
@@ -302,6 +303,7 @@ extern "C" int mp3d_batch_create(int device, int max_streams, int max_frames, mp
     } while (0)
     BALLOC(b->st, sizeof(StreamState) * max_streams);
     BALLOC(b->rec, sizeof(FrameRec) * (size_t)max_streams * max_frames);
+    BALLOC(b->sideu, sizeof(uint64_t) * units);
     BALLOC(b->is_buf, sizeof(int16_t) * 576 * units);
     BALLOC(b->meta, sizeof(UnitMeta) * units);
     BALLOC(b->carry, sizeof(int32_t) * 2 * max_streams);
@@ -327,7 +329,7 @@ extern "C" void mp3d_batch_destroy(mp3d_batch *b) {
     if (!b) return;
     (void)hipSetDevice(b->device);
     if (b->own) (void)hipStreamSynchronize(b->own);
-    void *ptrs[] = {b->st, b->rec, b->is_buf, b->meta, b->carry, b->d_in_off, b->d_md_off, b->d_in_len,
+    void *ptrs[] = {b->st, b->rec, b->sideu, b->is_buf, b->meta, b->carry, b->d_in_off, b->d_md_off, b->d_in_len,
                     b->d_infos, b->md, b->d_in, b->d_pcm, b->d_xr, b->d_bt, b->d_mx};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
@@ -415,11 +417,11 @@ static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offse
     if (r) return r;
     DeviceCtx &dc = g_dev[b->device];
     if (b->timing) HIPCHK(hipEventRecord(b->ev[0], s));
-    launch_scan(din, b->d_in_off, b->d_in_len, b->st, b->rec, b->carry, b->d_infos, n, F, s);
+    launch_scan(din, b->d_in_off, b->d_in_len, b->st, b->rec, b->sideu, b->carry, b->d_infos, n, F, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[1], s));
     launch_gather(din, b->md, b->d_md_off, b->st, b->rec, b->carry, n, F, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[2], s));
-    launch_huffman(din, b->md, b->d_md_off, b->rec, dc.tables, b->is_buf, b->meta, n, F, dc.n_cu, s);
+    launch_huffman(b->md, b->d_md_off, b->rec, b->sideu, dc.tables, b->is_buf, b->meta, n, F, dc.n_cu, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[3], s));
     HIPCHK(hipGetLastError());
     return MP3D_OK;

@@ -72,8 +72,9 @@ __device__ __forceinline__ uint32_t side_unit_bit(int nch, int gr, int ch) {
 /* ------------------------------------------------------------------------ */
 __global__ void __launch_bounds__(256) k_scan(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
                                               const uint32_t *__restrict__ in_len, StreamState *__restrict__ st,
-                                              FrameRec *__restrict__ rec, int32_t *__restrict__ carry,
-                                              DevInfo *__restrict__ infos, int n_streams, int F) {
+                                              FrameRec *__restrict__ rec, uint64_t *__restrict__ sideu,
+                                              int32_t *__restrict__ carry, DevInfo *__restrict__ infos,
+                                              int n_streams, int F) {
     int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n_streams) return;
     const uint8_t *p0 = in + in_off[s];
@@ -126,10 +127,20 @@ __global__ void __launch_bounds__(256) k_scan(const uint8_t *__restrict__ in, co
             int p23[2][2] = {{0, 0}, {0, 0}};
             bool bad = plen < 0;
             for (int gr = 0; gr < 2; gr++)
-                for (int ch = 0; ch < nch; ch++) {
-                    uint32_t b = side_unit_bit(nch, gr, ch);
-                    p23[gr][ch] = (int)bits_at(side, b, 12);
-                    if (bits_at(side, b + 12, 9) > 288) bad = true; /* SURVEY A.9 (5) */
+                for (int ch = 0; ch < 2; ch++) {
+                    uint64_t sw = 0;
+                    if (ch < nch && !bad) {
+                        const uint32_t b = side_unit_bit(nch, gr, ch);
+                        p23[gr][ch] = (int)bits_at(side, b, 12);
+                        if (bits_at(side, b + 12, 9) > 288) bad = true; /* SURVEY A.9 (5) */
+                        /* the unit's 59 side-info bits, MSB first, from bit 63;
+                         * this channel's scfsi in bits 4..1 (k_huffman) */
+                        const uint64_t v = ((uint64_t)bits_at(side, b, 20) << 39) |
+                                           ((uint64_t)bits_at(side, b + 20, 20) << 19) | bits_at(side, b + 40, 19);
+                        const uint32_t scfsi = bits_at(side, 9 + (nch == 1 ? 5 : 3) + 4 * ch, 4);
+                        sw = (v << 5) | ((uint64_t)scfsi << 1);
+                    }
+                    sideu[((size_t)s * F + f) * 4 + gr * 2 + ch] = sw;
                 }
             if (tag) {
                 r.first_gr = REC_TAG;
@@ -201,109 +212,87 @@ __global__ void __launch_bounds__(256) k_gather(const uint8_t *__restrict__ in, 
     if (threadIdx.x == 0) st[s].res_len = cout;
 }
 
-/* ------------------------------------------------------------------------ */
-/* Bit reader over a big-endian byte region read as 32-bit words.           */
-/* ------------------------------------------------------------------------ */
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
-struct BitReader {
-    /* 96-bit window a:b:c of big-endian words; c is prefetched one word
-     * ahead so a refill's load latency hides behind ~32 bits of decode */
-    const uint32_t *w;
-    uint32_t pos, cw, a, b, c;
-    __device__ __forceinline__ void seek(uint32_t p) {
-        pos = p;
-        cw = p >> 5;
-        a = bswap32(w[cw]);
-        b = bswap32(w[cw + 1]);
-        c = bswap32(w[cw + 2]);
-    }
-    __device__ __forceinline__ uint32_t peek() const {
-        uint32_t sh = pos & 31;
-        return sh ? __builtin_amdgcn_alignbit(a, b, 32 - sh) : a;
-    }
-    __device__ __forceinline__ void skip(uint32_t n) {
-        pos += n;
-        uint32_t nw = pos >> 5;
-        if (nw != cw) {
-            if (nw == cw + 1) {
-                a = b;
-                b = c;
-                c = bswap32(w[nw + 2]);
-            } else {
-                a = nw == cw + 2 ? c : bswap32(w[nw]);
-                b = bswap32(w[nw + 1]);
-                c = bswap32(w[nw + 2]);
-            }
-            cw = nw;
-        }
-    }
-    __device__ __forceinline__ uint32_t get(int n) { /* 0 <= n <= 24 */
-        uint32_t v = n ? peek() >> (32 - n) : 0u;
-        skip((uint32_t)n);
-        return v;
-    }
-};
+/* ------------------------------------------------------------------------ */
+/* k_huffman: one lane per unit (ISO 2.4.2.7 + Annex B), 64 consecutive     */
+/* units (16 frames) per wave.  Each wave first stages its units' main-data */
+/* words into LDS (byte-swapped, one contiguous segment per lane, placed by */
+/* a wave prefix sum; segments that do not fit are decoded in a further    */
+/* batch), then decodes from LDS: a 96-bit window per codeword, two-level  */
+/* u16 LUT (15 code tables + count1 table A, LDS), and linbits + sign bits */
+/* taken from the same window, so the big_values loop is branch-free and   */
+/* runs max(big_values) iterations per wave whatever the region tables.     */
+/* Side info arrives pre-extracted by k_scan (one u64 per unit).            */
+/* ------------------------------------------------------------------------ */
+#define HUFF_WAVES 4
+#define HUFF_BLOCK (64 * HUFF_WAVES)
+#define HUFF_CAPW 2400 /* staged bitstream words per wave (9.6 KB)            */
 
-struct UnitSide {
-    int part2_3_length, big_values, global_gain, scalefac_compress, ws, block_type, mixed;
-    int table_select[3], sbg[3], region0_count, region1_count, preflag, scalefac_scale, c1sel;
-};
+/* One wave per data region: LDS operations of a wave complete in issue
+ * order, so an LDS hand-off between lanes of ONE wave only needs the
+ * compiler not to reorder across it -- no s_barrier and, unlike
+ * __syncthreads(), no vmcnt(0) drain of loads/stores still in flight.    */
+__device__ __forceinline__ void wave_sync() { __asm__ volatile("" ::: "memory"); }
 
-__device__ __forceinline__ void parse_unit(const uint8_t *side, int nch, int gr, int ch, UnitSide &u) {
-    uint32_t b = side_unit_bit(nch, gr, ch);
-    u.part2_3_length = (int)bits_at(side, b, 12);
-    u.big_values = (int)bits_at(side, b + 12, 9);
-    u.global_gain = (int)bits_at(side, b + 21, 8);
-    u.scalefac_compress = (int)bits_at(side, b + 29, 4);
-    u.ws = (int)bits_at(side, b + 33, 1);
-    if (u.ws) {
-        u.block_type = (int)bits_at(side, b + 34, 2);
-        u.mixed = (int)bits_at(side, b + 36, 1);
-        u.table_select[0] = (int)bits_at(side, b + 37, 5);
-        u.table_select[1] = (int)bits_at(side, b + 42, 5);
-        u.table_select[2] = 0;
-        u.sbg[0] = (int)bits_at(side, b + 47, 3);
-        u.sbg[1] = (int)bits_at(side, b + 50, 3);
-        u.sbg[2] = (int)bits_at(side, b + 53, 3);
-        u.region0_count = u.region1_count = 0;
-    } else {
-        u.block_type = 0;
-        u.mixed = 0;
-        u.table_select[0] = (int)bits_at(side, b + 34, 5);
-        u.table_select[1] = (int)bits_at(side, b + 39, 5);
-        u.table_select[2] = (int)bits_at(side, b + 44, 5);
-        u.region0_count = (int)bits_at(side, b + 49, 4);
-        u.region1_count = (int)bits_at(side, b + 53, 3);
-        u.sbg[0] = u.sbg[1] = u.sbg[2] = 0;
-    }
-    u.preflag = (int)bits_at(side, b + 56, 1);
-    u.scalefac_scale = (int)bits_at(side, b + 57, 1);
-    u.c1sel = (int)bits_at(side, b + 58, 1);
+/* 64 bits of a staged (big-endian word) bitstream starting at bit pos */
+__device__ __forceinline__ void win64(const uint32_t *bits, uint32_t pos, uint32_t &hi, uint32_t &lo) {
+    uint32_t w = pos >> 5;
+    w = w < HUFF_CAPW ? w : HUFF_CAPW;
+    const uint32_t sh = pos & 31;
+    const uint32_t w0 = bits[w], w1 = bits[w + 1], w2 = bits[w + 2];
+    hi = sh ? __builtin_amdgcn_alignbit(w0, w1, 32 - sh) : w0;
+    lo = sh ? __builtin_amdgcn_alignbit(w1, w2, 32 - sh) : w1;
+}
+__device__ __forceinline__ uint32_t win32(const uint32_t *bits, uint32_t pos) {
+    uint32_t w = pos >> 5;
+    w = w < HUFF_CAPW ? w : HUFF_CAPW;
+    const uint32_t sh = pos & 31;
+    const uint32_t w0 = bits[w], w1 = bits[w + 1];
+    return sh ? __builtin_amdgcn_alignbit(w0, w1, 32 - sh) : w0;
+}
+/* top 32 bits of (hi:lo) << n, 0 <= n <= 31 */
+__device__ __forceinline__ uint32_t shl64hi(uint32_t hi, uint32_t lo, uint32_t n) {
+    return n ? __builtin_amdgcn_alignbit(hi, lo, 32 - n) : hi;
 }
 
-/* Scalefactors (part 2), ISO 2.4.2.7, read in place: bands whose scfsi bit
- * is set keep the granule-0 values already in sf (layout as UnitMeta.sf). */
-__device__ __forceinline__ void read_scalefactors(BitReader &br, const UnitSide &u, int scfsi, uint8_t *sf) {
-    int slen1 = MP3D_SLEN[0][u.scalefac_compress], slen2 = MP3D_SLEN[1][u.scalefac_compress];
-    int j = 0;
-    if (u.ws && u.block_type == 2) {
-        int n = u.mixed ? 17 : 18;
-        for (int i = 0; i < n; i++) sf[j++] = (uint8_t)br.get(slen1);
-        for (int i = 0; i < 18; i++) sf[j++] = (uint8_t)br.get(slen2);
-        for (; j < 40; j++) sf[j] = 0;
-    } else {
-        for (int k = 0; k < 4; k++) {
-            int n = k == 0 ? 6 : 5;
-            int slen = k < 2 ? slen1 : slen2;
-            if (scfsi & (8 >> k)) {
-                j += n;
-            } else {
-                for (int i = 0; i < n; i++) sf[j++] = (uint8_t)br.get(slen);
-            }
-        }
-        for (; j < 40; j++) sf[j] = 0;
+/* cnt (<= 8) scalefactors of sl (<= 4) bits at pos -> sf[j..j+cnt) */
+__device__ __forceinline__ uint32_t sf_group(const uint32_t *bits, uint32_t pos, int cnt, int sl, uint8_t *sf, int j) {
+    uint32_t w = sl ? win32(bits, pos) : 0u;
+    for (int i = 0; i < cnt; i++) {
+        sf[j + i] = sl ? (uint8_t)(w >> (32 - sl)) : (uint8_t)0;
+        w <<= sl;
     }
+    return pos + (uint32_t)(cnt * sl);
+}
+
+/* Scalefactors (part 2), ISO 2.4.2.7, read in place: groups whose scfsi bit
+ * is set keep the granule-0 values already in sf (layout as UnitMeta.sf). */
+__device__ __forceinline__ uint32_t read_sf(const uint32_t *bits, uint32_t pos, uint64_t side, int scfsi, uint8_t *sf) {
+    const int sfc = (int)(side >> 31) & 15, ws = (int)(side >> 30) & 1;
+    const int bt = ws ? (int)(side >> 28) & 3 : 0, mixed = ws ? (int)(side >> 27) & 1 : 0;
+    const int slen1 = MP3D_SLEN[0][sfc], slen2 = MP3D_SLEN[1][sfc];
+    int j;
+    if (bt == 2) {
+        /* (mixed) 17 / 18 values of slen1 then 18 of slen2, in groups of 6 */
+        const int n1 = mixed ? 17 : 18;
+        pos = sf_group(bits, pos, 6, slen1, sf, 0);
+        pos = sf_group(bits, pos, 6, slen1, sf, 6);
+        pos = sf_group(bits, pos, n1 - 12, slen1, sf, 12);
+        j = n1;
+        pos = sf_group(bits, pos, 6, slen2, sf, j);
+        pos = sf_group(bits, pos, 6, slen2, sf, j + 6);
+        pos = sf_group(bits, pos, 6, slen2, sf, j + 12);
+        j += 18;
+    } else {
+        if (!(scfsi & 8)) pos = sf_group(bits, pos, 6, slen1, sf, 0);
+        if (!(scfsi & 4)) pos = sf_group(bits, pos, 5, slen1, sf, 6);
+        if (!(scfsi & 2)) pos = sf_group(bits, pos, 5, slen2, sf, 11);
+        if (!(scfsi & 1)) pos = sf_group(bits, pos, 5, slen2, sf, 16);
+        j = 21;
+    }
+    for (; j < 40; j++) sf[j] = 0;
+    return pos;
 }
 
 /* is[] row writer: words (2 x int16) are shifted through 4 registers and
@@ -339,170 +328,246 @@ struct RowWriter {
     }
 };
 
-/* ------------------------------------------------------------------------ */
-/* k_huffman: one thread per unit (ISO 2.4.2.7 + Annex B).  Two-level u16   */
-/* LUT (15 code tables + count1 table A, 14 KB) staged in LDS once per     */
-/* block; grid-strided so it is loaded ~2k times per call, not per 256 u. */
-/* ------------------------------------------------------------------------ */
-#define HUFF_BLOCK 256
-__global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restrict__ in, const uint8_t *__restrict__ md,
-                                                        const uint64_t *__restrict__ md_off,
+__global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restrict__ md, const uint64_t *__restrict__ md_off,
                                                         const FrameRec *__restrict__ rec,
+                                                        const uint64_t *__restrict__ sideu,
                                                         const DevTables *__restrict__ tab, int16_t *__restrict__ is_buf,
                                                         UnitMeta *__restrict__ meta, int n_units, int F) {
     __shared__ uint16_t s_lut[MP3D_LUT_MAX];
-    __shared__ uint8_t s_sf[HUFF_BLOCK][40];
+    __shared__ __attribute__((aligned(16))) uint32_t s_bits[HUFF_WAVES][HUFF_CAPW + 4];
+    __shared__ uint32_t s_tsel[32]; /* table_select -> LUT base | bits1 << 16 | linbits << 24, or 0xFFFFFFFF */
     const int lut_n = tab->lut_hdr.base[MP3D_LUT_TABLES - 1] + (1 << tab->lut_hdr.bits1[MP3D_LUT_TABLES - 1]);
     for (int i = threadIdx.x; i < (lut_n + 1) / 2; i += blockDim.x)
         ((uint32_t *)s_lut)[i] = ((const uint32_t *)tab->lut)[i];
+    if (threadIdx.x < 32) {
+        const int t = MP3D_HTAB_OF_SELECT[threadIdx.x];
+        s_tsel[threadIdx.x] = t < 0 ? 0xFFFFFFFFu
+                                    : (uint32_t)tab->lut_hdr.base[t] | ((uint32_t)tab->lut_hdr.bits1[t] << 16) |
+                                          ((uint32_t)MP3D_LINBITS[threadIdx.x] << 24);
+    }
     __syncthreads();
-    uint8_t *sf = s_sf[threadIdx.x];
-    for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < n_units; u += gridDim.x * blockDim.x) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t *bits = s_bits[wv];
+    const uint32_t qbase = tab->lut_hdr.base[MP3D_LUT_TABLES - 1];
+    const int qb1 = tab->lut_hdr.bits1[MP3D_LUT_TABLES - 1];
+    const int n_chunks = (n_units + 63) >> 6;
+
+    for (int chunk = blockIdx.x * HUFF_WAVES + wv; chunk < n_chunks; chunk += gridDim.x * HUFF_WAVES) {
+        const int u = chunk * 64 + lane;
         const int fr = u >> 2, gr = (u >> 1) & 1, ch = u & 1;
-        const FrameRec r = rec[fr];
-        if (!r.frame_bytes || (r.first_gr & (REC_TAG | REC_DROP)) || ch >= r.nch) continue;
-        const int s = fr / F;
-        const int nch = r.nch;
-        const uint8_t *side = in + r.frame_off + r.side_off;
-        UnitSide us;
-        parse_unit(side, nch, gr, ch, us);
-        RowWriter rw;
-        rw.out = is_buf + (size_t)u * 576;
-        rw.nw = 0;
-        rw.w0 = rw.w1 = rw.w2 = rw.w3 = 0u;
-        const int first_gr = r.first_gr;
-        uint32_t start = r.md_bit;
-        for (int g = first_gr; g < 2; g++)
-            for (int c = 0; c < nch; c++)
-                if (g < gr || (g == gr && c < ch)) start += bits_at(side, side_unit_bit(nch, g, c), 12);
-        BitReader br;
-        br.w = (const uint32_t *)(md + md_off[s]);
-        uint32_t used = 0;
-        if (gr < first_gr) {
-            for (int i = 0; i < 40; i++) sf[i] = 0;
-        } else {
-            int scfsi = gr == 1 ? (int)bits_at(side, 9 + (nch == 1 ? 5 : 3) + 4 * ch, 4) : 0;
-            const bool long_blk = !(us.ws && us.block_type == 2);
-            if (!long_blk) scfsi = 0;
-            if (scfsi && first_gr == 0) {
-                /* scfsi reuse: decode granule 0's scalefactors of this channel
-                 * into sf first, then read granule 1's over them in place */
-                UnitSide u0;
-                parse_unit(side, nch, 0, ch, u0);
-                uint32_t s0 = r.md_bit;
-                for (int c = 0; c < ch; c++) s0 += bits_at(side, side_unit_bit(nch, 0, c), 12);
-                br.seek(s0);
-                read_scalefactors(br, u0, 0, sf);
-            } else if (scfsi) {
-                for (int i = 0; i < 40; i++) sf[i] = 0;
-            }
-            br.seek(start);
-            read_scalefactors(br, us, scfsi, sf);
-            /* big_values: region boundaries (ISO 2.4.2.7; FFmpeg clamp) */
-            const int bv2 = us.big_values * 2;
-            int r1, r2;
-            if (us.ws) {
-                r1 = 36;
-                r2 = 576;
-            } else {
-                int b1 = us.region0_count + 1, b2 = us.region0_count + us.region1_count + 2;
-                if (b2 > 22) b2 = 22;
-                r1 = 0;
-                for (int i = 0; i < b1; i++) r1 += MP3D_SFB_LONG_WIDTH[r.sr_idx][i];
-                r2 = 0;
-                for (int i = 0; i < b2; i++) r2 += MP3D_SFB_LONG_WIDTH[r.sr_idx][i];
-            }
-            r1 = r1 < bv2 ? r1 : bv2;
-            r2 = r2 < bv2 ? r2 : bv2;
-            int k = 0;
-            for (int reg = 0; reg < 3; reg++) {
-                const int end = reg == 0 ? r1 : reg == 1 ? r2 : bv2;
-                const int sel = us.table_select[reg];
-                const int t = MP3D_HTAB_OF_SELECT[sel];
-                const int lin = MP3D_LINBITS[sel];
-                if (t < 0) {
-                    for (; k < end; k += 2) rw.push(0u);
-                    continue;
-                }
-                const uint32_t base = tab->lut_hdr.base[t];
-                const int b1 = tab->lut_hdr.bits1[t];
-                for (; k < end; k += 2) {
-                    const uint32_t pk = br.peek();
-                    uint32_t e = s_lut[base + (pk >> (32 - b1))];
-                    if (e & 0x8000u) {
-                        const uint32_t nb = (e >> 11) & 15u;
-                        e = s_lut[base + ((e & 0x7FFu) << 1) + ((pk << b1) >> (32 - nb))];
-                    }
-                    int x = (e >> 4) & 15, y = e & 15;
-                    br.skip((e >> 8) & 31u);
-                    if (lin) {
-                        if (x == 15) x += (int)br.get(lin);
-                        if (x && br.get(1)) x = -x;
-                        if (y == 15) y += (int)br.get(lin);
-                        if (y && br.get(1)) y = -y;
-                    } else {
-                        /* no linbits: both sign bits are adjacent */
-                        const int nsb = (x != 0) + (y != 0);
-                        const uint32_t sb = br.get(nsb);
-                        if (y && (sb & 1)) y = -y;
-                        if (x && ((sb >> (y != 0)) & 1)) x = -x;
-                    }
-                    rw.push((uint32_t)(uint16_t)x | ((uint32_t)(uint16_t)y << 16));
-                }
-            }
-            /* count1 quadruples until part2_3 end; a quadruple that overreads
-             * it is discarded (FFmpeg huffman_decode) */
-            const uint32_t end_bit = start + (uint32_t)us.part2_3_length;
-            const uint32_t qbase = tab->lut_hdr.base[MP3D_LUT_TABLES - 1];
-            const int qb1 = tab->lut_hdr.bits1[MP3D_LUT_TABLES - 1];
-            while (k <= 572 && br.pos < end_bit) {
-                const uint32_t save = br.pos;
-                const uint32_t pk = br.peek();
-                int v, len;
-                if (us.c1sel) {
-                    v = 15 - (int)(pk >> 28);
-                    len = 4;
-                } else {
-                    const uint32_t e = s_lut[qbase + (pk >> (32 - qb1))];
-                    v = e & 15;
-                    len = (e >> 8) & 31;
-                }
-                /* the code and its sign bits are both inside the 32-bit peek
-                 * window (<= 6 + 4 bits), so decode signs without refills */
-                const int ns = __builtin_popcount(v);
-                const uint32_t sb = (pk << len) >> (32 - (ns ? ns : 1));
-                int bit = ns;
-                int q0 = (v >> 3) & 1, q1 = (v >> 2) & 1, q2 = (v >> 1) & 1, q3 = v & 1;
-                if (q0) { bit--; if ((sb >> bit) & 1) q0 = -1; }
-                if (q1) { bit--; if ((sb >> bit) & 1) q1 = -1; }
-                if (q2) { bit--; if ((sb >> bit) & 1) q2 = -1; }
-                if (q3) { bit--; if ((sb >> bit) & 1) q3 = -1; }
-                if (save + (uint32_t)(len + ns) > end_bit) break; /* overread: discard */
-                br.skip((uint32_t)(len + ns));
-                rw.push((uint32_t)(uint16_t)q0 | ((uint32_t)(uint16_t)q1 << 16));
-                rw.push((uint32_t)(uint16_t)q2 | ((uint32_t)(uint16_t)q3 << 16));
-                k += 4;
-            }
-            used = br.pos - start;
+        bool valid = u < n_units;
+        FrameRec r;
+        uint64_t side = 0;
+        if (valid) {
+            r = rec[fr];
+            valid = r.frame_bytes && !(r.first_gr & (REC_TAG | REC_DROP)) && ch < r.nch;
+            side = sideu[u];
         }
-        const int nz_end = 2 * rw.nw;
-        rw.finish();
-        UnitMeta m;
+        const int first_gr = valid ? (r.first_gr & 3) : 0;
+        const bool dec = valid && gr >= first_gr;
+        const uint32_t p23 = dec ? (uint32_t)(side >> 52) : 0u;
+        /* unit start = md_bit + part2_3 lengths of the frame's earlier units
+         * (lanes 4k .. 4k+3 hold one frame: exclusive sum within the quad) */
+        uint32_t before = 0, before_g0 = 0;
 #pragma unroll
-        for (int i = 0; i < 10; i++) ((uint32_t *)m.sf)[i] = ((const uint32_t *)sf)[i];
-        m.global_gain = (uint8_t)us.global_gain;
-        m.block_type = (uint8_t)(us.ws ? us.block_type : 0);
-        m.mixed = (uint8_t)(us.ws && us.block_type == 2 ? us.mixed : 0);
-        m.scalefac_scale = (uint8_t)us.scalefac_scale;
-        m.preflag = (uint8_t)us.preflag;
-        m.sbg[0] = (uint8_t)us.sbg[0];
-        m.sbg[1] = (uint8_t)us.sbg[1];
-        m.sbg[2] = (uint8_t)us.sbg[2];
-        m.nz_end = (uint16_t)nz_end;
-        m.part2_3_length = (uint16_t)(gr < first_gr ? 0 : us.part2_3_length);
-        m.used_bits = (uint16_t)used;
-        m.pad_ = (uint16_t)(gr < first_gr);
-        meta[u] = m;
+        for (int q = 1; q < 4; q++) {
+            const uint32_t v = __shfl(p23, (lane & ~3) + q - 1);
+            if ((lane & 3) >= q) before += v;
+        }
+        {   /* granule-0 units of this frame preceding (gr 0, ch) */
+            const uint32_t v0 = __shfl(p23, lane & ~3);
+            before_g0 = ch ? v0 : 0u;
+        }
+        const uint32_t start = dec ? r.md_bit + before : 0u;
+        const int scfsi_raw = (int)(side >> 1) & 15;
+        const bool long_blk = !(((side >> 30) & 1) && ((side >> 28) & 3) == 2);
+        const int scfsi = (gr == 1 && long_blk) ? scfsi_raw : 0;
+        const bool need_g0 = dec && scfsi && first_gr == 0;
+        const uint32_t g0_start = r.md_bit + before_g0;
+        const uint32_t lo_bit = need_g0 ? g0_start : start;
+        const uint32_t w0 = lo_bit >> 5;
+        /* words [w0, w0 + len): through the unit end + 2 words of window
+         * margin, rounded to 4 words (16-B LDS stores) */
+        const uint32_t len = dec ? ((((start + p23 + 31) >> 5) + 2 - w0 + 3) & ~3u) : 0u;
+        uint32_t incl = len;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(incl, o);
+            if (lane >= o) incl += t;
+        }
+        const uint32_t off = incl - len;
+        const uint32_t *src = (const uint32_t *)(md + (dec ? md_off[fr / F] : 0)) + w0;
+
+        bool pending = dec;
+        while (__ballot(pending)) {
+            uint32_t mo = pending ? off : 0xFFFFFFFFu;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) mo = min(mo, (uint32_t)__shfl_xor(mo, o));
+            const uint32_t base = mo;
+            const bool inb = pending && off + len - base <= HUFF_CAPW;
+            wave_sync();
+            /* stage: each lane copies its own segment, 4 x 16 B in flight */
+            if (inb) {
+                uint32_t *dst = bits + (off - base);
+                for (uint32_t i = 0; i < len; i += 16) {
+                    uint4 v[4];
+#pragma unroll
+                    for (int k = 0; k < 4; k++)
+                        if (i + 4 * k < len) v[k] = *(const uint4 *)(src + i + 4 * k);
+#pragma unroll
+                    for (int k = 0; k < 4; k++)
+                        if (i + 4 * k < len)
+                            *(uint4 *)(dst + i + 4 * k) =
+                                make_uint4(bswap32(v[k].x), bswap32(v[k].y), bswap32(v[k].z), bswap32(v[k].w));
+                }
+            }
+            wave_sync();
+            if (inb) {
+                /* scalefactors go straight to the output record */
+                uint8_t *sf = meta[u].sf;
+                const uint32_t seg = 32u * (off - base) - 32u * w0; /* md bit -> staged bit */
+                uint32_t pos = start + seg;
+                if (need_g0) {
+                    /* scfsi reuse: granule 0's scalefactors of this channel
+                     * first, then granule 1's read over them in place */
+                    read_sf(bits, g0_start + seg, sideu[u - 2], 0, sf);
+                } else if (scfsi) {
+                    for (int i = 0; i < 40; i++) sf[i] = 0;
+                }
+                pos = read_sf(bits, pos, side, scfsi, sf);
+                /* big_values: region boundaries (ISO 2.4.2.7; FFmpeg clamp) */
+                const int ws = (int)(side >> 30) & 1;
+                const int bv2 = 2 * ((int)(side >> 43) & 0x1FF);
+                int r1, r2;
+                uint32_t ts0, ts1, ts2;
+                if (ws) {
+                    r1 = 36;
+                    r2 = 576;
+                    ts0 = s_tsel[(side >> 22) & 31];
+                    ts1 = s_tsel[(side >> 17) & 31];
+                    ts2 = ts1;
+                } else {
+                    const int rc0 = (int)(side >> 11) & 15, rc1 = (int)(side >> 8) & 7;
+                    int b1 = rc0 + 1, b2 = rc0 + rc1 + 2;
+                    if (b2 > 22) b2 = 22;
+                    r1 = 0;
+                    r2 = 0;
+                    for (int i = 0; i < b2; i++) {
+                        const int wdt = MP3D_SFB_LONG_WIDTH[r.sr_idx][i];
+                        r1 += i < b1 ? wdt : 0;
+                        r2 += wdt;
+                    }
+                    ts0 = s_tsel[(side >> 25) & 31];
+                    ts1 = s_tsel[(side >> 20) & 31];
+                    ts2 = s_tsel[(side >> 15) & 31];
+                }
+                r1 = r1 < bv2 ? r1 : bv2;
+                r2 = r2 < bv2 ? r2 : bv2;
+                RowWriter rw;
+                rw.out = is_buf + (size_t)u * 576;
+                rw.nw = 0;
+                rw.w0 = rw.w1 = rw.w2 = rw.w3 = 0u;
+                int k = 0;
+                for (; k < bv2; k += 2) {
+                    const uint32_t ts = k < r1 ? ts0 : (k < r2 ? ts1 : ts2);
+                    const bool zt = ts == 0xFFFFFFFFu; /* table 0: no bits, zeros */
+                    const uint32_t tb = ts & 0xFFFFu, b1 = zt ? 1u : (ts >> 16) & 15u, lin = zt ? 0u : ts >> 24;
+                    uint32_t hi, lo;
+                    win64(bits, pos, hi, lo);
+                    const uint32_t i1 = tb + (hi >> (32 - b1));
+                    const uint32_t e1 = s_lut[i1];
+                    const uint32_t nb = (e1 >> 11) & 15u;
+                    const uint32_t i2 = (e1 & 0x8000u) ? tb + ((e1 & 0x7FFu) << 1) + ((hi << b1) >> (32 - nb)) : i1;
+                    const uint32_t e = zt ? 0u : (uint32_t)s_lut[i2];
+                    const uint32_t x = (e >> 4) & 15u, y = e & 15u, len_c = (e >> 8) & 31u;
+                    /* linbits and signs follow the code: <= 28 bits, all in
+                     * the window (code <= 19 bits) */
+                    uint32_t rb = shl64hi(hi, lo, len_c);
+                    const uint32_t nx = x == 15u ? lin : 0u, ny = y == 15u ? lin : 0u;
+                    const uint32_t ex = nx ? rb >> (32 - nx) : 0u;
+                    rb <<= nx;
+                    const uint32_t sx = x != 0u, sgx = rb >> 31;
+                    rb <<= sx;
+                    const uint32_t ey = ny ? rb >> (32 - ny) : 0u;
+                    rb <<= ny;
+                    const uint32_t sy = y != 0u, sgy = rb >> 31;
+                    pos += len_c + nx + sx + ny + sy;
+                    int X = (int)(x + ex), Y = (int)(y + ey);
+                    X = (sx && sgx) ? -X : X;
+                    Y = (sy && sgy) ? -Y : Y;
+                    rw.push((uint32_t)(uint16_t)X | ((uint32_t)(uint16_t)Y << 16));
+                }
+                /* count1 quadruples until the part2_3 end; a quadruple that
+                 * overreads it is discarded (FFmpeg) */
+                const uint32_t end_bit = start + seg + p23;
+                const bool c1b = (side >> 5) & 1;
+                while (k <= 572 && pos < end_bit) {
+                    const uint32_t hw = win32(bits, pos);
+                    uint32_t v, lq;
+                    if (c1b) {
+                        v = 15u - (hw >> 28);
+                        lq = 4u;
+                    } else {
+                        const uint32_t e = s_lut[qbase + (hw >> (32 - qb1))];
+                        v = e & 15u;
+                        lq = (e >> 8) & 31u;
+                    }
+                    const uint32_t ns = __builtin_popcount(v);
+                    if (pos + lq + ns > end_bit) break;
+                    const uint32_t sbits = (hw << lq) >> (32 - (ns ? ns : 1));
+                    int bit = (int)ns;
+                    int q0 = (v >> 3) & 1, q1 = (v >> 2) & 1, q2 = (v >> 1) & 1, q3 = v & 1;
+                    if (q0) { bit--; if ((sbits >> bit) & 1) q0 = -1; }
+                    if (q1) { bit--; if ((sbits >> bit) & 1) q1 = -1; }
+                    if (q2) { bit--; if ((sbits >> bit) & 1) q2 = -1; }
+                    if (q3) { bit--; if ((sbits >> bit) & 1) q3 = -1; }
+                    pos += lq + ns;
+                    rw.push((uint32_t)(uint16_t)q0 | ((uint32_t)(uint16_t)q1 << 16));
+                    rw.push((uint32_t)(uint16_t)q2 | ((uint32_t)(uint16_t)q3 << 16));
+                    k += 4;
+                }
+                const int nz_end = 2 * rw.nw;
+                rw.finish();
+                UnitMeta m;
+                m.global_gain = (uint8_t)(side >> 35);
+                m.block_type = (uint8_t)(ws ? (side >> 28) & 3 : 0);
+                m.mixed = (uint8_t)(ws && ((side >> 28) & 3) == 2 ? (side >> 27) & 1 : 0);
+                m.scalefac_scale = (uint8_t)((side >> 6) & 1);
+                m.preflag = (uint8_t)((side >> 7) & 1);
+                m.sbg[0] = (uint8_t)(ws ? (side >> 14) & 7 : 0);
+                m.sbg[1] = (uint8_t)(ws ? (side >> 11) & 7 : 0);
+                m.sbg[2] = (uint8_t)(ws ? (side >> 8) & 7 : 0);
+                m.nz_end = (uint16_t)nz_end;
+                m.part2_3_length = (uint16_t)p23;
+                m.used_bits = (uint16_t)(pos - start - seg);
+                m.pad_ = 0;
+                /* everything after sf[40]: one 16-B store */
+                *(uint4 *)((uint8_t *)&meta[u] + 40) = *(const uint4 *)((const uint8_t *)&m + 40);
+            }
+            pending = pending && !inb;
+        }
+        if (valid && !dec) {
+            /* granule lost to a reservoir underflow: silence (FFmpeg) */
+            int16_t *out = is_buf + (size_t)u * 576;
+            for (int kk = 0; kk < 576; kk += 8) *(uint4 *)(out + kk) = make_uint4(0, 0, 0, 0);
+            UnitMeta m;
+#pragma unroll
+            for (int i = 0; i < 10; i++) ((uint32_t *)m.sf)[i] = 0u;
+            const int ws = (int)(side >> 30) & 1;
+            m.global_gain = (uint8_t)(side >> 35);
+            m.block_type = (uint8_t)(ws ? (side >> 28) & 3 : 0);
+            m.mixed = (uint8_t)(ws && ((side >> 28) & 3) == 2 ? (side >> 27) & 1 : 0);
+            m.scalefac_scale = (uint8_t)((side >> 6) & 1);
+            m.preflag = (uint8_t)((side >> 7) & 1);
+            m.sbg[0] = (uint8_t)(ws ? (side >> 14) & 7 : 0);
+            m.sbg[1] = (uint8_t)(ws ? (side >> 11) & 7 : 0);
+            m.sbg[2] = (uint8_t)(ws ? (side >> 8) & 7 : 0);
+            m.nz_end = 0;
+            m.part2_3_length = 0;
+            m.used_bits = 0;
+            m.pad_ = 1;
+            meta[u] = m;
+        }
     }
 }
 
@@ -599,11 +664,6 @@ __device__ __forceinline__ float pow2_quarter(int q) { /* 2^(q/4), exact table *
     return ldexpf(f, q >> 2);
 }
 
-/* One wave per workgroup: LDS operations of a wave complete in issue order,
- * so a phase hand-off through LDS only needs the compiler not to reorder
- * across it -- no s_barrier and, unlike __syncthreads(), no vmcnt(0) drain
- * of the global loads (prefetches) and PCM stores still in flight.      */
-__device__ __forceinline__ void wave_sync() { __asm__ volatile("" ::: "memory"); }
 
 template <bool SRC_XR>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
@@ -1034,9 +1094,9 @@ hipError_t upload_constants(const float *imdct12, const float *win36, const floa
 }
 
 void launch_scan(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len, StreamState *st, FrameRec *rec,
-                 int32_t *carry, void *infos, int n_streams, int F, hipStream_t strm) {
-    hipLaunchKernelGGL(k_scan, dim3((n_streams + 255) / 256), dim3(256), 0, strm, in, in_off, in_len, st, rec, carry,
-                       (DevInfo *)infos, n_streams, F);
+                 uint64_t *sideu, int32_t *carry, void *infos, int n_streams, int F, hipStream_t strm) {
+    hipLaunchKernelGGL(k_scan, dim3((n_streams + 255) / 256), dim3(256), 0, strm, in, in_off, in_len, st, rec, sideu,
+                       carry, (DevInfo *)infos, n_streams, F);
 }
 
 void launch_gather(const uint8_t *in, uint8_t *md, const uint64_t *md_off, StreamState *st, const FrameRec *rec,
@@ -1044,14 +1104,15 @@ void launch_gather(const uint8_t *in, uint8_t *md, const uint64_t *md_off, Strea
     hipLaunchKernelGGL(k_gather, dim3(n_streams), dim3(256), 0, strm, in, md, md_off, st, rec, carry, F);
 }
 
-void launch_huffman(const uint8_t *in, const uint8_t *md, const uint64_t *md_off, const FrameRec *rec,
+void launch_huffman(const uint8_t *md, const uint64_t *md_off, const FrameRec *rec, const uint64_t *sideu,
                     const DevTables *tab, int16_t *is_buf, UnitMeta *meta, int n_streams, int F, int n_cu,
                     hipStream_t strm) {
     int n_units = n_streams * F * 4;
-    int blocks = (n_units + HUFF_BLOCK - 1) / HUFF_BLOCK;
-    int cap = n_cu * 8;
+    int chunks = (n_units + 63) / 64;
+    int blocks = (chunks + HUFF_WAVES - 1) / HUFF_WAVES;
+    int cap = n_cu * 12;
     if (blocks > cap) blocks = cap;
-    hipLaunchKernelGGL(k_huffman, dim3(blocks), dim3(HUFF_BLOCK), 0, strm, in, md, md_off, rec, tab, is_buf, meta,
+    hipLaunchKernelGGL(k_huffman, dim3(blocks), dim3(HUFF_BLOCK), 0, strm, md, md_off, rec, sideu, tab, is_buf, meta,
                        n_units, F);
 }
 
