@@ -100,6 +100,7 @@ def main():
     import torch.distributed as dist
     import _gen
     import mp3_amd
+    from mp3_amd import shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -113,7 +114,7 @@ def main():
     # --- synthetic C3 shard of this rank (seed by global stream id) -------
     t0 = time.time()
     gen_threads = min(16, os.cpu_count() or 1)
-    buf, offs, sizes = _gen.batch(_gen.C3, 3_000_003 + rank * n, n, F, threads=gen_threads)
+    buf, offs, sizes = _gen.batch(_gen.C3, shard.shard_seed_base(rank, n), n, F, threads=gen_threads)
     log("rank %d: generated %d streams x %d frames (%.1f MB) in %.1fs" % (rank, n, F, buf.size / 1e6, time.time() - t0))
     d_in = torch.from_numpy(buf).to(dev)
     pcm = torch.empty((n, F, 2304), dtype=torch.int16, device=dev)
@@ -141,11 +142,7 @@ def main():
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    dt = shard.max_over_ranks(time.perf_counter() - t0, dev)
     frames_total = n * F * world * args.steps
     value = frames_total / dt
     ms_per_step = dt / args.steps * 1e3
@@ -179,11 +176,10 @@ def main():
     gather = None
     if args.gather and world > 1:
         # optional xGMI PCM gather to rank 0 (RCCL), timed apart from decode
-        out = [torch.empty_like(pcm) for _ in range(world)] if rank == 0 else None
         dist.barrier()
         torch.cuda.synchronize(dev)
         tg = time.perf_counter()
-        dist.gather(pcm, out, dst=0)
+        shard.gather_to_root(pcm)
         torch.cuda.synchronize(dev)
         gather = {"ms": (time.perf_counter() - tg) * 1e3, "bytes": pcm.numel() * 2 * world}
 

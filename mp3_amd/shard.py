@@ -1,0 +1,48 @@
+"""Stream sharding across ranks.
+
+Streams are independent, so rank r of W owns the contiguous global stream ids
+[r*n, (r+1)*n) and decodes them with no data-path collective (weak scaling:
+per-GPU work is fixed as W grows).  Synthetic inputs are seeded by global
+stream id, so a stream's bytes do not depend on W.  The optional PCM gather
+to rank 0 is a plain torch.distributed gather -- RCCL over xGMI with the
+"nccl" backend on MI355X, gloo on CPU -- and is timed apart from decode.
+"""
+import torch
+import torch.distributed as dist
+
+BASE_SEED_C3 = 3_000_003  # global stream g of the C3 workload uses seed BASE_SEED_C3 + g
+
+
+def shard_range(rank: int, n_per_rank: int):
+    """(first global stream id, count) owned by `rank`."""
+    return rank * n_per_rank, n_per_rank
+
+
+def shard_seed_base(rank: int, n_per_rank: int, base: int = BASE_SEED_C3) -> int:
+    """Seed of the rank's first stream (the generator adds the local index)."""
+    first, _ = shard_range(rank, n_per_rank)
+    return base + first
+
+
+def max_over_ranks(seconds: float, device=None) -> float:
+    """Job time = the slowest rank's time (identity when not distributed)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return seconds
+    t = torch.tensor([seconds], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_to_root(t: torch.Tensor, root: int = 0):
+    """Gather every rank's equally-shaped tensor to `root` (list there, None
+    elsewhere).  gloo has no 8/16-bit gather, so such tensors travel as int32
+    words there (PCM rows are 2304 int16 = 1152 words)."""
+    world, rank = dist.get_world_size(), dist.get_rank()
+    src = t.contiguous()
+    if dist.get_backend() == "gloo" and src.dtype in (torch.int16, torch.uint8, torch.int8):
+        src = src.view(torch.int32)
+    out = [torch.empty_like(src) for _ in range(world)] if rank == root else None
+    dist.gather(src, out, dst=root)
+    if out is not None:
+        out = [o.view(t.dtype) for o in out]
+    return out
