@@ -225,9 +225,9 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap
 /* runs max(big_values) iterations per wave whatever the region tables.     */
 /* Side info arrives pre-extracted by k_scan (one u64 per unit).            */
 /* ------------------------------------------------------------------------ */
-#define HUFF_WAVES 4
+#define HUFF_WAVES 16
 #define HUFF_BLOCK (64 * HUFF_WAVES)
-#define HUFF_CAPW 2400 /* staged bitstream words per wave (9.6 KB)            */
+#define HUFF_CAPW 2200 /* staged bitstream words per wave (8.8 KB)            */
 
 /* One wave per data region: LDS operations of a wave complete in issue
  * order, so an LDS hand-off between lanes of ONE wave only needs the
@@ -235,25 +235,25 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap
  * __syncthreads(), no vmcnt(0) drain of loads/stores still in flight.    */
 __device__ __forceinline__ void wave_sync() { __asm__ volatile("" ::: "memory"); }
 
-/* 64 bits of a staged (big-endian word) bitstream starting at bit pos */
+/* 64 bits of a staged (big-endian word) bitstream starting at bit pos;
+ * 64-bit funnel shifts keep it branch-free (sh = 0 included) */
 __device__ __forceinline__ void win64(const uint32_t *bits, uint32_t pos, uint32_t &hi, uint32_t &lo) {
     uint32_t w = pos >> 5;
     w = w < HUFF_CAPW ? w : HUFF_CAPW;
-    const uint32_t sh = pos & 31;
+    const uint32_t sh = 32u - (pos & 31u);
     const uint32_t w0 = bits[w], w1 = bits[w + 1], w2 = bits[w + 2];
-    hi = sh ? __builtin_amdgcn_alignbit(w0, w1, 32 - sh) : w0;
-    lo = sh ? __builtin_amdgcn_alignbit(w1, w2, 32 - sh) : w1;
+    hi = (uint32_t)((((uint64_t)w0 << 32) | w1) >> sh);
+    lo = (uint32_t)((((uint64_t)w1 << 32) | w2) >> sh);
 }
 __device__ __forceinline__ uint32_t win32(const uint32_t *bits, uint32_t pos) {
     uint32_t w = pos >> 5;
     w = w < HUFF_CAPW ? w : HUFF_CAPW;
-    const uint32_t sh = pos & 31;
     const uint32_t w0 = bits[w], w1 = bits[w + 1];
-    return sh ? __builtin_amdgcn_alignbit(w0, w1, 32 - sh) : w0;
+    return (uint32_t)((((uint64_t)w0 << 32) | w1) >> (32u - (pos & 31u)));
 }
-/* top 32 bits of (hi:lo) << n, 0 <= n <= 31 */
+/* top 32 bits of (hi:lo) << n, 0 <= n <= 32 */
 __device__ __forceinline__ uint32_t shl64hi(uint32_t hi, uint32_t lo, uint32_t n) {
-    return n ? __builtin_amdgcn_alignbit(hi, lo, 32 - n) : hi;
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (32u - n));
 }
 
 /* cnt (<= 8) scalefactors of sl (<= 4) bits at pos -> sf[j..j+cnt) */
@@ -268,10 +268,11 @@ __device__ __forceinline__ uint32_t sf_group(const uint32_t *bits, uint32_t pos,
 
 /* Scalefactors (part 2), ISO 2.4.2.7, read in place: groups whose scfsi bit
  * is set keep the granule-0 values already in sf (layout as UnitMeta.sf). */
-__device__ __forceinline__ uint32_t read_sf(const uint32_t *bits, uint32_t pos, uint64_t side, int scfsi, uint8_t *sf) {
+__device__ __forceinline__ uint32_t read_sf(const uint32_t *bits, uint32_t pos, uint64_t side, int scfsi, uint8_t *sf,
+                                            const uint8_t *slen) {
     const int sfc = (int)(side >> 31) & 15, ws = (int)(side >> 30) & 1;
     const int bt = ws ? (int)(side >> 28) & 3 : 0, mixed = ws ? (int)(side >> 27) & 1 : 0;
-    const int slen1 = MP3D_SLEN[0][sfc], slen2 = MP3D_SLEN[1][sfc];
+    const int slen1 = slen[sfc], slen2 = slen[16 + sfc];
     int j;
     if (bt == 2) {
         /* (mixed) 17 / 18 values of slen1 then 18 of slen2, in groups of 6 */
@@ -336,9 +337,20 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
     __shared__ uint16_t s_lut[MP3D_LUT_MAX];
     __shared__ __attribute__((aligned(16))) uint32_t s_bits[HUFF_WAVES][HUFF_CAPW + 4];
     __shared__ uint32_t s_tsel[32]; /* table_select -> LUT base | bits1 << 16 | linbits << 24, or 0xFFFFFFFF */
+    __shared__ uint16_t s_lbnd[3][24]; /* long sfb start line per sample rate (23 bounds)       */
+    __shared__ uint8_t s_slen[32];     /* MPEG-1 slen1 | slen2 per scalefac_compress          */
     const int lut_n = tab->lut_hdr.base[MP3D_LUT_TABLES - 1] + (1 << tab->lut_hdr.bits1[MP3D_LUT_TABLES - 1]);
     for (int i = threadIdx.x; i < (lut_n + 1) / 2; i += blockDim.x)
         ((uint32_t *)s_lut)[i] = ((const uint32_t *)tab->lut)[i];
+    if (threadIdx.x < 3) {
+        int acc = 0;
+        for (int i = 0; i < 22; i++) {
+            s_lbnd[threadIdx.x][i] = (uint16_t)acc;
+            acc += MP3D_SFB_LONG_WIDTH[threadIdx.x][i];
+        }
+        s_lbnd[threadIdx.x][22] = (uint16_t)acc;
+    }
+    if (threadIdx.x < 32) s_slen[threadIdx.x] = MP3D_SLEN[threadIdx.x >> 4][threadIdx.x & 15];
     if (threadIdx.x < 32) {
         const int t = MP3D_HTAB_OF_SELECT[threadIdx.x];
         s_tsel[threadIdx.x] = t < 0 ? 0xFFFFFFFFu
@@ -430,11 +442,11 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                 if (need_g0) {
                     /* scfsi reuse: granule 0's scalefactors of this channel
                      * first, then granule 1's read over them in place */
-                    read_sf(bits, g0_start + seg, sideu[u - 2], 0, sf);
+                    read_sf(bits, g0_start + seg, sideu[u - 2], 0, sf, s_slen);
                 } else if (scfsi) {
                     for (int i = 0; i < 40; i++) sf[i] = 0;
                 }
-                pos = read_sf(bits, pos, side, scfsi, sf);
+                pos = read_sf(bits, pos, side, scfsi, sf, s_slen);
                 /* big_values: region boundaries (ISO 2.4.2.7; FFmpeg clamp) */
                 const int ws = (int)(side >> 30) & 1;
                 const int bv2 = 2 * ((int)(side >> 43) & 0x1FF);
@@ -450,13 +462,8 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                     const int rc0 = (int)(side >> 11) & 15, rc1 = (int)(side >> 8) & 7;
                     int b1 = rc0 + 1, b2 = rc0 + rc1 + 2;
                     if (b2 > 22) b2 = 22;
-                    r1 = 0;
-                    r2 = 0;
-                    for (int i = 0; i < b2; i++) {
-                        const int wdt = MP3D_SFB_LONG_WIDTH[r.sr_idx][i];
-                        r1 += i < b1 ? wdt : 0;
-                        r2 += wdt;
-                    }
+                    r1 = s_lbnd[r.sr_idx][b1];
+                    r2 = s_lbnd[r.sr_idx][b2];
                     ts0 = s_tsel[(side >> 25) & 31];
                     ts1 = s_tsel[(side >> 20) & 31];
                     ts2 = s_tsel[(side >> 15) & 31];
@@ -476,8 +483,10 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                     win64(bits, pos, hi, lo);
                     const uint32_t i1 = tb + (hi >> (32 - b1));
                     const uint32_t e1 = s_lut[i1];
+                    /* second level, branch-free: i2 = i1 for a leaf */
                     const uint32_t nb = (e1 >> 11) & 15u;
-                    const uint32_t i2 = (e1 & 0x8000u) ? tb + ((e1 & 0x7FFu) << 1) + ((hi << b1) >> (32 - nb)) : i1;
+                    const uint32_t sub = ((e1 & 0x7FFu) << 1) + (uint32_t)((((uint64_t)hi << b1) & 0xFFFFFFFFull) >> (32u - nb));
+                    const uint32_t i2 = i1 + ((sub + tb - i1) & (0u - (e1 >> 15)));
                     const uint32_t e = zt ? 0u : (uint32_t)s_lut[i2];
                     const uint32_t x = (e >> 4) & 15u, y = e & 15u, len_c = (e >> 8) & 31u;
                     /* linbits and signs follow the code: <= 28 bits, all in
@@ -1110,7 +1119,7 @@ void launch_huffman(const uint8_t *md, const uint64_t *md_off, const FrameRec *r
     int n_units = n_streams * F * 4;
     int chunks = (n_units + 63) / 64;
     int blocks = (chunks + HUFF_WAVES - 1) / HUFF_WAVES;
-    int cap = n_cu * 12;
+    int cap = n_cu * 4;
     if (blocks > cap) blocks = cap;
     hipLaunchKernelGGL(k_huffman, dim3(blocks), dim3(HUFF_BLOCK), 0, strm, md, md_off, rec, sideu, tab, is_buf, meta,
                        n_units, F);
