@@ -225,9 +225,11 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap
 /* runs max(big_values) iterations per wave whatever the region tables.     */
 /* Side info arrives pre-extracted by k_scan (one u64 per unit).            */
 /* ------------------------------------------------------------------------ */
-#define HUFF_WAVES 16
+#define HUFF_WAVES 4
+#define HUFF_ROUNDS 4                    /* 64-unit rounds per super-chunk          */
+#define HUFF_SUPER (64 * HUFF_ROUNDS)    /* units ranked together by big_values     */
 #define HUFF_BLOCK (64 * HUFF_WAVES)
-#define HUFF_CAPW 2200 /* staged bitstream words per wave (8.8 KB)            */
+#define HUFF_CAPW 2400 /* staged bitstream words per wave (9.6 KB)            */
 
 /* One wave per data region: LDS operations of a wave complete in issue
  * order, so an LDS hand-off between lanes of ONE wave only needs the
@@ -336,12 +338,14 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                                                         UnitMeta *__restrict__ meta, int n_units, int F) {
     __shared__ uint16_t s_lut[MP3D_LUT_MAX];
     __shared__ __attribute__((aligned(16))) uint32_t s_bits[HUFF_WAVES][HUFF_CAPW + 4];
-    __shared__ uint32_t s_tsel[32]; /* table_select -> LUT base | bits1 << 16 | linbits << 24, or 0xFFFFFFFF */
+    __shared__ uint32_t s_tsel[32]; /* table_select -> LUT base | bits1 << 16 | linbits << 24 */
     __shared__ uint16_t s_lbnd[3][24]; /* long sfb start line per sample rate (23 bounds)       */
     __shared__ uint8_t s_slen[32];     /* MPEG-1 slen1 | slen2 per scalefac_compress          */
     const int lut_n = tab->lut_hdr.base[MP3D_LUT_TABLES - 1] + (1 << tab->lut_hdr.bits1[MP3D_LUT_TABLES - 1]);
+    const int zbase = (lut_n + 1) & ~1; /* 2-entry all-zero table for table_select 0, 4, 14 */
     for (int i = threadIdx.x; i < (lut_n + 1) / 2; i += blockDim.x)
         ((uint32_t *)s_lut)[i] = ((const uint32_t *)tab->lut)[i];
+    if (threadIdx.x == 0) ((uint32_t *)s_lut)[zbase / 2] = 0u;
     if (threadIdx.x < 3) {
         int acc = 0;
         for (int i = 0; i < 22; i++) {
@@ -353,7 +357,7 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
     if (threadIdx.x < 32) s_slen[threadIdx.x] = MP3D_SLEN[threadIdx.x >> 4][threadIdx.x & 15];
     if (threadIdx.x < 32) {
         const int t = MP3D_HTAB_OF_SELECT[threadIdx.x];
-        s_tsel[threadIdx.x] = t < 0 ? 0xFFFFFFFFu
+        s_tsel[threadIdx.x] = t < 0 ? (uint32_t)zbase | (1u << 16)
                                     : (uint32_t)tab->lut_hdr.base[t] | ((uint32_t)tab->lut_hdr.bits1[t] << 16) |
                                           ((uint32_t)MP3D_LINBITS[threadIdx.x] << 24);
     }
@@ -362,182 +366,241 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
     uint32_t *bits = s_bits[wv];
     const uint32_t qbase = tab->lut_hdr.base[MP3D_LUT_TABLES - 1];
     const int qb1 = tab->lut_hdr.bits1[MP3D_LUT_TABLES - 1];
-    const int n_chunks = (n_units + 63) >> 6;
+    const int n_super = (n_units + HUFF_SUPER - 1) / HUFF_SUPER;
 
-    for (int chunk = blockIdx.x * HUFF_WAVES + wv; chunk < n_chunks; chunk += gridDim.x * HUFF_WAVES) {
-        const int u = chunk * 64 + lane;
-        const int fr = u >> 2, gr = (u >> 1) & 1, ch = u & 1;
-        bool valid = u < n_units;
-        FrameRec r;
-        uint64_t side = 0;
-        if (valid) {
-            r = rec[fr];
-            valid = r.frame_bytes && !(r.first_gr & (REC_TAG | REC_DROP)) && ch < r.nch;
-            side = sideu[u];
-        }
-        const int first_gr = valid ? (r.first_gr & 3) : 0;
-        const bool dec = valid && gr >= first_gr;
-        const uint32_t p23 = dec ? (uint32_t)(side >> 52) : 0u;
-        /* unit start = md_bit + part2_3 lengths of the frame's earlier units
-         * (lanes 4k .. 4k+3 hold one frame: exclusive sum within the quad) */
-        uint32_t before = 0, before_g0 = 0;
+    for (int sc = blockIdx.x * HUFF_WAVES + wv; sc < n_super; sc += gridDim.x * HUFF_WAVES) {
+        /* ---- order the super-chunk's units by big_values, so each 64-unit
+         * round holds units of similar length (the big_values loop runs
+         * max-over-lanes iterations) */
+        const int ubase = sc * HUFF_SUPER;
+        uint32_t key[HUFF_ROUNDS];
 #pragma unroll
-        for (int q = 1; q < 4; q++) {
-            const uint32_t v = __shfl(p23, (lane & ~3) + q - 1);
-            if ((lane & 3) >= q) before += v;
+        for (int j = 0; j < HUFF_ROUNDS; j++) {
+            const int li = 64 * j + lane, u = ubase + li;
+            const uint32_t bv = u < n_units ? (uint32_t)(sideu[u] >> 43) & 0x1FFu : 0u;
+            key[j] = (bv << 9) | (uint32_t)li;
         }
-        {   /* granule-0 units of this frame preceding (gr 0, ch) */
-            const uint32_t v0 = __shfl(p23, lane & ~3);
-            before_g0 = ch ? v0 : 0u;
-        }
-        const uint32_t start = dec ? r.md_bit + before : 0u;
-        const int scfsi_raw = (int)(side >> 1) & 15;
-        const bool long_blk = !(((side >> 30) & 1) && ((side >> 28) & 3) == 2);
-        const int scfsi = (gr == 1 && long_blk) ? scfsi_raw : 0;
-        const bool need_g0 = dec && scfsi && first_gr == 0;
-        const uint32_t g0_start = r.md_bit + before_g0;
-        const uint32_t lo_bit = need_g0 ? g0_start : start;
-        const uint32_t w0 = lo_bit >> 5;
-        /* words [w0, w0 + len): through the unit end + 2 words of window
-         * margin, rounded to 4 words (16-B LDS stores) */
-        const uint32_t len = dec ? ((((start + p23 + 31) >> 5) + 2 - w0 + 3) & ~3u) : 0u;
-        uint32_t incl = len;
+        wave_sync();
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t t = __shfl_up(incl, o);
-            if (lane >= o) incl += t;
+        for (int j = 0; j < HUFF_ROUNDS; j++) bits[64 * j + lane] = key[j];
+        wave_sync();
+        uint32_t rank[HUFF_ROUNDS];
+#pragma unroll
+        for (int j = 0; j < HUFF_ROUNDS; j++) rank[j] = 0;
+        for (int i = 0; i < HUFF_SUPER; i += 4) {
+            const uint4 k4 = *(const uint4 *)&bits[i];
+#pragma unroll
+            for (int j = 0; j < HUFF_ROUNDS; j++)
+                rank[j] += (k4.x < key[j]) + (k4.y < key[j]) + (k4.z < key[j]) + (k4.w < key[j]);
         }
-        const uint32_t off = incl - len;
-        const uint32_t *src = (const uint32_t *)(md + (dec ? md_off[fr / F] : 0)) + w0;
+        wave_sync();
+#pragma unroll
+        for (int j = 0; j < HUFF_ROUNDS; j++) bits[HUFF_SUPER + rank[j]] = key[j] & 0x1FFu;
+        wave_sync();
+        int order[HUFF_ROUNDS];
+#pragma unroll
+        for (int j = 0; j < HUFF_ROUNDS; j++) order[j] = (int)bits[HUFF_SUPER + 64 * j + lane];
+        wave_sync();
 
-        bool pending = dec;
-        while (__ballot(pending)) {
-            uint32_t mo = pending ? off : 0xFFFFFFFFu;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) mo = min(mo, (uint32_t)__shfl_xor(mo, o));
-            const uint32_t base = mo;
-            const bool inb = pending && off + len - base <= HUFF_CAPW;
-            wave_sync();
-            /* stage: each lane copies its own segment, 4 x 16 B in flight */
-            if (inb) {
-                uint32_t *dst = bits + (off - base);
-                for (uint32_t i = 0; i < len; i += 16) {
-                    uint4 v[4];
-#pragma unroll
-                    for (int k = 0; k < 4; k++)
-                        if (i + 4 * k < len) v[k] = *(const uint4 *)(src + i + 4 * k);
-#pragma unroll
-                    for (int k = 0; k < 4; k++)
-                        if (i + 4 * k < len)
-                            *(uint4 *)(dst + i + 4 * k) =
-                                make_uint4(bswap32(v[k].x), bswap32(v[k].y), bswap32(v[k].z), bswap32(v[k].w));
-                }
+        for (int rd = 0; rd < HUFF_ROUNDS; rd++) {
+            const int u = ubase + order[rd];
+            const int fr = u >> 2, gr = (u >> 1) & 1, ch = u & 1;
+            bool valid = u < n_units;
+            FrameRec r;
+            uint64_t sq[4] = {0, 0, 0, 0};
+            if (valid) {
+                r = rec[fr];
+                valid = r.frame_bytes && !(r.first_gr & (REC_TAG | REC_DROP)) && ch < r.nch;
+                const ulonglong2 a = *(const ulonglong2 *)&sideu[u & ~3];
+                const ulonglong2 b = *(const ulonglong2 *)&sideu[(u & ~3) + 2];
+                sq[0] = a.x; sq[1] = a.y; sq[2] = b.x; sq[3] = b.y;
             }
-            wave_sync();
-            if (inb) {
-                /* scalefactors go straight to the output record */
-                uint8_t *sf = meta[u].sf;
-                const uint32_t seg = 32u * (off - base) - 32u * w0; /* md bit -> staged bit */
-                uint32_t pos = start + seg;
-                if (need_g0) {
-                    /* scfsi reuse: granule 0's scalefactors of this channel
-                     * first, then granule 1's read over them in place */
-                    read_sf(bits, g0_start + seg, sideu[u - 2], 0, sf, s_slen);
-                } else if (scfsi) {
-                    for (int i = 0; i < 40; i++) sf[i] = 0;
-                }
-                pos = read_sf(bits, pos, side, scfsi, sf, s_slen);
-                /* big_values: region boundaries (ISO 2.4.2.7; FFmpeg clamp) */
-                const int ws = (int)(side >> 30) & 1;
-                const int bv2 = 2 * ((int)(side >> 43) & 0x1FF);
-                int r1, r2;
-                uint32_t ts0, ts1, ts2;
-                if (ws) {
-                    r1 = 36;
-                    r2 = 576;
-                    ts0 = s_tsel[(side >> 22) & 31];
-                    ts1 = s_tsel[(side >> 17) & 31];
-                    ts2 = ts1;
-                } else {
-                    const int rc0 = (int)(side >> 11) & 15, rc1 = (int)(side >> 8) & 7;
-                    int b1 = rc0 + 1, b2 = rc0 + rc1 + 2;
-                    if (b2 > 22) b2 = 22;
-                    r1 = s_lbnd[r.sr_idx][b1];
-                    r2 = s_lbnd[r.sr_idx][b2];
-                    ts0 = s_tsel[(side >> 25) & 31];
-                    ts1 = s_tsel[(side >> 20) & 31];
-                    ts2 = s_tsel[(side >> 15) & 31];
-                }
-                r1 = r1 < bv2 ? r1 : bv2;
-                r2 = r2 < bv2 ? r2 : bv2;
-                RowWriter rw;
-                rw.out = is_buf + (size_t)u * 576;
-                rw.nw = 0;
-                rw.w0 = rw.w1 = rw.w2 = rw.w3 = 0u;
-                int k = 0;
-                for (; k < bv2; k += 2) {
-                    const uint32_t ts = k < r1 ? ts0 : (k < r2 ? ts1 : ts2);
-                    const bool zt = ts == 0xFFFFFFFFu; /* table 0: no bits, zeros */
-                    const uint32_t tb = ts & 0xFFFFu, b1 = zt ? 1u : (ts >> 16) & 15u, lin = zt ? 0u : ts >> 24;
-                    uint32_t hi, lo;
-                    win64(bits, pos, hi, lo);
-                    const uint32_t i1 = tb + (hi >> (32 - b1));
-                    const uint32_t e1 = s_lut[i1];
-                    /* second level, branch-free: i2 = i1 for a leaf */
-                    const uint32_t nb = (e1 >> 11) & 15u;
-                    const uint32_t sub = ((e1 & 0x7FFu) << 1) + (uint32_t)((((uint64_t)hi << b1) & 0xFFFFFFFFull) >> (32u - nb));
-                    const uint32_t i2 = i1 + ((sub + tb - i1) & (0u - (e1 >> 15)));
-                    const uint32_t e = zt ? 0u : (uint32_t)s_lut[i2];
-                    const uint32_t x = (e >> 4) & 15u, y = e & 15u, len_c = (e >> 8) & 31u;
-                    /* linbits and signs follow the code: <= 28 bits, all in
-                     * the window (code <= 19 bits) */
-                    uint32_t rb = shl64hi(hi, lo, len_c);
-                    const uint32_t nx = x == 15u ? lin : 0u, ny = y == 15u ? lin : 0u;
-                    const uint32_t ex = nx ? rb >> (32 - nx) : 0u;
-                    rb <<= nx;
-                    const uint32_t sx = x != 0u, sgx = rb >> 31;
-                    rb <<= sx;
-                    const uint32_t ey = ny ? rb >> (32 - ny) : 0u;
-                    rb <<= ny;
-                    const uint32_t sy = y != 0u, sgy = rb >> 31;
-                    pos += len_c + nx + sx + ny + sy;
-                    int X = (int)(x + ex), Y = (int)(y + ey);
-                    X = (sx && sgx) ? -X : X;
-                    Y = (sy && sgy) ? -Y : Y;
-                    rw.push((uint32_t)(uint16_t)X | ((uint32_t)(uint16_t)Y << 16));
-                }
-                /* count1 quadruples until the part2_3 end; a quadruple that
-                 * overreads it is discarded (FFmpeg) */
-                const uint32_t end_bit = start + seg + p23;
-                const bool c1b = (side >> 5) & 1;
-                while (k <= 572 && pos < end_bit) {
-                    const uint32_t hw = win32(bits, pos);
-                    uint32_t v, lq;
-                    if (c1b) {
-                        v = 15u - (hw >> 28);
-                        lq = 4u;
-                    } else {
-                        const uint32_t e = s_lut[qbase + (hw >> (32 - qb1))];
-                        v = e & 15u;
-                        lq = (e >> 8) & 31u;
+            const int first_gr = valid ? (r.first_gr & 3) : 0;
+            const int nch = valid ? r.nch : 1;
+            const bool dec = valid && gr >= first_gr;
+            const int q = u & 3;
+            const uint64_t side = sq[q];
+            const uint32_t p23 = dec ? (uint32_t)(side >> 52) : 0u;
+            /* unit start = md_bit + part2_3 lengths of the frame's earlier
+             * decoded units (gr >= first_gr, ch < nch) */
+            uint32_t before = 0;
+#pragma unroll
+            for (int qq = 0; qq < 3; qq++)
+                if (qq < q && (qq >> 1) >= first_gr && (qq & 1) < nch) before += (uint32_t)(sq[qq] >> 52);
+            const uint32_t start = dec ? r.md_bit + before : 0u;
+            const int scfsi_raw = (int)(side >> 1) & 15;
+            const bool long_blk = !(((side >> 30) & 1) && ((side >> 28) & 3) == 2);
+            const int scfsi = (gr == 1 && long_blk) ? scfsi_raw : 0;
+            const bool need_g0 = dec && scfsi && first_gr == 0;
+            const uint32_t g0_start = r.md_bit + (ch ? (uint32_t)(sq[0] >> 52) : 0u);
+            const uint32_t lo_bit = need_g0 ? g0_start : start;
+            const uint32_t w0 = lo_bit >> 5;
+            /* words [w0, w0 + len): through the unit end + 2 words of window
+             * margin, rounded to 4 words (16-B LDS stores) */
+            const uint32_t len = dec ? ((((start + p23 + 31) >> 5) + 2 - w0 + 3) & ~3u) : 0u;
+            uint32_t incl = len;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = __shfl_up(incl, o);
+                if (lane >= o) incl += t;
+            }
+            const uint32_t off = incl - len;
+            const uint32_t *src = (const uint32_t *)(md + (dec ? md_off[fr / F] : 0)) + w0;
+
+            bool pending = dec;
+            while (__ballot(pending)) {
+                uint32_t mo = pending ? off : 0xFFFFFFFFu;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) mo = min(mo, (uint32_t)__shfl_xor(mo, o));
+                const uint32_t base = mo;
+                const bool inb = pending && off + len - base <= HUFF_CAPW;
+                wave_sync();
+                /* stage: each lane copies its own segment, 4 x 16 B in flight */
+                if (inb) {
+                    uint32_t *dst = bits + (off - base);
+                    for (uint32_t i = 0; i < len; i += 16) {
+                        uint4 v[4];
+#pragma unroll
+                        for (int k = 0; k < 4; k++)
+                            if (i + 4 * k < len) v[k] = *(const uint4 *)(src + i + 4 * k);
+#pragma unroll
+                        for (int k = 0; k < 4; k++)
+                            if (i + 4 * k < len)
+                                *(uint4 *)(dst + i + 4 * k) =
+                                    make_uint4(bswap32(v[k].x), bswap32(v[k].y), bswap32(v[k].z), bswap32(v[k].w));
                     }
-                    const uint32_t ns = __builtin_popcount(v);
-                    if (pos + lq + ns > end_bit) break;
-                    const uint32_t sbits = (hw << lq) >> (32 - (ns ? ns : 1));
-                    int bit = (int)ns;
-                    int q0 = (v >> 3) & 1, q1 = (v >> 2) & 1, q2 = (v >> 1) & 1, q3 = v & 1;
-                    if (q0) { bit--; if ((sbits >> bit) & 1) q0 = -1; }
-                    if (q1) { bit--; if ((sbits >> bit) & 1) q1 = -1; }
-                    if (q2) { bit--; if ((sbits >> bit) & 1) q2 = -1; }
-                    if (q3) { bit--; if ((sbits >> bit) & 1) q3 = -1; }
-                    pos += lq + ns;
-                    rw.push((uint32_t)(uint16_t)q0 | ((uint32_t)(uint16_t)q1 << 16));
-                    rw.push((uint32_t)(uint16_t)q2 | ((uint32_t)(uint16_t)q3 << 16));
-                    k += 4;
                 }
-                const int nz_end = 2 * rw.nw;
-                rw.finish();
+                wave_sync();
+                if (inb) {
+                    /* scalefactors go straight to the output record */
+                    uint8_t *sf = meta[u].sf;
+                    const uint32_t seg = 32u * (off - base) - 32u * w0; /* md bit -> staged bit */
+                    uint32_t pos = start + seg;
+                    if (need_g0) {
+                        /* scfsi reuse: granule 0's scalefactors of this channel
+                         * first, then granule 1's read over them in place */
+                        read_sf(bits, g0_start + seg, sq[ch], 0, sf, s_slen);
+                    } else if (scfsi) {
+                        for (int i = 0; i < 40; i++) sf[i] = 0;
+                    }
+                    pos = read_sf(bits, pos, side, scfsi, sf, s_slen);
+                    /* big_values: region boundaries (ISO 2.4.2.7; FFmpeg clamp) */
+                    const int ws = (int)(side >> 30) & 1;
+                    const int bv2 = 2 * ((int)(side >> 43) & 0x1FF);
+                    int r1, r2;
+                    uint32_t ts0, ts1, ts2;
+                    if (ws) {
+                        r1 = 36;
+                        r2 = 576;
+                        ts0 = s_tsel[(side >> 22) & 31];
+                        ts1 = s_tsel[(side >> 17) & 31];
+                        ts2 = ts1;
+                    } else {
+                        const int rc0 = (int)(side >> 11) & 15, rc1 = (int)(side >> 8) & 7;
+                        const int b1 = rc0 + 1;
+                        int b2 = rc0 + rc1 + 2;
+                        if (b2 > 22) b2 = 22;
+                        r1 = s_lbnd[r.sr_idx][b1];
+                        r2 = s_lbnd[r.sr_idx][b2];
+                        ts0 = s_tsel[(side >> 25) & 31];
+                        ts1 = s_tsel[(side >> 20) & 31];
+                        ts2 = s_tsel[(side >> 15) & 31];
+                    }
+                    r1 = r1 < bv2 ? r1 : bv2;
+                    r2 = r2 < bv2 ? r2 : bv2;
+                    RowWriter rw;
+                    rw.out = is_buf + (size_t)u * 576;
+                    rw.nw = 0;
+                    rw.w0 = rw.w1 = rw.w2 = rw.w3 = 0u;
+                    int k = 0;
+                    for (; k < bv2; k += 2) {
+                        const uint32_t ts = k < r1 ? ts0 : (k < r2 ? ts1 : ts2);
+                        const uint32_t tb = ts & 0xFFFFu, b1 = (ts >> 16) & 15u, lin = ts >> 24;
+                        uint32_t hi, lo;
+                        win64(bits, pos, hi, lo);
+                        const uint32_t i1 = tb + (hi >> (32 - b1));
+                        const uint32_t e1 = s_lut[i1];
+                        /* second level, branch-free: i2 = i1 for a leaf */
+                        const uint32_t nb = (e1 >> 11) & 15u;
+                        const uint32_t sub =
+                            ((e1 & 0x7FFu) << 1) + (uint32_t)((((uint64_t)hi << b1) & 0xFFFFFFFFull) >> (32u - nb));
+                        const uint32_t i2 = i1 + ((sub + tb - i1) & (0u - (e1 >> 15)));
+                        const uint32_t e = s_lut[i2];
+                        const uint32_t x = (e >> 4) & 15u, y = e & 15u, len_c = (e >> 8) & 31u;
+                        /* linbits and signs follow the code: <= 28 bits, all in
+                         * the window (code <= 19 bits) */
+                        uint32_t rb = shl64hi(hi, lo, len_c);
+                        const uint32_t nx = x == 15u ? lin : 0u, ny = y == 15u ? lin : 0u;
+                        const uint32_t ex = nx ? rb >> (32 - nx) : 0u;
+                        rb <<= nx;
+                        const uint32_t sx = x != 0u, sgx = rb >> 31;
+                        rb <<= sx;
+                        const uint32_t ey = ny ? rb >> (32 - ny) : 0u;
+                        rb <<= ny;
+                        const uint32_t sy = y != 0u, sgy = rb >> 31;
+                        pos += len_c + nx + sx + ny + sy;
+                        int X = (int)(x + ex), Y = (int)(y + ey);
+                        X = (sx && sgx) ? -X : X;
+                        Y = (sy && sgy) ? -Y : Y;
+                        rw.push((uint32_t)(uint16_t)X | ((uint32_t)(uint16_t)Y << 16));
+                    }
+                    /* count1 quadruples until the part2_3 end; a quadruple that
+                     * overreads it is discarded (FFmpeg) */
+                    const uint32_t end_bit = start + seg + p23;
+                    const bool c1b = (side >> 5) & 1;
+                    while (k <= 572 && pos < end_bit) {
+                        const uint32_t hw = win32(bits, pos);
+                        uint32_t v, lq;
+                        if (c1b) {
+                            v = 15u - (hw >> 28);
+                            lq = 4u;
+                        } else {
+                            const uint32_t e = s_lut[qbase + (hw >> (32 - qb1))];
+                            v = e & 15u;
+                            lq = (e >> 8) & 31u;
+                        }
+                        const uint32_t ns = __builtin_popcount(v);
+                        if (pos + lq + ns > end_bit) break;
+                        const uint32_t sbits = (hw << lq) >> (32 - (ns ? ns : 1));
+                        int bit = (int)ns;
+                        int q0 = (v >> 3) & 1, q1 = (v >> 2) & 1, q2 = (v >> 1) & 1, q3 = v & 1;
+                        if (q0) { bit--; if ((sbits >> bit) & 1) q0 = -1; }
+                        if (q1) { bit--; if ((sbits >> bit) & 1) q1 = -1; }
+                        if (q2) { bit--; if ((sbits >> bit) & 1) q2 = -1; }
+                        if (q3) { bit--; if ((sbits >> bit) & 1) q3 = -1; }
+                        pos += lq + ns;
+                        rw.push((uint32_t)(uint16_t)q0 | ((uint32_t)(uint16_t)q1 << 16));
+                        rw.push((uint32_t)(uint16_t)q2 | ((uint32_t)(uint16_t)q3 << 16));
+                        k += 4;
+                    }
+                    const int nz_end = 2 * rw.nw;
+                    rw.finish();
+                    UnitMeta m;
+                    m.global_gain = (uint8_t)(side >> 35);
+                    m.block_type = (uint8_t)(ws ? (side >> 28) & 3 : 0);
+                    m.mixed = (uint8_t)(ws && ((side >> 28) & 3) == 2 ? (side >> 27) & 1 : 0);
+                    m.scalefac_scale = (uint8_t)((side >> 6) & 1);
+                    m.preflag = (uint8_t)((side >> 7) & 1);
+                    m.sbg[0] = (uint8_t)(ws ? (side >> 14) & 7 : 0);
+                    m.sbg[1] = (uint8_t)(ws ? (side >> 11) & 7 : 0);
+                    m.sbg[2] = (uint8_t)(ws ? (side >> 8) & 7 : 0);
+                    m.nz_end = (uint16_t)nz_end;
+                    m.part2_3_length = (uint16_t)p23;
+                    m.used_bits = (uint16_t)(pos - start - seg);
+                    m.pad_ = 0;
+                    /* everything after sf[40]: one 16-B store */
+                    *(uint4 *)((uint8_t *)&meta[u] + 40) = *(const uint4 *)((const uint8_t *)&m + 40);
+                }
+                pending = pending && !inb;
+            }
+            if (valid && !dec) {
+                /* granule lost to a reservoir underflow: silence (FFmpeg) */
+                int16_t *out = is_buf + (size_t)u * 576;
+                for (int kk = 0; kk < 576; kk += 8) *(uint4 *)(out + kk) = make_uint4(0, 0, 0, 0);
                 UnitMeta m;
+#pragma unroll
+                for (int i = 0; i < 10; i++) ((uint32_t *)m.sf)[i] = 0u;
+                const int ws = (int)(side >> 30) & 1;
                 m.global_gain = (uint8_t)(side >> 35);
                 m.block_type = (uint8_t)(ws ? (side >> 28) & 3 : 0);
                 m.mixed = (uint8_t)(ws && ((side >> 28) & 3) == 2 ? (side >> 27) & 1 : 0);
@@ -546,36 +609,12 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                 m.sbg[0] = (uint8_t)(ws ? (side >> 14) & 7 : 0);
                 m.sbg[1] = (uint8_t)(ws ? (side >> 11) & 7 : 0);
                 m.sbg[2] = (uint8_t)(ws ? (side >> 8) & 7 : 0);
-                m.nz_end = (uint16_t)nz_end;
-                m.part2_3_length = (uint16_t)p23;
-                m.used_bits = (uint16_t)(pos - start - seg);
-                m.pad_ = 0;
-                /* everything after sf[40]: one 16-B store */
-                *(uint4 *)((uint8_t *)&meta[u] + 40) = *(const uint4 *)((const uint8_t *)&m + 40);
+                m.nz_end = 0;
+                m.part2_3_length = 0;
+                m.used_bits = 0;
+                m.pad_ = 1;
+                meta[u] = m;
             }
-            pending = pending && !inb;
-        }
-        if (valid && !dec) {
-            /* granule lost to a reservoir underflow: silence (FFmpeg) */
-            int16_t *out = is_buf + (size_t)u * 576;
-            for (int kk = 0; kk < 576; kk += 8) *(uint4 *)(out + kk) = make_uint4(0, 0, 0, 0);
-            UnitMeta m;
-#pragma unroll
-            for (int i = 0; i < 10; i++) ((uint32_t *)m.sf)[i] = 0u;
-            const int ws = (int)(side >> 30) & 1;
-            m.global_gain = (uint8_t)(side >> 35);
-            m.block_type = (uint8_t)(ws ? (side >> 28) & 3 : 0);
-            m.mixed = (uint8_t)(ws && ((side >> 28) & 3) == 2 ? (side >> 27) & 1 : 0);
-            m.scalefac_scale = (uint8_t)((side >> 6) & 1);
-            m.preflag = (uint8_t)((side >> 7) & 1);
-            m.sbg[0] = (uint8_t)(ws ? (side >> 14) & 7 : 0);
-            m.sbg[1] = (uint8_t)(ws ? (side >> 11) & 7 : 0);
-            m.sbg[2] = (uint8_t)(ws ? (side >> 8) & 7 : 0);
-            m.nz_end = 0;
-            m.part2_3_length = 0;
-            m.used_bits = 0;
-            m.pad_ = 1;
-            meta[u] = m;
         }
     }
 }
@@ -1117,9 +1156,9 @@ void launch_huffman(const uint8_t *md, const uint64_t *md_off, const FrameRec *r
                     const DevTables *tab, int16_t *is_buf, UnitMeta *meta, int n_streams, int F, int n_cu,
                     hipStream_t strm) {
     int n_units = n_streams * F * 4;
-    int chunks = (n_units + 63) / 64;
-    int blocks = (chunks + HUFF_WAVES - 1) / HUFF_WAVES;
-    int cap = n_cu * 4;
+    int supers = (n_units + HUFF_SUPER - 1) / HUFF_SUPER;
+    int blocks = (supers + HUFF_WAVES - 1) / HUFF_WAVES;
+    int cap = n_cu * 12;
     if (blocks > cap) blocks = cap;
     hipLaunchKernelGGL(k_huffman, dim3(blocks), dim3(HUFF_BLOCK), 0, strm, md, md_off, rec, sideu, tab, is_buf, meta,
                        n_units, F);
