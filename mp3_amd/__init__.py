@@ -11,12 +11,13 @@ The compute path is the HIP library mp3_amd/libmp3d.so; there is no CPU
 fallback.  Importing works without a GPU; creating a decoder does not.
 """
 import ctypes
+import os
 import pathlib
 
 import numpy as np
 
 _HERE = pathlib.Path(__file__).resolve().parent
-LIB_PATH = _HERE / "libmp3d.so"
+LIB_PATH = pathlib.Path(os.environ["MP3D_LIB"]) if os.environ.get("MP3D_LIB") else _HERE / "libmp3d.so"
 
 MP3D_E = {0: "ok", -1: "bad argument", -2: "no usable HIP device", -3: "HIP runtime error", -4: "out of memory",
           -5: "batch exceeds handle capacity", -6: "no complete frame in buffer"}

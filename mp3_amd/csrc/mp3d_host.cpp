@@ -471,9 +471,15 @@ extern "C" int mp3d_batch_huffman_only(mp3d_batch *b, const uint8_t *frames, con
     if (!b) return MP3D_E_ARG;
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : b->own;
     bool sync_needed = false;
+    size_t units = (size_t)n * F * 4;
+    if (n > 0 && F > 0 && n <= b->max_streams && F <= b->max_frames) {
+        /* k_huffman stores only each row's nonzero prefix (nz_end); the tap
+         * returns whole rows, so clear them first */
+        HIPCHK(hipSetDevice(b->device));
+        HIPCHK(hipMemsetAsync(b->is_buf, 0, units * 576 * sizeof(int16_t), s));
+    }
     int r = run_front(b, frames, offsets, sizes, n, F, s, &sync_needed);
     if (r) return r;
-    size_t units = (size_t)n * F * 4;
     if (is_out) {
         hipMemcpyKind k = is_device_ptr(is_out) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
         HIPCHK(hipMemcpyAsync(is_out, b->is_buf, units * 576 * sizeof(int16_t), k, s));

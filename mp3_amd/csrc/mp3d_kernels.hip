@@ -312,22 +312,15 @@ struct RowWriter {
         nw++;
         if ((nw & 3) == 0) *(uint4 *)(out + 2 * (nw - 4)) = make_uint4(w0, w1, w2, w3);
     }
-    __device__ __forceinline__ void finish() { /* flush + rzero to 576 lines */
-        int r = nw & 3, k = 2 * (nw - r);
-        if (r == 3) {
-            *(uint32_t *)(out + k) = w1;
-            *(uint32_t *)(out + k + 2) = w2;
-            *(uint32_t *)(out + k + 4) = w3;
-            *(uint32_t *)(out + k + 6) = 0u;
-        } else if (r == 2) {
-            *(uint2 *)(out + k) = make_uint2(w2, w3);
-            *(uint2 *)(out + k + 4) = make_uint2(0u, 0u);
-        } else if (r == 1) {
-            *(uint32_t *)(out + k) = w3;
-            *(uint32_t *)(out + k + 2) = 0u;
-            *(uint2 *)(out + k + 4) = make_uint2(0u, 0u);
-        }
-        for (int kk = k + (r ? 8 : 0); kk < 576; kk += 8) *(uint4 *)(out + kk) = make_uint4(0, 0, 0, 0);
+    /* flush the last partial 16-B chunk.  Lines from 2 nw (UnitMeta.nz_end)
+     * to 575 are the rzero region: NOT stored (k_synth masks them), which
+     * removes ~2/3 of the row stores -- one row per lane is the slow,
+     * uncoalesced store pattern of this kernel. */
+    __device__ __forceinline__ void finish() {
+        const int r = nw & 3;
+        if (r == 3) *(uint4 *)(out + 2 * (nw - 3)) = make_uint4(w1, w2, w3, 0u);
+        else if (r == 2) *(uint2 *)(out + 2 * (nw - 2)) = make_uint2(w2, w3);
+        else if (r == 1) *(uint32_t *)(out + 2 * (nw - 1)) = w3;
     }
 };
 
@@ -387,6 +380,10 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
         uint32_t rank[HUFF_ROUNDS];
 #pragma unroll
         for (int j = 0; j < HUFF_ROUNDS; j++) rank[j] = 0;
+#ifdef HUFF_SKIP_SORT
+        for (int j = 0; j < HUFF_ROUNDS; j++) rank[j] = key[j] & 0x1FFu;
+        if (false)
+#endif
         for (int i = 0; i < HUFF_SUPER; i += 4) {
             const uint4 k4 = *(const uint4 *)&bits[i];
 #pragma unroll
@@ -456,7 +453,11 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                 const bool inb = pending && off + len - base <= HUFF_CAPW;
                 wave_sync();
                 /* stage: each lane copies its own segment, 4 x 16 B in flight */
+#ifdef HUFF_SKIP_STAGE
+                if (false) {
+#else
                 if (inb) {
+#endif
                     uint32_t *dst = bits + (off - base);
                     for (uint32_t i = 0; i < len; i += 16) {
                         uint4 v[4];
@@ -513,6 +514,9 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                     rw.nw = 0;
                     rw.w0 = rw.w1 = rw.w2 = rw.w3 = 0u;
                     int k = 0;
+#ifdef HUFF_SKIP_LOOPS
+                    k = 600;
+#endif
                     for (; k < bv2; k += 2) {
                         const uint32_t ts = k < r1 ? ts0 : (k < r2 ? ts1 : ts2);
                         const uint32_t tb = ts & 0xFFFFu, b1 = (ts >> 16) & 15u, lin = ts >> 24;
@@ -855,6 +859,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                  * for lanes < 32; xv[c][2 i + e] */
                 float xv[2][10];
                 uint64_t nzR = 0;
+                const int nz[2] = {sM[0].nz_end, nch == 2 ? sM[1].nz_end : 0};
 #pragma unroll
                 for (int i = 0; i < 5; i++) {
                     const int l0 = 2 * lane + 128 * i;
@@ -869,7 +874,8 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                         for (int c = 0; c < 2; c++) {
                             const int bt = c ? bt1 : bt0, mx = c ? mx1 : mx0;
                             const bool sh = bt == 2 && !(mx && l < 36);
-                            const int v = (int)(int16_t)(e ? (cis[c][i] >> 16) : (cis[c][i] & 0xFFFFu));
+                            int v = (int)(int16_t)(e ? (cis[c][i] >> 16) : (cis[c][i] & 0xFFFFu));
+                            v = l < nz[c] ? v : 0; /* rzero lines are not stored by k_huffman */
                             const int a = v < 0 ? -v : v;
                             float p = sP43[a < 16 ? a : 0];
                             if (a >= 16) p = tab->pow43[a];
