@@ -189,22 +189,44 @@ __global__ void __launch_bounds__(256) k_scan(const uint8_t *__restrict__ in, co
 
 /* ------------------------------------------------------------------------ */
 /* k_gather: one block per stream.  md region = [carry-in][payload 0][...]  */
-/* then the last `carry` bytes become the next call's carry-in.             */
+/* then the last `carry` bytes become the next call's carry-in.  Payloads   */
+/* are copied as aligned 32-bit destination words built from two aligned   */
+/* source words (alignbit) -- the byte offsets of a payload in the input  */
+/* and in md differ arbitrarily; the <= 3 edge bytes per side go as bytes  */
+/* (a neighbouring frame owns the rest of that word).  Wave w of the block */
+/* copies frames f = w mod 4.                                              */
 /* ------------------------------------------------------------------------ */
 __global__ void __launch_bounds__(256) k_gather(const uint8_t *__restrict__ in, uint8_t *__restrict__ md,
                                                 const uint64_t *__restrict__ md_off, StreamState *__restrict__ st,
                                                 const FrameRec *__restrict__ rec, const int32_t *__restrict__ carry,
                                                 int F) {
-    int s = blockIdx.x;
+    const int s = blockIdx.x;
     uint8_t *dst = md + md_off[s];
     const int cin = st[s].res_len;
-    for (int i = threadIdx.x; i < cin; i += blockDim.x) dst[i] = st[s].res[i];
-    for (int f = 0; f < F; f++) {
-        const FrameRec &r = rec[(size_t)s * F + f];
+    for (int i = threadIdx.x; i < (cin + 3) / 4; i += blockDim.x)
+        ((uint32_t *)dst)[i] = ((const uint32_t *)st[s].res)[i];
+    __syncthreads(); /* carry words may spill past cin into payload 0's head */
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int f = wv; f < F; f += 4) {
+        const FrameRec r = rec[(size_t)s * F + f];
         if (!r.frame_bytes || (r.first_gr & REC_TAG)) continue;
         const uint8_t *src = in + r.frame_off + r.side_off + (r.nch == 1 ? 17 : 32);
-        uint8_t *d = dst + r.payload_md;
-        for (int i = threadIdx.x; i < r.payload_len; i += blockDim.x) d[i] = src[i];
+        const uint32_t P = r.payload_md, L = r.payload_len;
+        const uint32_t h = min((4u - (P & 3u)) & 3u, L); /* head bytes up to an aligned word */
+        const uint32_t wb = (P + h) >> 2, we = (P + L) >> 2; /* whole words [wb, we) */
+        if ((uint32_t)lane < h) dst[P + lane] = src[lane];
+        const uint32_t t0 = wb > we ? 0u : 4u * we - P; /* tail bytes [t0, L) */
+        if (wb < we && (uint32_t)lane < L - t0) dst[P + t0 + lane] = src[t0 + lane];
+        if (wb < we) {
+            const uint64_t sa0 = (uint64_t)(src + (4u * wb - P));
+            const uint32_t sh = (uint32_t)(sa0 & 3u) * 8u;
+            const uint32_t *sw = (const uint32_t *)(sa0 & ~(uint64_t)3);
+            for (uint32_t w = lane; w < we - wb; w += 64) {
+                const uint32_t lo = sw[w];
+                const uint32_t v = sh ? __builtin_amdgcn_alignbit(sw[w + 1], lo, sh) : lo;
+                ((uint32_t *)dst)[wb + w] = v;
+            }
+        }
     }
     __syncthreads();
     const int cout = carry[2 * s], pend = carry[2 * s + 1];
@@ -723,7 +745,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
         const float *__restrict__ xr_in, const uint8_t *__restrict__ xr_bt, const uint8_t *__restrict__ xr_mixed,
         const DevTables *__restrict__ tab, StreamState *__restrict__ st, int16_t *__restrict__ pcm, int F, int xr_nch,
         int xr_sr) {
-    __shared__ float sBuf[SYN_BUF];
+    __shared__ __attribute__((aligned(16))) float sBuf[SYN_BUF];
     __shared__ uint32_t sLinfo[576]; /* tab->linfo[sr] of the current sample rate   */
     __shared__ float sScale[2][64];  /* 2^(q/4) per (ch, band idx): long b | 22 + 3 b + w */
     __shared__ uint8_t sIS[64];      /* intensity position per right-channel band idx, 0xFF none */
@@ -989,7 +1011,11 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                 if (long_imdct) {
                     const float *wv = sW[bt == 2 ? 0 : bt];
                     float w[18];
+#ifdef SYN_SKIP_I
+                    for (int i = 0; i < 18; i++) w[i] = x[i];
+#else
                     imdct36_w(x, w);
+#endif
 #pragma unroll
                     for (int i = 0; i < 9; i++) {
                         o18[i] = fmaf(w[9 + i], wv[i], ov[i]);
@@ -1039,48 +1065,56 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
             }
             wave_sync();
             /* ---------------- phase M: matrixing on the matrix cores ------- */
+            /* one butterfly level of the 32-point DCT-II (ISO Annex A matrixing):
+             *   X[2m]   = sum_i C[2m][i]   (S_i + S_31-i)
+             *   X[2m+1] = sum_i C[2m+1][i] (S_i - S_31-i),  i, m < 16
+             * = two 16x16 products: half the MFMAs of the dense 32x32.
+             * v_mfma_f32_16x16x4_f32, rows m, cols n = (ch, t), K order
+             * i = 4 q + ks (q = lane >> 4): a lane's 4 B values and their
+             * mirrors are two 16-B runs of an S row. */
             {
                 const int q = lane >> 4, r16 = lane & 15;
-                /* k = 4 ks + q <-> sb = 8 q + ks: each lane's 8 B values are
-                 * one contiguous 32-B run of an S row */
-                float Af[2][8];
-#pragma unroll
-                for (int mt = 0; mt < 2; mt++) {
-                    const float4 *src = (const float4 *)&tab->dct_c[16 * mt + r16][8 * q];
-                    const float4 a0 = src[0], a1 = src[1];
-                    Af[mt][0] = a0.x; Af[mt][1] = a0.y; Af[mt][2] = a0.z; Af[mt][3] = a0.w;
-                    Af[mt][4] = a1.x; Af[mt][5] = a1.y; Af[mt][6] = a1.z; Af[mt][7] = a1.w;
-                }
-                float Bf[3][8];
+                const float4 ae = *(const float4 *)&tab->dct_c[2 * r16][4 * q];
+                const float4 ao = *(const float4 *)&tab->dct_c[2 * r16 + 1][4 * q];
+                const float Ae[4] = {ae.x, ae.y, ae.z, ae.w}, Ao[4] = {ao.x, ao.y, ao.z, ao.w};
+                float Be[3][4], Bo[3][4];
 #pragma unroll
                 for (int nt = 0; nt < 3; nt++) {
                     int n = 16 * nt + r16;
                     n = n < 36 ? n : 35;
-                    const float4 *src = (const float4 *)&sBuf[n * SROW + 8 * q];
-                    const float4 b0 = src[0], b1 = src[1];
-                    Bf[nt][0] = b0.x; Bf[nt][1] = b0.y; Bf[nt][2] = b0.z; Bf[nt][3] = b0.w;
-                    Bf[nt][4] = b1.x; Bf[nt][5] = b1.y; Bf[nt][6] = b1.z; Bf[nt][7] = b1.w;
+                    const float4 a4 = *(const float4 *)&sBuf[n * SROW + 4 * q];
+                    const float4 b4 = *(const float4 *)&sBuf[n * SROW + 28 - 4 * q]; /* S[31-i] = b4[3-ks] */
+                    const float av[4] = {a4.x, a4.y, a4.z, a4.w}, bv[4] = {b4.w, b4.z, b4.y, b4.x};
+#pragma unroll
+                    for (int ks = 0; ks < 4; ks++) {
+                        Be[nt][ks] = av[ks] + bv[ks];
+                        Bo[nt][ks] = av[ks] - bv[ks];
+                    }
                 }
-                f32x4 acc[3][2];
+                f32x4 ce[3], co[3];
 #pragma unroll
-                for (int nt = 0; nt < 3; nt++)
+                for (int nt = 0; nt < 3; nt++) ce[nt] = co[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                    for (int mt = 0; mt < 2; mt++) acc[nt][mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                for (int ks = 0; ks < 4; ks++)
 #pragma unroll
-                for (int ks = 0; ks < 8; ks++)
-#pragma unroll
-                    for (int nt = 0; nt < 3; nt++)
-#pragma unroll
-                        for (int mt = 0; mt < 2; mt++)
-                            acc[nt][mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[mt][ks], Bf[nt][ks], acc[nt][mt], 0, 0, 0);
+                    for (int nt = 0; nt < 3; nt++) {
+#ifdef SYN_SKIP_MFMA
+                        ce[nt][0] += Be[nt][ks];
+                        co[nt][0] += Bo[nt][ks];
+#else
+                        ce[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ae[ks], Be[nt][ks], ce[nt], 0, 0, 0);
+                        co[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ao[ks], Bo[nt][ks], co[nt], 0, 0, 0);
+#endif
+                    }
                 wave_sync(); /* all S reads retired before X overwrites them */
-                /* D[row m = 16 mt + 4 q + r][col n] -> X[n][m] */
+                /* D[row m = 4 q + r][col n] -> X[n][2m] (even), X[n][2m+1] (odd) */
 #pragma unroll
                 for (int nt = 0; nt < 3; nt++) {
                     const int n = 16 * nt + r16;
-                    if (n < 36)
-#pragma unroll
-                        for (int mt = 0; mt < 2; mt++) *(f32x4 *)&sBuf[n * 32 + 16 * mt + 4 * q] = acc[nt][mt];
+                    if (n < 36) {
+                        *(f32x4 *)&sBuf[n * 32 + 8 * q] = (f32x4){ce[nt][0], co[nt][0], ce[nt][1], co[nt][1]};
+                        *(f32x4 *)&sBuf[n * 32 + 8 * q + 4] = (f32x4){ce[nt][2], co[nt][2], ce[nt][3], co[nt][3]};
+                    }
                 }
             }
             wave_sync();
@@ -1107,12 +1141,20 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                         const int sa = t - 2 * i, sbb = t - 2 * i - 1;
                         const float va = sa >= 0 ? xa[sa] : ha[sa + 14];
                         const float vb = sbb >= 0 ? xb[sbb] : hb[sbb + 15];
+#ifdef SYN_SKIP_W
+                        if (i == 0) o = va + vb + Dw[t & 15];
+#else
                         o = fmaf(Dw[2 * i], va, o);
                         o = fmaf(Dw[2 * i + 1], vb, o);
+#endif
                     }
                     float pv = rintf(o * 32768.f);
                     pv = fminf(fmaxf(pv, -32768.f), 32767.f);
+#ifdef SYN_SKIP_STORE
+                    if (active && pv == 0.123f) out[(gr * 576 + t * 32 + sb) * nch + ch] = (int16_t)pv;
+#else
                     if (active) out[(gr * 576 + t * 32 + sb) * nch + ch] = (int16_t)pv;
+#endif
                 }
 #pragma unroll
                 for (int k = 0; k < 14; k++) ha[k] = active ? xa[k + 4] : ha[k];
