@@ -143,17 +143,24 @@ static void build_tables(DevTables &t) {
         }
     }
     for (int sr = 0; sr < 3; sr++) {
+        int lb[576], sidx[576], sdst[576];
         int l = 0;
         for (int b = 0; b < 22; b++)
-            for (int n = 0; n < MP3D_SFB_LONG_WIDTH[sr][b]; n++) t.linfo[sr][l++] = (uint32_t)b;
+            for (int n = 0; n < MP3D_SFB_LONG_WIDTH[sr][b]; n++) lb[l++] = b;
         int p = 0;
         for (int b = 0; b < 13; b++) {
             int w = MP3D_SFB_SHORT_WIDTH[sr][b];
             for (int off = 0; off < 3 * w; off++) {
                 int win = off / w, f = off % w;
-                t.linfo[sr][p + off] |= ((uint32_t)b << 5) | ((uint32_t)win << 9) | ((uint32_t)(p + 3 * f + win) << 11);
+                sidx[p + off] = 22 + 3 * b + win;
+                sdst[p + off] = p + 3 * f + win;
             }
             p += 3 * w;
+        }
+        for (int i = 0; i < 576; i++) {
+            t.lvar[sr][0][i] = (uint16_t)(lb[i] | i << 6);
+            t.lvar[sr][1][i] = (uint16_t)(sidx[i] | sdst[i] << 6);
+            t.lvar[sr][2][i] = i < 36 ? t.lvar[sr][0][i] : t.lvar[sr][1][i];
         }
     }
     build_huffman_lut(t);

@@ -78,9 +78,10 @@ struct DevTables {
     float pow43[8208];         /* |is|^(4/3), |is| <= 8206               */
     float dct_c[32][32];       /* C[m][sb] = cos(m (2 sb + 1) pi / 64)  */
     float dwin[32][16];        /* per output j: signed window taps       */
-    /* per (sample-rate, bitstream line): bits 0..4 long band, 5..8 short
-     * band, 9..10 short window, 11..20 reordered (short) position      */
-    uint32_t linfo[3][576];
+    /* per (sample rate, block variant long / short / mixed, bitstream
+     * line): bits 0..5 scale index (long band b, or 22 + 3 b + w for short
+     * band b window w), bits 6..15 position after the short reorder      */
+    uint16_t lvar[3][3][576];
     uint8_t win_a[32];         /* V[j] = sgn * X[a[j]]                   */
     uint8_t win_b[32];         /* V[32 + j] = sgn * X[b[j]]              */
     uint16_t lut[MP3D_LUT_MAX];

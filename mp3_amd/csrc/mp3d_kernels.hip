@@ -746,10 +746,10 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
         const DevTables *__restrict__ tab, StreamState *__restrict__ st, int16_t *__restrict__ pcm, int F, int xr_nch,
         int xr_sr) {
     __shared__ __attribute__((aligned(16))) float sBuf[SYN_BUF];
-    __shared__ uint32_t sLinfo[576]; /* tab->linfo[sr] of the current sample rate   */
+    __shared__ uint32_t sLvar[3][288]; /* tab->lvar[sr] (u16 pairs): per block variant    */
     __shared__ float sScale[2][64];  /* 2^(q/4) per (ch, band idx): long b | 22 + 3 b + w */
     __shared__ uint8_t sIS[64];      /* intensity position per right-channel band idx, 0xFF none */
-    __shared__ float sP43[16];       /* |is|^(4/3) for |is| < 16                       */
+    __shared__ float sP43[256];      /* |is|^(4/3) for |is| < 256                      */
     __shared__ float sW[4][36];      /* long-block windows                             */
     __shared__ float sISR[7][2];     /* MPEG-1 intensity ratios                        */
     __shared__ UnitMeta sM[2];
@@ -759,7 +759,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
     const int sb = lane & 31; /* phase I: subband; phase W: output j */
     constexpr int MW = (int)(sizeof(UnitMeta) / 4); /* 14 words per unit */
 
-    if (lane < 16) sP43[lane] = tab->pow43[lane];
+    for (int i = lane; i < 256; i += 64) sP43[i] = tab->pow43[i];
     if (lane < 14) (&sISR[0][0])[lane] = (&c_is_ratio[0][0])[lane];
     for (int i = lane; i < 4 * 36; i += 64) (&sW[0][0])[i] = (&c_win36[0][0])[i];
 
@@ -809,7 +809,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
         }
         if (sr != cur_sr) { /* line tables of this sample rate into LDS */
             wave_sync();
-            for (int i = lane; i < 576; i += 64) sLinfo[i] = tab->linfo[sr][i];
+            for (int i = lane; i < 3 * 288; i += 64) (&sLvar[0][0])[i] = ((const uint32_t *)tab->lvar[sr])[i];
             cur_sr = sr;
             wave_sync();
         }
@@ -831,16 +831,13 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                     bt1 = xr_bt[ux + 1];
                     mx1 = bt1 == 2 ? xr_mixed[ux + 1] : 0;
                 }
+                const uint16_t *lv0 = (const uint16_t *)sLvar[bt0 == 2 ? (mx0 ? 2 : 1) : 0];
+                const uint16_t *lv1 = (const uint16_t *)sLvar[bt1 == 2 ? (mx1 ? 2 : 1) : 0];
 #pragma unroll
                 for (int i = 0; i < 9; i++) {
                     const int l = lane + 64 * i;
-                    const int dst = (int)(sLinfo[l] >> 11);
-                    const float x0 = xr_in[ux * 576 + l];
-                    sBuf[(bt0 == 2 && !(mx0 && l < 36)) ? dst : l] = x0;
-                    if (nch == 2) {
-                        const float x1 = xr_in[(ux + 1) * 576 + l];
-                        sBuf[576 + ((bt1 == 2 && !(mx1 && l < 36)) ? dst : l)] = x1;
-                    }
+                    sBuf[lv0[l] >> 6] = xr_in[ux * 576 + l];
+                    if (nch == 2) sBuf[576 + (lv1[l] >> 6)] = xr_in[(ux + 1) * 576 + l];
                 }
             } else {
                 const size_t up = fr * 2 + gr;
@@ -861,115 +858,126 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                     bt1 = sM[1].block_type;
                     mx1 = sM[1].mixed;
                 }
-                /* per-band scale, lane = band idx */
+                const int var[2] = {bt0 == 2 ? (mx0 ? 2 : 1) : 0, bt1 == 2 ? (mx1 ? 2 : 1) : 0};
+                const bool is_on = mode == 1 && nch == 2 && (mext & 1);
+                const bool ms_fold = mode == 1 && nch == 2 && mext == 2; /* M/S only: 1/sqrt2 in the scale */
+                const float isq = 0.70710678118654752f;
+                /* per-band scale 2^(q/4), lane = band idx (long b | 22 + 3 b + w) */
                 for (int c = 0; c < nch; c++) {
                     const UnitMeta &M = sM[c];
                     const int gain = (int)M.global_gain - 210, shift = M.scalefac_scale + 1;
                     int q;
                     if (lane < 22) {
-                        q = gain - ((M.sf[lane] + (M.preflag ? MP3D_PRETAB[lane] : 0)) << shift);
+                        q = gain - ((M.sf[lane] + (M.preflag ? (int)MP3D_PRETAB[lane] : 0)) << shift);
                     } else {
                         const int b = (lane - 22) / 3, w = lane - 22 - 3 * b;
                         int k = M.mixed ? 8 + 3 * (b - 3) + w : 3 * b + w;
                         k = k < 0 ? 0 : (k > 39 ? 39 : k);
                         q = gain - 8 * M.sbg[w < 3 ? w : 0] - (M.sf[k] << shift);
                     }
-                    sScale[c][lane] = pow2_quarter(q);
+                    sScale[c][lane] = ms_fold ? pow2_quarter(q) * isq : pow2_quarter(q);
                 }
                 wave_sync();
                 /* lane owns lines 2 lane + 128 i + e (e = 0, 1), i < 4, or i = 4
-                 * for lanes < 32; xv[c][2 i + e] */
-                float xv[2][10];
-                uint64_t nzR = 0;
+                 * for lanes < 32; xv[c][2 i + e].  Per line: one u16 table entry
+                 * (scale idx | reordered position), |is|^(4/3) from LDS. */
                 const int nz[2] = {sM[0].nz_end, nch == 2 ? sM[1].nz_end : 0};
+                float xv[2][10];
 #pragma unroll
                 for (int i = 0; i < 5; i++) {
                     const int l0 = 2 * lane + 128 * i;
                     const bool ok = i < 4 || lane < 32;
-                    const uint2 inf2 = ok ? *(const uint2 *)&sLinfo[l0] : make_uint2(0u, 0u);
 #pragma unroll
-                    for (int e = 0; e < 2; e++) {
-                        const int l = l0 + e;
-                        const uint32_t inf = e ? inf2.y : inf2.x;
-                        const int lb = inf & 31, sbd = (inf >> 5) & 15, w = (inf >> 9) & 3;
+                    for (int c = 0; c < 2; c++) {
+                        const uint32_t tv2 = ok ? sLvar[var[c]][l0 >> 1] : 0u;
 #pragma unroll
-                        for (int c = 0; c < 2; c++) {
-                            const int bt = c ? bt1 : bt0, mx = c ? mx1 : mx0;
-                            const bool sh = bt == 2 && !(mx && l < 36);
+                        for (int e = 0; e < 2; e++) {
+                            const int l = l0 + e;
                             int v = (int)(int16_t)(e ? (cis[c][i] >> 16) : (cis[c][i] & 0xFFFFu));
                             v = l < nz[c] ? v : 0; /* rzero lines are not stored by k_huffman */
                             const int a = v < 0 ? -v : v;
-                            float p = sP43[a < 16 ? a : 0];
-                            if (a >= 16) p = tab->pow43[a];
-                            const float mag = p * sScale[c][sh ? 22 + 3 * sbd + w : lb];
-                            xv[c][2 * i + e] = v < 0 ? -mag : (v ? mag : 0.f);
-                            if (c == 1 && v) nzR |= sh ? (1ull << (22 + 13 * w + sbd)) : (1ull << lb);
+                            float p = sP43[a < 256 ? a : 0];
+                            if (a >= 256) p = tab->pow43[a];
+                            const float mag = p * sScale[c][(e ? tv2 >> 16 : tv2) & 63u];
+                            xv[c][2 * i + e] = v < 0 ? -mag : mag;
                         }
                     }
                 }
-                /* joint stereo (ISO 2.4.3.4): MPEG-1 intensity + M/S, paired by
-                 * bitstream line; the right channel's block structure and its
-                 * highest nonzero band (per window) decide the IS bands
-                 * (FFmpeg compute_stereo; oracle/mp3_oracle.c orc_stereo) */
-                if (mode == 1 && nch == 2 && mext) {
-                    if (mext & 1) {
-#pragma unroll
-                        for (int o = 1; o < 64; o <<= 1) nzR |= __shfl_xor(nzR, o);
-                        const UnitMeta &R = sM[1];
-                        int ip = 0xFF;
-                        if (lane < 22) {
-                            if (bt1 != 2 || (mx1 && lane < 8)) {
-                                const int p = R.sf[lane == 21 ? 20 : lane];
-                                const bool short_nz = (nzR >> 22) != 0ull;
-                                if (!short_nz && ((uint32_t)(nzR & 0x3FFFFFull) >> lane) == 0u && p < 7) ip = p;
-                            }
-                        } else if (lane < 61 && bt1 == 2) {
-                            const int b = (lane - 22) / 3, w = lane - 22 - 3 * b;
-                            if (!mx1 || b >= 3) {
-                                const int kb = b == 12 ? 11 : b;
-                                const int p = R.sf[mx1 ? 8 + 3 * (kb - 3) + w : 3 * kb + w];
-                                const uint32_t wm = (uint32_t)(nzR >> (22 + 13 * w)) & 0x1FFFu;
-                                if ((wm >> b) == 0u && p < 7) ip = p;
-                            }
-                        }
-                        sIS[lane] = (uint8_t)ip;
-                        wave_sync();
-                    }
-                    const float isq = 0.70710678118654752f;
+                if (is_on) {
+                    /* joint stereo with MPEG-1 intensity (ISO 2.4.3.4), paired by
+                     * bitstream line; the right channel's block structure and
+                     * its highest nonzero band (per window) decide the IS bands
+                     * (FFmpeg compute_stereo; oracle/mp3_oracle.c orc_stereo).
+                     * nzR bit = right-channel band idx holding a nonzero line. */
+                    uint64_t nzR = 0;
 #pragma unroll
                     for (int i = 0; i < 5; i++) {
                         const int l0 = 2 * lane + 128 * i;
+                        const uint32_t tv2 = (i < 4 || lane < 32) ? sLvar[var[1]][l0 >> 1] : 0u;
+                        if (xv[1][2 * i] != 0.f) nzR |= 1ull << (tv2 & 63u);
+                        if (xv[1][2 * i + 1] != 0.f) nzR |= 1ull << ((tv2 >> 16) & 63u);
+                    }
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) nzR |= __shfl_xor(nzR, o);
+                    const UnitMeta &R = sM[1];
+                    int ip = 0xFF;
+                    if (lane < 22) {
+                        if (bt1 != 2 || (mx1 && lane < 8)) {
+                            const int p = R.sf[lane == 21 ? 20 : lane];
+                            const bool short_nz = (nzR >> 22) != 0ull;
+                            if (!short_nz && ((uint32_t)(nzR & 0x3FFFFFull) >> lane) == 0u && p < 7) ip = p;
+                        }
+                    } else if (lane < 61 && bt1 == 2) {
+                        const int b = (lane - 22) / 3, w = lane - 22 - 3 * b;
+                        if (!mx1 || b >= 3) {
+                            const int kb = b == 12 ? 11 : b;
+                            const int p = R.sf[mx1 ? 8 + 3 * (kb - 3) + w : 3 * kb + w];
+                            /* no nonzero line in window w at bands >= b */
+                            uint64_t above = 0;
+                            for (int bb = b; bb < 13; bb++) above |= 1ull << (22 + 3 * bb + w);
+                            if ((nzR & above) == 0ull && p < 7) ip = p;
+                        }
+                    }
+                    sIS[lane] = (uint8_t)ip;
+                    wave_sync();
+#pragma unroll
+                    for (int i = 0; i < 5; i++) {
+                        const int l0 = 2 * lane + 128 * i;
+                        const uint32_t tv2 = (i < 4 || lane < 32) ? sLvar[var[1]][l0 >> 1] : 0u;
 #pragma unroll
                         for (int e = 0; e < 2; e++) {
-                            const int l = l0 + e, k = 2 * i + e;
+                            const int k = 2 * i + e;
                             const float lv = xv[0][k], rv = xv[1][k];
-                            int ip = 0xFF;
-                            if ((mext & 1) && (i < 4 || lane < 32)) {
-                                const uint32_t inf = sLinfo[l];
-                                const bool shR = bt1 == 2 && !(mx1 && l < 36);
-                                ip = sIS[shR ? 22 + 3 * ((inf >> 5) & 15) + ((inf >> 9) & 3) : (inf & 31)];
-                            }
-                            if (ip != 0xFF) {
-                                xv[0][k] = lv * sISR[ip][0];
-                                xv[1][k] = lv * sISR[ip][1];
+                            const int ipl = sIS[(e ? tv2 >> 16 : tv2) & 63u];
+                            if (ipl != 0xFF) {
+                                xv[0][k] = lv * sISR[ipl][0];
+                                xv[1][k] = lv * sISR[ipl][1];
                             } else if (mext & 2) {
                                 xv[0][k] = (lv + rv) * isq;
                                 xv[1][k] = (lv - rv) * isq;
                             }
                         }
                     }
+                } else if (ms_fold) {
+#pragma unroll
+                    for (int k = 0; k < 10; k++) {
+                        const float lv = xv[0][k], rv = xv[1][k];
+                        xv[0][k] = lv + rv;
+                        xv[1][k] = lv - rv;
+                    }
                 }
+                /* scatter in (short-block reordered) position */
 #pragma unroll
                 for (int i = 0; i < 5; i++) {
                     if (i < 4 || lane < 32) {
                         const int l0 = 2 * lane + 128 * i;
-                        const uint2 inf2 = *(const uint2 *)&sLinfo[l0];
 #pragma unroll
-                        for (int e = 0; e < 2; e++) {
-                            const int l = l0 + e;
-                            const int dst = (int)((e ? inf2.y : inf2.x) >> 11);
-                            sBuf[(bt0 == 2 && !(mx0 && l < 36)) ? dst : l] = xv[0][2 * i + e];
-                            if (nch == 2) sBuf[576 + ((bt1 == 2 && !(mx1 && l < 36)) ? dst : l)] = xv[1][2 * i + e];
+                        for (int c = 0; c < 2; c++) {
+                            if (c < nch) {
+                                const uint32_t tv2 = sLvar[var[c]][l0 >> 1];
+                                sBuf[576 * c + (tv2 >> 6 & 1023u)] = xv[c][2 * i];
+                                sBuf[576 * c + (tv2 >> 22)] = xv[c][2 * i + 1];
+                            }
                         }
                     }
                 }
