@@ -391,7 +391,9 @@ static int prepare_geometry(mp3d_batch *b, const uint64_t *offsets, const uint32
     size_t o = 0;
     for (int i = 0; i < n; i++) {
         b->md_off_host[i] = o;
-        o += ((size_t)sizes[i] + MP3D_RES_BYTES + 16 + 15) & ~(size_t)15;
+        /* carry-in + payloads; a cut-short final frame is completed with
+         * zeros, so allow one maximal frame beyond the stream's bytes */
+        o += ((size_t)sizes[i] + MP3D_RES_BYTES + MP3D_MAX_FRAME_BYTES + 16 + 15) & ~(size_t)15;
     }
     int r = grow((void **)&b->md, &b->md_cap, o + 8192);
     if (r) return r;

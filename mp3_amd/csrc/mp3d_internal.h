@@ -35,6 +35,8 @@ struct FrameRec {
     uint8_t first_gr;    /* first decoded granule (reservoir underflow)      */
     uint8_t sr_idx;
     uint8_t pad_;
+    uint16_t payload_avail; /* payload bytes present (< payload_len: the final
+                             * frame was cut short; the rest reads as zeros) */
 };
 
 /* Per-unit side information + scalefactors, written by k_huffman. */

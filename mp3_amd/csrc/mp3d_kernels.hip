@@ -94,6 +94,7 @@ __global__ void __launch_bounds__(256) k_scan(const uint8_t *__restrict__ in, co
         FrameRec r;
         r.frame_off = 0; r.md_bit = 0; r.payload_md = P; r.frame_bytes = 0; r.payload_len = 0;
         r.hdr1 = r.hdr2 = r.hdr3 = 0; r.nch = 0; r.side_off = 4; r.first_gr = 0; r.sr_idx = 0; r.pad_ = 0;
+        r.payload_avail = 0;
         DevInfo inf = {0, 0, 0, 0, 0, 0};
         int fb = -1;
         while (cur + 4 <= len) {
@@ -103,11 +104,15 @@ __global__ void __launch_bounds__(256) k_scan(const uint8_t *__restrict__ in, co
             }
             cur++;
         }
-        if (fb > 0 && cur + (uint32_t)fb <= len) {
+        /* a final frame cut short still decodes (FFmpeg: the missing bytes
+         * read as zeros) once its header and side info are present */
+        const uint32_t need = fb > 0 ? 4u + ((p0[cur + 1] & 1) ? 0u : 2u) + ((p0[cur + 3] >> 6) == 3 ? 17u : 32u) : 0u;
+        if (fb > 0 && (cur + (uint32_t)fb <= len || cur + need <= len)) {
             const uint8_t *fp = p0 + cur;
             int nch = (fp[3] >> 6) == 3 ? 1 : 2;
             int crc = (fp[1] & 1) ? 0 : 2;
             int side_bytes = nch == 1 ? 17 : 32;
+            const uint32_t have = min(len - cur, (uint32_t)fb); /* bytes of this frame present */
             int plen = fb - 4 - crc - side_bytes;
             const uint8_t *side = fp + 4 + crc;
             r.frame_off = in_off[s] + cur;
@@ -120,7 +125,7 @@ __global__ void __launch_bounds__(256) k_scan(const uint8_t *__restrict__ in, co
             inf.frame_bytes = fb; inf.channels = nch; inf.hz = (int)MP3D_SAMPLE_RATE[r.sr_idx];
             inf.layer = 3; inf.bitrate_kbps = MP3D_BITRATE_L3[fp[2] >> 4];
             const uint8_t *tg = side + side_bytes;
-            bool tag = stream_start && f == 0 && plen >= 4 &&
+            bool tag = stream_start && f == 0 && plen >= 4 && have == (uint32_t)fb &&
                        ((tg[0] == 'X' && tg[1] == 'i' && tg[2] == 'n' && tg[3] == 'g') ||
                         (tg[0] == 'I' && tg[1] == 'n' && tg[2] == 'f' && tg[3] == 'o'));
             int mdb = (int)bits_at(side, 0, 9);
@@ -145,9 +150,11 @@ __global__ void __launch_bounds__(256) k_scan(const uint8_t *__restrict__ in, co
             if (tag) {
                 r.first_gr = REC_TAG;
             } else if (bad) {
-                /* FFmpeg drops the frame; its reservoir restarts from the frame tail */
+                /* FFmpeg drops the frame; its reservoir restarts as the frame's
+                 * last min(512, bytes - 4) post-header bytes (mp_decode_frame) */
                 r.first_gr = REC_DROP;
-                avail = plen > 0 ? (plen < MP3D_RES_BYTES ? plen : MP3D_RES_BYTES) : 0;
+                r.payload_len = (uint16_t)(fb - 4);
+                avail = fb - 4 < MP3D_RES_BYTES ? fb - 4 : MP3D_RES_BYTES;
                 P += (uint32_t)r.payload_len;
             } else {
                 int gr0 = 0;
@@ -173,7 +180,12 @@ __global__ void __launch_bounds__(256) k_scan(const uint8_t *__restrict__ in, co
                 inf.samples = 1152;
                 decoded++;
             }
-            cur += (uint32_t)fb;
+            {
+                const uint32_t body = (r.first_gr & REC_DROP) ? 4u : 4u + (uint32_t)crc + (uint32_t)side_bytes;
+                const uint32_t av = have > body ? have - body : 0u;
+                r.payload_avail = (uint16_t)(av < r.payload_len ? av : r.payload_len);
+            }
+            cur = have == (uint32_t)fb ? cur + (uint32_t)fb : len;
         } else {
             cur = len;
         }
@@ -210,8 +222,11 @@ __global__ void __launch_bounds__(256) k_gather(const uint8_t *__restrict__ in, 
     for (int f = wv; f < F; f += 4) {
         const FrameRec r = rec[(size_t)s * F + f];
         if (!r.frame_bytes || (r.first_gr & REC_TAG)) continue;
-        const uint8_t *src = in + r.frame_off + r.side_off + (r.nch == 1 ? 17 : 32);
-        const uint32_t P = r.payload_md, L = r.payload_len;
+        /* a dropped frame's post-header bytes (CRC, side info, payload) all
+         * enter the reservoir (FFmpeg); otherwise just the payload */
+        const uint8_t *src = in + r.frame_off + ((r.first_gr & REC_DROP) ? 4 : r.side_off + (r.nch == 1 ? 17 : 32));
+        const uint32_t P = r.payload_md, L = r.payload_avail;
+        for (uint32_t i = L + lane; i < r.payload_len; i += 64) dst[P + i] = 0; /* cut-short final frame */
         const uint32_t h = min((4u - (P & 3u)) & 3u, L); /* head bytes up to an aligned word */
         const uint32_t wb = (P + h) >> 2, we = (P + L) >> 2; /* whole words [wb, we) */
         if ((uint32_t)lane < h) dst[P + lane] = src[lane];
@@ -895,11 +910,15 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                             const int l = l0 + e;
                             int v = (int)(int16_t)(e ? (cis[c][i] >> 16) : (cis[c][i] & 0xFFFFu));
                             v = l < nz[c] ? v : 0; /* rzero lines are not stored by k_huffman */
+#ifdef SYN_SKIP_Q
+                            xv[c][2 * i + e] = (float)v + (float)tv2;
+#else
                             const int a = v < 0 ? -v : v;
                             float p = sP43[a < 256 ? a : 0];
                             if (a >= 256) p = tab->pow43[a];
                             const float mag = p * sScale[c][(e ? tv2 >> 16 : tv2) & 63u];
                             xv[c][2 * i + e] = v < 0 ? -mag : mag;
+#endif
                         }
                     }
                 }

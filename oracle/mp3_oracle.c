@@ -552,7 +552,16 @@ ORC_API int orc_decode_frame_f64(orc_dec *d, const uint8_t *buf, int bytes, doub
     orc_parse_side(side, h.nch, s);
     for (int gr = 0; gr < 2; gr++)
         for (int ch = 0; ch < h.nch; ch++)
-            if (s->gr[gr][ch].big_values > 288) return -3; /* dropped, SURVEY A.9 (5) */
+            if (s->gr[gr][ch].big_values > 288) {
+                /* dropped; FFmpeg mp_decode_frame then keeps
+                 * the frame's last min(BACKSTEP_SIZE = 512, bytes - 4) post-
+                 * header bytes as the whole reservoir */
+                int keep = fb - 4 < 512 ? fb - 4 : 512;
+                memcpy(d->hist, buf + fb - keep, (size_t)keep);
+                d->hist_len = keep;
+                d->avail = keep;
+                return -3;
+            }
     const uint8_t *payload = side + h.side_bytes;
     int plen = fb - 4 - h.crc_bytes - h.side_bytes;
     if (plen < 0) return -4;
@@ -701,7 +710,24 @@ ORC_API long orc_decode_stream(const uint8_t *buf, long len, float *pcm, long ma
         orc_hdr h;
         int fb = orc_parse_header(buf + pos, &h);
         if (fb < 0) { pos++; continue; }
-        if (pos + fb > len) break;
+        if (pos + fb > len) {
+            /* a final frame cut short: FFmpeg still decodes it, the missing
+             * bytes reading as zeros */
+            if (len - pos < 4 + h.crc_bytes + h.side_bytes || nf >= max_frames) break;
+            uint8_t *pad = (uint8_t *)calloc((size_t)fb, 1);
+            memcpy(pad, buf + pos, (size_t)(len - pos));
+            orc_info info;
+            int r = orc_decode_frame(d, pad, fb, &tmp[0][0], &info);
+            free(pad);
+            if (r > 0) {
+                nch = info.channels;
+                hz = info.hz;
+                for (int ch = 0; ch < nch; ch++)
+                    memcpy(pcm + (size_t)ch * max_frames * 1152 + nf * 1152, tmp[ch], sizeof(float) * 1152);
+                nf++;
+            }
+            break;
+        }
         if (first && orc_is_info_frame(buf + pos, len - pos)) { pos += fb; first = 0; continue; }
         first = 0;
         orc_info info;

@@ -23,3 +23,15 @@ def names():
 
 def to_int16(x):
     return np.clip(np.rint(np.asarray(x, np.float64) * 32768.0), -32768, 32767).astype(np.int16)
+
+
+def compare(name, ours, ref):
+    """Max |ours - ref| in LSB over the frames both decoders emitted, after
+    checking our frame count (edge cases: tests/golden/manifest.json notes)."""
+    import numpy as np
+    meta = manifest()[name]
+    want = meta.get("our_frames") or ref.shape[1] // 1152
+    assert ours.shape[1] == want * 1152, (name, ours.shape, want)
+    k = min(ours.shape[1], ref.shape[1])
+    d = np.abs(ours[:, :k].astype(np.int32) - ref[:, :k].astype(np.int32))
+    return int(d.max()), float((d == 0).mean())

@@ -14,10 +14,9 @@ def test_oracle_matches_ffmpeg_golden(name):
     data, ref = _golden.case(name)
     pcm, hz = _oracle.decode_stream(data)
     ours = _golden.to_int16(pcm)
-    assert ours.shape == ref.shape
-    d = np.abs(ours.astype(np.int32) - ref.astype(np.int32))
-    assert d.max() <= 1, (name, int(d.max()))  # ±1 LSB (north_star tolerance)
-    assert (d == 0).mean() > 0.6  # FFmpeg is fixed-point: ~75% exact
+    worst, exact = _golden.compare(name, ours, ref)
+    assert worst <= 1, (name, worst)  # ±1 LSB (north_star tolerance)
+    assert exact > 0.6  # FFmpeg is fixed-point: ~75% exact
 
 
 def test_keypress_bitstream_facts():
