@@ -734,7 +734,8 @@ __device__ __forceinline__ void imdct36_w(const float *X, float *w) {
 /* Template SRC_XR: config-2 entry (spectra given as f32 xr, after stereo). */
 /* ------------------------------------------------------------------------ */
 #define SROW 36      /* LDS row stride of S (floats): 16-B rows, few conflicts */
-#define SYN_BUF 1296 /* floats: max(xr 2x576, S 36x36, X 36x32)              */
+#define SYN_BUF 1296 /* floats: max(xr 2x576, S 36x36, X 36x36)              */
+#define XROW 36      /* LDS row stride of X: 16-B rows, conflict-free b128 writes */
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -993,9 +994,13 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
 #pragma unroll
                         for (int c = 0; c < 2; c++) {
                             if (c < nch) {
-                                const uint32_t tv2 = sLvar[var[c]][l0 >> 1];
-                                sBuf[576 * c + (tv2 >> 6 & 1023u)] = xv[c][2 * i];
-                                sBuf[576 * c + (tv2 >> 22)] = xv[c][2 * i + 1];
+                                if (var[c] == 0) { /* long block: in place, one 8-B store */
+                                    *(float2 *)&sBuf[576 * c + l0] = make_float2(xv[c][2 * i], xv[c][2 * i + 1]);
+                                } else {
+                                    const uint32_t tv2 = sLvar[var[c]][l0 >> 1];
+                                    sBuf[576 * c + (tv2 >> 6 & 1023u)] = xv[c][2 * i];
+                                    sBuf[576 * c + (tv2 >> 22)] = xv[c][2 * i + 1];
+                                }
                             }
                         }
                     }
@@ -1139,8 +1144,8 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                 for (int nt = 0; nt < 3; nt++) {
                     const int n = 16 * nt + r16;
                     if (n < 36) {
-                        *(f32x4 *)&sBuf[n * 32 + 8 * q] = (f32x4){ce[nt][0], co[nt][0], ce[nt][1], co[nt][1]};
-                        *(f32x4 *)&sBuf[n * 32 + 8 * q + 4] = (f32x4){ce[nt][2], co[nt][2], ce[nt][3], co[nt][3]};
+                        *(f32x4 *)&sBuf[n * XROW + 8 * q] = (f32x4){ce[nt][0], co[nt][0], ce[nt][1], co[nt][1]};
+                        *(f32x4 *)&sBuf[n * XROW + 8 * q + 4] = (f32x4){ce[nt][2], co[nt][2], ce[nt][3], co[nt][3]};
                     }
                 }
             }
@@ -1154,11 +1159,11 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                     Dw[4 * i] = d.x; Dw[4 * i + 1] = d.y; Dw[4 * i + 2] = d.z; Dw[4 * i + 3] = d.w;
                 }
                 float xa[18], xb[18];
-                const int pa = opaque(18 * ch * 32 + wa), pb = opaque(18 * ch * 32 + wb);
+                const int pa = opaque(18 * ch * XROW + wa), pb = opaque(18 * ch * XROW + wb);
 #pragma unroll
                 for (int t = 0; t < 18; t++) {
-                    xa[t] = sBuf[pa + t * 32];
-                    xb[t] = sBuf[pb + t * 32];
+                    xa[t] = sBuf[pa + t * XROW];
+                    xb[t] = sBuf[pb + t * XROW];
                 }
 #pragma unroll
                 for (int t = 0; t < 18; t++) {

@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Condense a tools/profile.sh run (gpurun_out/prof_TAG/) into committed
+summaries under profiles/:
+
+  profiles/TAG_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary
+  profiles/TAG_pmc.json           per-kernel PMC counters (mean per dispatch)
+  profiles/pmc_traffic.json       HBM bytes per k_synth launch for bench.py
+
+HBM traffic per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes): on
+gfx950 FETCH_SIZE reports half the bytes of wide coalesced reads
+(MI355X_MICROARCH.md, HBM section); WRITE_SIZE is exact for 16-B stores.
+Usage: python tools/summarize_profile.py TAG [--streams N --frames F]
+"""
+import argparse
+import collections
+import csv
+import json
+import pathlib
+import shutil
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+
+
+def counters(d):
+    rows = list(csv.DictReader(open(d / "run_counter_collection.csv")))
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in rows:
+        name = r["Kernel_Name"]
+        if "mp3d::" not in name:
+            continue
+        k = name.split("(")[0].replace("void ", "").replace("mp3d::", "")
+        agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in agg.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("--streams", type=int, default=65536)
+    ap.add_argument("--frames", type=int, default=32)
+    a = ap.parse_args()
+    src = ROOT / "gpurun_out" / ("prof_" + a.tag)
+    dst = ROOT / "profiles"
+    dst.mkdir(exist_ok=True)
+    shutil.copy(src / "stats" / "run_kernel_stats.csv", dst / (a.tag + "_kernel_stats.csv"))
+    out = {}
+    for p in ("pmc_sq1", "pmc_sq2", "pmc_fetch", "pmc_write"):
+        for k, cs in counters(src / p).items():
+            out.setdefault(k, {}).update(cs)
+    for k, cs in out.items():
+        if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
+            cs["hbm_bytes_per_launch"] = (2 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024.0
+    (dst / (a.tag + "_pmc.json")).write_text(json.dumps(out, indent=1, sort_keys=True))
+    synth = out.get("k_synth<false>", {})
+    if "hbm_bytes_per_launch" in synth:
+        (dst / "pmc_traffic.json").write_text(json.dumps({
+            "tag": a.tag, "streams": a.streams, "frames": a.frames,
+            "k_synth_hbm_bytes_per_launch": synth["hbm_bytes_per_launch"],
+            "k_synth_fetch_kib": synth["FETCH_SIZE"], "k_synth_write_kib": synth["WRITE_SIZE"],
+            "method": "2 x FETCH_SIZE + WRITE_SIZE, separate rocprofv3 --pmc passes (tools/profile.sh)"}, indent=1))
+    for k, cs in sorted(out.items()):
+        print(k, {c: "%.4g" % v for c, v in cs.items()})
+
+
+if __name__ == "__main__":
+    main()
