@@ -295,43 +295,60 @@ __device__ __forceinline__ uint32_t shl64hi(uint32_t hi, uint32_t lo, uint32_t n
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> (32u - n));
 }
 
-/* cnt (<= 8) scalefactors of sl (<= 4) bits at pos -> sf[j..j+cnt) */
-__device__ __forceinline__ uint32_t sf_group(const uint32_t *bits, uint32_t pos, int cnt, int sl, uint8_t *sf, int j) {
-    uint32_t w = sl ? win32(bits, pos) : 0u;
-    for (int i = 0; i < cnt; i++) {
-        sf[j + i] = sl ? (uint8_t)(w >> (32 - sl)) : (uint8_t)0;
-        w <<= sl;
+/* Scalefactors are built in 10 packed registers (byte j of UnitMeta.sf in
+ * byte j & 3 of w[j >> 2]) with compile-time positions and stored with
+ * three wide stores: per-byte global stores from 64 lanes to 64 different
+ * records are the slow, uncoalesced store pattern of this kernel.       */
+template <int BASE, int CNT>
+__device__ __forceinline__ uint32_t sf_group(const uint32_t *bits, uint32_t pos, int sl, uint32_t *w) {
+    uint32_t v = win32(bits, pos);
+#pragma unroll
+    for (int i = 0; i < CNT; i++) {
+        const uint32_t x = sl ? v >> (32 - sl) : 0u;
+        v = sl ? v << sl : 0u;
+        const int j = BASE + i;
+        w[j >> 2] = (w[j >> 2] & ~(0xFFu << (8 * (j & 3)))) | (x << (8 * (j & 3)));
     }
-    return pos + (uint32_t)(cnt * sl);
+    return pos + (uint32_t)(CNT * sl);
 }
 
 /* Scalefactors (part 2), ISO 2.4.2.7, read in place: groups whose scfsi bit
- * is set keep the granule-0 values already in sf (layout as UnitMeta.sf). */
-__device__ __forceinline__ uint32_t read_sf(const uint32_t *bits, uint32_t pos, uint64_t side, int scfsi, uint8_t *sf,
+ * is set keep the granule-0 values already in w (layout as UnitMeta.sf). */
+__device__ __forceinline__ uint32_t read_sf(const uint32_t *bits, uint32_t pos, uint64_t side, int scfsi, uint32_t *w,
                                             const uint8_t *slen) {
     const int sfc = (int)(side >> 31) & 15, ws = (int)(side >> 30) & 1;
     const int bt = ws ? (int)(side >> 28) & 3 : 0, mixed = ws ? (int)(side >> 27) & 1 : 0;
     const int slen1 = slen[sfc], slen2 = slen[16 + sfc];
-    int j;
     if (bt == 2) {
-        /* (mixed) 17 / 18 values of slen1 then 18 of slen2, in groups of 6 */
-        const int n1 = mixed ? 17 : 18;
-        pos = sf_group(bits, pos, 6, slen1, sf, 0);
-        pos = sf_group(bits, pos, 6, slen1, sf, 6);
-        pos = sf_group(bits, pos, n1 - 12, slen1, sf, 12);
-        j = n1;
-        pos = sf_group(bits, pos, 6, slen2, sf, j);
-        pos = sf_group(bits, pos, 6, slen2, sf, j + 6);
-        pos = sf_group(bits, pos, 6, slen2, sf, j + 12);
-        j += 18;
+        /* (mixed) 17 / 18 values of slen1 then 18 of slen2: written as the
+         * 18 + 18 layout, then shifted down one byte from 17 when mixed */
+#pragma unroll
+        for (int i = 0; i < 10; i++) w[i] = 0u;
+        pos = sf_group<0, 6>(bits, pos, slen1, w);
+        pos = sf_group<6, 6>(bits, pos, slen1, w);
+        if (mixed) pos = sf_group<12, 5>(bits, pos, slen1, w);
+        else pos = sf_group<12, 6>(bits, pos, slen1, w);
+        pos = sf_group<18, 6>(bits, pos, slen2, w);
+        pos = sf_group<24, 6>(bits, pos, slen2, w);
+        pos = sf_group<30, 6>(bits, pos, slen2, w);
+        if (mixed) {
+            uint32_t sh[5];
+#pragma unroll
+            for (int k = 0; k < 5; k++) sh[k] = __builtin_amdgcn_alignbit(w[5 + k], w[4 + k], 8);
+            w[4] = (w[4] & 0xFFu) | (sh[0] & 0xFFFFFF00u);
+#pragma unroll
+            for (int k = 1; k < 5; k++) w[4 + k] = sh[k];
+            w[9] >>= 8;
+        }
     } else {
-        if (!(scfsi & 8)) pos = sf_group(bits, pos, 6, slen1, sf, 0);
-        if (!(scfsi & 4)) pos = sf_group(bits, pos, 5, slen1, sf, 6);
-        if (!(scfsi & 2)) pos = sf_group(bits, pos, 5, slen2, sf, 11);
-        if (!(scfsi & 1)) pos = sf_group(bits, pos, 5, slen2, sf, 16);
-        j = 21;
+        if (!(scfsi & 8)) pos = sf_group<0, 6>(bits, pos, slen1, w);
+        if (!(scfsi & 4)) pos = sf_group<6, 5>(bits, pos, slen1, w);
+        if (!(scfsi & 2)) pos = sf_group<11, 5>(bits, pos, slen2, w);
+        if (!(scfsi & 1)) pos = sf_group<16, 5>(bits, pos, slen2, w);
+        w[5] &= 0xFFu; /* bytes 21 .. 39 are zero */
+#pragma unroll
+        for (int i = 6; i < 10; i++) w[i] = 0u;
     }
-    for (; j < 40; j++) sf[j] = 0;
     return pos;
 }
 
@@ -510,18 +527,23 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                 }
                 wave_sync();
                 if (inb) {
-                    /* scalefactors go straight to the output record */
-                    uint8_t *sf = meta[u].sf;
+                    uint32_t sfw[10];
+#pragma unroll
+                    for (int i = 0; i < 10; i++) sfw[i] = 0u;
                     const uint32_t seg = 32u * (off - base) - 32u * w0; /* md bit -> staged bit */
                     uint32_t pos = start + seg;
                     if (need_g0) {
                         /* scfsi reuse: granule 0's scalefactors of this channel
                          * first, then granule 1's read over them in place */
-                        read_sf(bits, g0_start + seg, sq[ch], 0, sf, s_slen);
-                    } else if (scfsi) {
-                        for (int i = 0; i < 40; i++) sf[i] = 0;
+                        read_sf(bits, g0_start + seg, sq[ch], 0, sfw, s_slen);
                     }
-                    pos = read_sf(bits, pos, side, scfsi, sf, s_slen);
+                    pos = read_sf(bits, pos, side, scfsi, sfw, s_slen);
+                    {
+                        uint8_t *mrec = (uint8_t *)&meta[u];
+                        *(uint4 *)mrec = make_uint4(sfw[0], sfw[1], sfw[2], sfw[3]);
+                        *(uint4 *)(mrec + 16) = make_uint4(sfw[4], sfw[5], sfw[6], sfw[7]);
+                        *(uint2 *)(mrec + 32) = make_uint2(sfw[8], sfw[9]);
+                    }
                     /* big_values: region boundaries (ISO 2.4.2.7; FFmpeg clamp) */
                     const int ws = (int)(side >> 30) & 1;
                     const int bv2 = 2 * ((int)(side >> 43) & 0x1FF);
