@@ -434,10 +434,6 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
         uint32_t rank[HUFF_ROUNDS];
 #pragma unroll
         for (int j = 0; j < HUFF_ROUNDS; j++) rank[j] = 0;
-#ifdef HUFF_SKIP_SORT
-        for (int j = 0; j < HUFF_ROUNDS; j++) rank[j] = key[j] & 0x1FFu;
-        if (false)
-#endif
         for (int i = 0; i < HUFF_SUPER; i += 4) {
             const uint4 k4 = *(const uint4 *)&bits[i];
 #pragma unroll
@@ -507,11 +503,7 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                 const bool inb = pending && off + len - base <= HUFF_CAPW;
                 wave_sync();
                 /* stage: each lane copies its own segment, 4 x 16 B in flight */
-#ifdef HUFF_SKIP_STAGE
-                if (false) {
-#else
                 if (inb) {
-#endif
                     uint32_t *dst = bits + (off - base);
                     for (uint32_t i = 0; i < len; i += 16) {
                         uint4 v[4];
@@ -573,9 +565,6 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                     rw.nw = 0;
                     rw.w0 = rw.w1 = rw.w2 = rw.w3 = 0u;
                     int k = 0;
-#ifdef HUFF_SKIP_LOOPS
-                    k = 600;
-#endif
                     for (; k < bv2; k += 2) {
                         const uint32_t ts = k < r1 ? ts0 : (k < r2 ? ts1 : ts2);
                         const uint32_t tb = ts & 0xFFFFu, b1 = (ts >> 16) & 15u, lin = ts >> 24;
@@ -933,15 +922,11 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                             const int l = l0 + e;
                             int v = (int)(int16_t)(e ? (cis[c][i] >> 16) : (cis[c][i] & 0xFFFFu));
                             v = l < nz[c] ? v : 0; /* rzero lines are not stored by k_huffman */
-#ifdef SYN_SKIP_Q
-                            xv[c][2 * i + e] = (float)v + (float)tv2;
-#else
                             const int a = v < 0 ? -v : v;
                             float p = sP43[a < 256 ? a : 0];
                             if (a >= 256) p = tab->pow43[a];
                             const float mag = p * sScale[c][(e ? tv2 >> 16 : tv2) & 63u];
                             xv[c][2 * i + e] = v < 0 ? -mag : mag;
-#endif
                         }
                     }
                 }
@@ -1065,11 +1050,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                 if (long_imdct) {
                     const float *wv = sW[bt == 2 ? 0 : bt];
                     float w[18];
-#ifdef SYN_SKIP_I
-                    for (int i = 0; i < 18; i++) w[i] = x[i];
-#else
                     imdct36_w(x, w);
-#endif
 #pragma unroll
                     for (int i = 0; i < 9; i++) {
                         o18[i] = fmaf(w[9 + i], wv[i], ov[i]);
@@ -1152,13 +1133,8 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                 for (int ks = 0; ks < 4; ks++)
 #pragma unroll
                     for (int nt = 0; nt < 3; nt++) {
-#ifdef SYN_SKIP_MFMA
-                        ce[nt][0] += Be[nt][ks];
-                        co[nt][0] += Bo[nt][ks];
-#else
                         ce[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ae[ks], Be[nt][ks], ce[nt], 0, 0, 0);
                         co[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ao[ks], Bo[nt][ks], co[nt], 0, 0, 0);
-#endif
                     }
                 wave_sync(); /* all S reads retired before X overwrites them */
                 /* D[row m = 4 q + r][col n] -> X[n][2m] (even), X[n][2m+1] (odd) */
@@ -1195,20 +1171,12 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                         const int sa = t - 2 * i, sbb = t - 2 * i - 1;
                         const float va = sa >= 0 ? xa[sa] : ha[sa + 14];
                         const float vb = sbb >= 0 ? xb[sbb] : hb[sbb + 15];
-#ifdef SYN_SKIP_W
-                        if (i == 0) o = va + vb + Dw[t & 15];
-#else
                         o = fmaf(Dw[2 * i], va, o);
                         o = fmaf(Dw[2 * i + 1], vb, o);
-#endif
                     }
                     float pv = rintf(o * 32768.f);
                     pv = fminf(fmaxf(pv, -32768.f), 32767.f);
-#ifdef SYN_SKIP_STORE
-                    if (active && pv == 0.123f) out[(gr * 576 + t * 32 + sb) * nch + ch] = (int16_t)pv;
-#else
                     if (active) out[(gr * 576 + t * 32 + sb) * nch + ch] = (int16_t)pv;
-#endif
                 }
 #pragma unroll
                 for (int k = 0; k < 14; k++) ha[k] = active ? xa[k + 4] : ha[k];
