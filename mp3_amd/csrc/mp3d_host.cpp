@@ -88,15 +88,15 @@ static void build_huffman_lut(DevTables &t) {
         std::vector<size_t> subbase(1u << b1, 0);
         for (uint32_t p = 0; p < (1u << b1); p++)
             if (subbits[p]) {
-                if (lut.size() & 1) lut.push_back(UNUSED);
-                size_t rel = lut.size() - base;
-                if (rel / 2 > 0x7FF || subbits[p] > 15) {
+                while (lut.size() & 3) lut.push_back(UNUSED); /* sub-tables 4-entry aligned */
+                const size_t abs4 = lut.size() / 4;
+                if (abs4 > 0x7FF || subbits[p] > 15) {
                     fprintf(stderr, "mp3d: LUT pointer overflow\n");
                     abort();
                 }
                 subbase[p] = lut.size();
                 lut.resize(lut.size() + (1u << subbits[p]), UNUSED);
-                lut[base + p] = (uint16_t)(0x8000u | ((uint32_t)subbits[p] << 11) | (uint32_t)(rel / 2));
+                lut[base + p] = (uint16_t)(0x8000u | ((uint32_t)subbits[p] << 11) | (uint32_t)abs4);
             }
         for (size_t i = 0; i < code.size(); i++) {
             uint16_t leaf = (uint16_t)((len[i] << 8) | val[i]);

@@ -66,8 +66,8 @@ struct StreamState {
 
 /* Huffman LUT layout (u16 entries, two levels, first level <= 8 bits):
  * leaf:    bit15 = 0, bits 8..12 code length, bits 4..7 x, bits 0..3 y
- * pointer: bit15 = 1, bits 11..14 sub-index bits, bits 0..10 sub-table
- *          offset / 2 relative to the table's first-level base          */
+ * pointer: bit15 = 1, bits 11..14 sub-index bits, bits 0..10 absolute
+ *          sub-table index / 4 (sub-tables are 4-entry aligned)          */
 #define MP3D_LUT_TABLES 16 /* 15 big_values code tables + count1 table A   */
 #define MP3D_LUT_MAX 7168
 struct HuffLutHeader {

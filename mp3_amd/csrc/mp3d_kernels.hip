@@ -266,7 +266,8 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap
 #define HUFF_ROUNDS 4                    /* 64-unit rounds per super-chunk          */
 #define HUFF_SUPER (64 * HUFF_ROUNDS)    /* units ranked together by big_values     */
 #define HUFF_BLOCK (64 * HUFF_WAVES)
-#define HUFF_CAPW 2400 /* staged bitstream words per wave (9.6 KB)            */
+#define HUFF_CAPW 2400 /* LDS words per wave (9.6 KB): staging + round order    */
+#define HUFF_STAGEW (HUFF_CAPW - HUFF_SUPER / 2) /* staging words; the u16 order follows */
 
 /* One wave per data region: LDS operations of a wave complete in issue
  * order, so an LDS hand-off between lanes of ONE wave only needs the
@@ -416,41 +417,52 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
     const int n_super = (n_units + HUFF_SUPER - 1) / HUFF_SUPER;
 
     for (int sc = blockIdx.x * HUFF_WAVES + wv; sc < n_super; sc += gridDim.x * HUFF_WAVES) {
-        /* ---- order the super-chunk's units by big_values, so each 64-unit
-         * round holds units of similar length (the big_values loop runs
-         * max-over-lanes iterations) */
+        /* ---- order the super-chunk's units by big_values (counting sort in
+         * LDS: histogram by ds_add_rtn, wave scan), so each 64-unit round
+         * holds units of similar length -- the big_values loop runs
+         * max-over-lanes iterations.  The order (u16) lives past the
+         * staging area, the histogram in it. */
         const int ubase = sc * HUFF_SUPER;
-        uint32_t key[HUFF_ROUNDS];
+        uint16_t *order16 = (uint16_t *)(bits + HUFF_STAGEW + 4);
+        wave_sync();
+        for (int i = lane; i < 320; i += 64) bits[i] = 0u;
+        wave_sync();
+        uint32_t bvk[HUFF_ROUNDS], slot[HUFF_ROUNDS];
 #pragma unroll
         for (int j = 0; j < HUFF_ROUNDS; j++) {
-            const int li = 64 * j + lane, u = ubase + li;
-            const uint32_t bv = u < n_units ? (uint32_t)(sideu[u] >> 43) & 0x1FFu : 0u;
-            key[j] = (bv << 9) | (uint32_t)li;
+            const int u = ubase + 64 * j + lane;
+            bvk[j] = u < n_units ? (uint32_t)(sideu[u] >> 43) & 0x1FFu : 0u;
+            bvk[j] = bvk[j] < 320u ? bvk[j] : 319u;
+            slot[j] = atomicAdd(&bits[bvk[j]], 1u);
+        }
+        wave_sync();
+        {   /* exclusive prefix over the 320 bins: lane owns bins 5 lane .. +4 */
+            uint32_t c[5], sum = 0;
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+                c[k] = bits[5 * lane + k];
+                sum += c[k];
+            }
+            uint32_t incl = sum;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = __shfl_up(incl, o);
+                if (lane >= o) incl += t;
+            }
+            uint32_t run = incl - sum;
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+                bits[5 * lane + k] = run;
+                run += c[k];
+            }
         }
         wave_sync();
 #pragma unroll
-        for (int j = 0; j < HUFF_ROUNDS; j++) bits[64 * j + lane] = key[j];
-        wave_sync();
-        uint32_t rank[HUFF_ROUNDS];
-#pragma unroll
-        for (int j = 0; j < HUFF_ROUNDS; j++) rank[j] = 0;
-        for (int i = 0; i < HUFF_SUPER; i += 4) {
-            const uint4 k4 = *(const uint4 *)&bits[i];
-#pragma unroll
-            for (int j = 0; j < HUFF_ROUNDS; j++)
-                rank[j] += (k4.x < key[j]) + (k4.y < key[j]) + (k4.z < key[j]) + (k4.w < key[j]);
-        }
-        wave_sync();
-#pragma unroll
-        for (int j = 0; j < HUFF_ROUNDS; j++) bits[HUFF_SUPER + rank[j]] = key[j] & 0x1FFu;
-        wave_sync();
-        int order[HUFF_ROUNDS];
-#pragma unroll
-        for (int j = 0; j < HUFF_ROUNDS; j++) order[j] = (int)bits[HUFF_SUPER + 64 * j + lane];
+        for (int j = 0; j < HUFF_ROUNDS; j++) order16[bits[bvk[j]] + slot[j]] = (uint16_t)(64 * j + lane);
         wave_sync();
 
         for (int rd = 0; rd < HUFF_ROUNDS; rd++) {
-            const int u = ubase + order[rd];
+            const int u = ubase + (int)order16[64 * rd + lane];
             const int fr = u >> 2, gr = (u >> 1) & 1, ch = u & 1;
             bool valid = u < n_units;
             FrameRec r;
@@ -500,7 +512,7 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
 #pragma unroll
                 for (int o = 1; o < 64; o <<= 1) mo = min(mo, (uint32_t)__shfl_xor(mo, o));
                 const uint32_t base = mo;
-                const bool inb = pending && off + len - base <= HUFF_CAPW;
+                const bool inb = pending && off + len - base <= HUFF_STAGEW;
                 wave_sync();
                 /* stage: each lane copies its own segment, 4 x 16 B in flight */
                 if (inb) {
@@ -575,8 +587,8 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                         /* second level, branch-free: i2 = i1 for a leaf */
                         const uint32_t nb = (e1 >> 11) & 15u;
                         const uint32_t sub =
-                            ((e1 & 0x7FFu) << 1) + (uint32_t)((((uint64_t)hi << b1) & 0xFFFFFFFFull) >> (32u - nb));
-                        const uint32_t i2 = i1 + ((sub + tb - i1) & (0u - (e1 >> 15)));
+                            ((e1 & 0x7FFu) << 2) + (uint32_t)((((uint64_t)hi << b1) & 0xFFFFFFFFull) >> (32u - nb));
+                        const uint32_t i2 = (e1 & 0x8000u) ? sub : i1;
                         const uint32_t e = s_lut[i2];
                         const uint32_t x = (e >> 4) & 15u, y = e & 15u, len_c = (e >> 8) & 31u;
                         /* linbits and signs follow the code: <= 28 bits, all in
@@ -875,9 +887,6 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
 #pragma unroll
                     for (int i = 0; i < 5; i++) cis[c][i] = nis[c][i];
                 if (lane < 2 * MW && lane / MW < nch) ((uint32_t *)&sM[0])[lane] = nmeta;
-                /* the next granule's loads fly during this one */
-                if (gr == 0) prefetch(up + 1);
-                else if (f + 1 < F) prefetch(up + 1);
                 wave_sync();
                 bt0 = sM[0].block_type;
                 mx0 = sM[0].mixed;
@@ -993,6 +1002,10 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                         xv[1][k] = lv - rv;
                     }
                 }
+                /* the next granule's loads fly during phases I, M, W (issued
+                 * after cis is consumed: fewer live registers in phase Q) */
+                if (gr == 0) prefetch(up + 1);
+                else if (f + 1 < F) prefetch(up + 1);
                 /* scatter in (short-block reordered) position */
 #pragma unroll
                 for (int i = 0; i < 5; i++) {
@@ -1227,9 +1240,10 @@ void launch_huffman(const uint8_t *md, const uint64_t *md_off, const FrameRec *r
                     hipStream_t strm) {
     int n_units = n_streams * F * 4;
     int supers = (n_units + HUFF_SUPER - 1) / HUFF_SUPER;
+    /* one super-chunk per wave, no grid-stride: the hardware hands out
+     * blocks as CUs free up, so uneven super-chunks balance themselves */
     int blocks = (supers + HUFF_WAVES - 1) / HUFF_WAVES;
-    int cap = n_cu * 12;
-    if (blocks > cap) blocks = cap;
+    (void)n_cu;
     hipLaunchKernelGGL(k_huffman, dim3(blocks), dim3(HUFF_BLOCK), 0, strm, md, md_off, rec, sideu, tab, is_buf, meta,
                        n_units, F);
 }
