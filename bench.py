@@ -149,7 +149,7 @@ def main():
 
     # --- per-kernel device time (HIP events on the decode stream) ---------
     dec.set_timing(True)
-    kt = {"scan": 0.0, "gather": 0.0, "huffman": 0.0, "synth": 0.0}
+    kt = {"demux": 0.0, "huffman": 0.0, "synth": 0.0}
     reps = max(1, min(3, args.steps))
     for _ in range(reps):
         step()

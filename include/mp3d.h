@@ -119,9 +119,9 @@ MP3D_API const char *mp3d_strerror(int err);
 MP3D_API int mp3d_last_hip_error(void);
 MP3D_API int mp3d_abi_version(void);
 /* device-side microseconds of each pipeline kernel in the last batch call
- * (scan, gather, huffman, synth); needs mp3d_batch_set_timing(b, 1).        */
+ * (demux, huffman, synth); needs mp3d_batch_set_timing(b, 1).               */
 MP3D_API int mp3d_batch_set_timing(mp3d_batch *b, int enable);
-MP3D_API int mp3d_batch_kernel_times(mp3d_batch *b, float *us4);
+MP3D_API int mp3d_batch_kernel_times(mp3d_batch *b, float *us3);
 
 #ifdef __cplusplus
 }

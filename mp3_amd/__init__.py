@@ -177,9 +177,9 @@ class BatchDecoder:
         _check(lib().mp3d_batch_set_timing(self._h, int(on)))
 
     def kernel_times_us(self):
-        t = np.zeros(4, np.float32)
+        t = np.zeros(3, np.float32)
         _check(lib().mp3d_batch_kernel_times(self._h, t.ctypes.data))
-        return dict(zip(("scan", "gather", "huffman", "synth"), t.tolist()))
+        return dict(zip(("demux", "huffman", "synth"), t.tolist()))
 
     @staticmethod
     def _geom(offsets, sizes):

@@ -23,10 +23,8 @@
 namespace mp3d {
 hipError_t upload_constants(const float *, const float *, const float *, const float *, const float *, const float *,
                             const float *);
-void launch_scan(const uint8_t *, const uint64_t *, const uint32_t *, StreamState *, FrameRec *, uint64_t *, int32_t *,
-                 void *, int, int, hipStream_t);
-void launch_gather(const uint8_t *, uint8_t *, const uint64_t *, StreamState *, const FrameRec *, const int32_t *, int,
-                   int, hipStream_t);
+void launch_demux(const uint8_t *, const uint64_t *, const uint32_t *, uint8_t *, const uint64_t *, StreamState *,
+                  FrameRec *, uint64_t *, void *, int, int, hipStream_t);
 void launch_huffman(const uint8_t *, const uint64_t *, const FrameRec *, const uint64_t *, const DevTables *, int16_t *,
                     UnitMeta *, int, int, int, hipStream_t);
 void launch_synth(const FrameRec *, const int16_t *, const UnitMeta *, const DevTables *, StreamState *, int16_t *, int,
@@ -244,10 +242,9 @@ struct mp3d_batch {
     hipStream_t own = nullptr;
     StreamState *st = nullptr;
     FrameRec *rec = nullptr;
-    uint64_t *sideu = nullptr; /* per-unit side info (k_scan -> k_huffman) */
+    uint64_t *sideu = nullptr; /* per-unit side info (k_demux -> k_huffman) */
     int16_t *is_buf = nullptr;
     UnitMeta *meta = nullptr;
-    int32_t *carry = nullptr;
     uint64_t *d_in_off = nullptr, *d_md_off = nullptr;
     uint32_t *d_in_len = nullptr;
     mp3d_frame_info *d_infos = nullptr;
@@ -264,7 +261,7 @@ struct mp3d_batch {
     std::vector<uint32_t> last_len;
     int last_n = -1;
     bool timing = false;
-    hipEvent_t ev[5] = {};
+    hipEvent_t ev[4] = {};
     float times[4] = {0, 0, 0, 0};
 };
 
@@ -313,7 +310,6 @@ extern "C" int mp3d_batch_create(int device, int max_streams, int max_frames, mp
     BALLOC(b->sideu, sizeof(uint64_t) * units);
     BALLOC(b->is_buf, sizeof(int16_t) * 576 * units);
     BALLOC(b->meta, sizeof(UnitMeta) * units);
-    BALLOC(b->carry, sizeof(int32_t) * 2 * max_streams);
     BALLOC(b->d_in_off, sizeof(uint64_t) * max_streams);
     BALLOC(b->d_md_off, sizeof(uint64_t) * max_streams);
     BALLOC(b->d_in_len, sizeof(uint32_t) * max_streams);
@@ -323,7 +319,7 @@ extern "C" int mp3d_batch_create(int device, int max_streams, int max_frames, mp
         mp3d_batch_destroy(b);
         return MP3D_E_HIP;
     }
-    for (int i = 0; i < 5; i++) (void)hipEventCreate(&b->ev[i]);
+    for (int i = 0; i < 4; i++) (void)hipEventCreate(&b->ev[i]);
     if (hipMemset(b->st, 0, sizeof(StreamState) * max_streams) != hipSuccess) {
         mp3d_batch_destroy(b);
         return MP3D_E_HIP;
@@ -336,7 +332,7 @@ extern "C" void mp3d_batch_destroy(mp3d_batch *b) {
     if (!b) return;
     (void)hipSetDevice(b->device);
     if (b->own) (void)hipStreamSynchronize(b->own);
-    void *ptrs[] = {b->st, b->rec, b->sideu, b->is_buf, b->meta, b->carry, b->d_in_off, b->d_md_off, b->d_in_len,
+    void *ptrs[] = {b->st, b->rec, b->sideu, b->is_buf, b->meta, b->d_in_off, b->d_md_off, b->d_in_len,
                     b->d_infos, b->md, b->d_in, b->d_pcm, b->d_xr, b->d_bt, b->d_mx};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
@@ -368,14 +364,14 @@ extern "C" int mp3d_batch_set_timing(mp3d_batch *b, int enable) {
     return MP3D_OK;
 }
 
-extern "C" int mp3d_batch_kernel_times(mp3d_batch *b, float *us4) {
-    if (!b || !us4) return MP3D_E_ARG;
+extern "C" int mp3d_batch_kernel_times(mp3d_batch *b, float *us3) {
+    if (!b || !us3) return MP3D_E_ARG;
     if (!b->timing) return MP3D_E_ARG;
-    HIPCHK(hipEventSynchronize(b->ev[4]));
-    for (int i = 0; i < 4; i++) {
+    HIPCHK(hipEventSynchronize(b->ev[3]));
+    for (int i = 0; i < 3; i++) {
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, b->ev[i], b->ev[i + 1]));
-        us4[i] = ms * 1000.f;
+        us3[i] = ms * 1000.f;
     }
     return MP3D_OK;
 }
@@ -405,8 +401,8 @@ static int prepare_geometry(mp3d_batch *b, const uint64_t *offsets, const uint32
     return MP3D_OK;
 }
 
-/* Front half shared by decode and huffman_only: input staging + k_scan,
- * k_gather, k_huffman. */
+/* Front half shared by decode and huffman_only: input staging, k_demux,
+ * k_huffman. */
 static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets, const uint32_t *sizes, int n,
                      int F, hipStream_t s, bool *sync_needed) {
     if (!b || !frames || !offsets || !sizes || n <= 0 || F <= 0) return MP3D_E_ARG;
@@ -426,12 +422,11 @@ static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offse
     if (r) return r;
     DeviceCtx &dc = g_dev[b->device];
     if (b->timing) HIPCHK(hipEventRecord(b->ev[0], s));
-    launch_scan(din, b->d_in_off, b->d_in_len, b->st, b->rec, b->sideu, b->carry, b->d_infos, n, F, s);
+    /* demux + main-data gather in one pass */
+    launch_demux(din, b->d_in_off, b->d_in_len, b->md, b->d_md_off, b->st, b->rec, b->sideu, b->d_infos, n, F, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[1], s));
-    launch_gather(din, b->md, b->d_md_off, b->st, b->rec, b->carry, n, F, s);
-    if (b->timing) HIPCHK(hipEventRecord(b->ev[2], s));
     launch_huffman(b->md, b->d_md_off, b->rec, b->sideu, dc.tables, b->is_buf, b->meta, n, F, dc.n_cu, s);
-    if (b->timing) HIPCHK(hipEventRecord(b->ev[3], s));
+    if (b->timing) HIPCHK(hipEventRecord(b->ev[2], s));
     HIPCHK(hipGetLastError());
     return MP3D_OK;
 }
@@ -455,7 +450,7 @@ extern "C" int mp3d_batch_decode(mp3d_batch *b, const uint8_t *frames, const uin
     }
     DeviceCtx &dc = g_dev[b->device];
     launch_synth(b->rec, b->is_buf, b->meta, dc.tables, b->st, dpcm, n, F, s);
-    if (b->timing) HIPCHK(hipEventRecord(b->ev[4], s));
+    if (b->timing) HIPCHK(hipEventRecord(b->ev[3], s));
     HIPCHK(hipGetLastError());
     if (pcm_host) {
         HIPCHK(hipMemcpyAsync(pcm, dpcm, pcm_bytes, hipMemcpyDeviceToHost, s));
@@ -539,10 +534,10 @@ extern "C" int mp3d_batch_synth_only(mp3d_batch *b, const float *xr, const uint8
     }
     DeviceCtx &dc = g_dev[b->device];
     if (b->timing) {
-        for (int i = 0; i < 4; i++) HIPCHK(hipEventRecord(b->ev[i], s));
+        for (int i = 0; i < 3; i++) HIPCHK(hipEventRecord(b->ev[i], s));
     }
     launch_synth_xr(dxr, dbt, dmx, dc.tables, b->st, dpcm, n, F, nch, sr, s);
-    if (b->timing) HIPCHK(hipEventRecord(b->ev[4], s));
+    if (b->timing) HIPCHK(hipEventRecord(b->ev[3], s));
     HIPCHK(hipGetLastError());
     if (pcm_host) {
         HIPCHK(hipMemcpyAsync(pcm, dpcm, pcm_bytes, hipMemcpyDeviceToHost, s));

@@ -4,7 +4,7 @@
  *
  * HBM layout of one batch (SoA, one process per GPU):
  *   input   : caller's frame bytes, stream s at in_off[s] (u64), in_len[s]
- *   rec     : FrameRec[n_streams * F]         (k_scan, 32 B per frame)
+ *   rec     : FrameRec[n_streams * F]         (k_demux, 32 B per frame)
  *   md      : per-stream main-data byte region (carry-in + payloads),
  *             stream s at md_off[s] (16-B aligned), read as big-endian words
  *   is_buf  : int16 [n_streams * F * 4][576]  (k_huffman -> k_synth)
@@ -22,7 +22,7 @@
 #define MP3D_FIFO_SLOTS 15       /* synthesis history slots carried        */
 #define MP3D_MAX_FRAME_BYTES 1441
 
-/* Per-frame record written by k_scan. */
+/* Per-frame record written by k_demux. */
 struct FrameRec {
     uint64_t frame_off;  /* byte offset of the frame header in input        */
     uint32_t md_bit;     /* bit offset of main-data start inside md region   */

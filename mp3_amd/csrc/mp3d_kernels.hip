@@ -5,14 +5,14 @@
  * decode loop (REF/README.md:2-3) is the path these kernels replace.
  *
  * Pipeline for one batch call (all on one HIP stream, state resident in HBM):
- *   k_scan     thread / stream  : header + side-info walk, bit-reservoir map
- *   k_gather   block  / stream  : main-data bytes -> contiguous md region
+ *   k_demux    wave   / stream  : header + side-info walk, bit-reservoir map,
+ *                                 main-data bytes -> contiguous md region
  *   k_huffman  thread / unit    : scalefactors + Huffman (LDS LUT) -> is[576]
  *   k_synth    wave   / stream  : requantise, stereo, alias, IMDCT, overlap,
  *                                 32-band matrixing + 512-tap window -> PCM
  * A unit is one (frame, granule, channel).  Streams are independent, so the
  * batch is embarrassingly parallel over streams; frames of one stream are
- * walked in order inside k_scan / k_synth, which keep the per-stream state
+ * walked in order inside k_demux / k_synth, which keep the per-stream state
  * (reservoir, overlap, synthesis FIFO) in registers / LDS between frames.
  */
 #include <hip/hip_runtime.h>
@@ -43,16 +43,6 @@ struct DevInfo { /* mirrors mp3d_frame_info (include/mp3d.h) */
 /* ------------------------------------------------------------------------ */
 /* Header / side-info helpers (ISO 2.4.1.3, 2.4.1.7)                          */
 /* ------------------------------------------------------------------------ */
-__device__ __forceinline__ uint32_t ld_be32(const uint8_t *p) {
-    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
-}
-
-/* bits [pos, pos+n) of a byte array, n <= 24 */
-__device__ __forceinline__ uint32_t bits_at(const uint8_t *p, uint32_t pos, int n) {
-    uint32_t w = ld_be32(p + (pos >> 3));
-    return (w << (pos & 7)) >> (32 - n);
-}
-
 __device__ __forceinline__ int hdr_frame_bytes(uint8_t b1, uint8_t b2) {
     if ((b1 & 0xFE) != 0xFA) return -1;
     int bi = b2 >> 4, si = (b2 >> 2) & 3;
@@ -66,187 +56,223 @@ __device__ __forceinline__ uint32_t side_unit_bit(int nch, int gr, int ch) {
 }
 
 /* ------------------------------------------------------------------------ */
-/* k_scan: one thread per stream.  Walks the stream's frames (ISO 2.4.1.3), */
-/* maps each frame's main data into the stream's md region (bit reservoir, */
-/* ISO 2.4.3.4 main_data_begin; FFmpeg's underflow rule), records results. */
+/* k_demux: one wave per stream.  Walks the stream's frames (ISO 2.4.1.3),   */
+/* maps each frame's main data into the stream's md region (bit reservoir,  */
+/* ISO 2.4.3.4 main_data_begin, FFmpeg's underflow / drop rules), writes    */
+/* FrameRec + per-unit side words, and copies the payload bytes into md --  */
+/* the demux and the main-data gather in one pass.  The next frame's 64-B   */
+/* header window is loaded while the current payload is copied, so the     */
+/* serial header walk costs about one load latency per frame.              */
 /* ------------------------------------------------------------------------ */
-__global__ void __launch_bounds__(256) k_scan(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
-                                              const uint32_t *__restrict__ in_len, StreamState *__restrict__ st,
+struct HdrWin {        /* 64 bytes at a stream position, spread over lanes 0..15 */
+    uint32_t le;       /* lane i: little-endian dword at (pos & ~3) + 4 i        */
+    uint32_t pos;
+};
+
+__device__ __forceinline__ HdrWin load_win(const uint8_t *p0, uint32_t len, uint32_t pos, int lane) {
+    HdrWin w;
+    w.pos = pos;
+    const uint32_t a = (pos & ~3u) + 4u * (uint32_t)lane;
+    /* a dword is read only if it starts inside the stream: it then cannot
+     * leave the caller's allocation */
+    w.le = (lane < 16 && a < len) ? *(const uint32_t *)(p0 + a) : 0u;
+    return w;
+}
+
+/* byte k of the window (uniform k; k + (pos & 3) < 64) */
+__device__ __forceinline__ uint32_t win_byte(const HdrWin &w, uint32_t k) {
+    const uint32_t i = k + (w.pos & 3u);
+    const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)w.le, (int)(i >> 2));
+    return (d >> (8 * (i & 3u))) & 0xFFu;
+}
+
+/* 64 bits of the window's big-endian bit string starting at bit b of byte
+ * position (w.pos & ~3) -- per lane b (lane-varying) */
+__device__ __forceinline__ uint64_t win_bits64(const HdrWin &w, uint32_t b) {
+    const uint32_t be = __builtin_bswap32(w.le);
+    const int wi = (int)(b >> 5);
+    const uint32_t x0 = (uint32_t)__shfl((int)be, wi), x1 = (uint32_t)__shfl((int)be, wi + 1),
+                   x2 = (uint32_t)__shfl((int)be, wi + 2);
+    const uint32_t sh = b & 31u;
+    const uint64_t hi = ((uint64_t)x0 << 32) | x1;
+    return sh ? (hi << sh) | ((uint64_t)x2 >> (32 - sh)) : hi;
+}
+
+__global__ void __launch_bounds__(64) k_demux(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
+                                              const uint32_t *__restrict__ in_len, uint8_t *__restrict__ md,
+                                              const uint64_t *__restrict__ md_off, StreamState *__restrict__ st,
                                               FrameRec *__restrict__ rec, uint64_t *__restrict__ sideu,
-                                              int32_t *__restrict__ carry, DevInfo *__restrict__ infos,
-                                              int n_streams, int F) {
-    int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n_streams) return;
+                                              DevInfo *__restrict__ infos, int F) {
+    const int s = blockIdx.x;
+    const int lane = threadIdx.x;
     const uint8_t *p0 = in + in_off[s];
-    uint32_t len = in_len[s];
-    uint32_t cur = 0;
-    const int carry_in = st[s].res_len;
-    const int stream_start = st[s].frames == 0;
+    const uint32_t len = in_len[s];
+    uint8_t *dst = md + md_off[s];
+    StreamState &S = st[s];
+    const int carry_in = S.res_len;
+    const bool stream_start = S.frames == 0;
+    for (int i = lane; i < (carry_in + 3) / 4; i += 64) ((uint32_t *)dst)[i] = ((const uint32_t *)S.res)[i];
+    __threadfence_block(); /* carry words may spill past carry_in into payload 0's head */
+
     uint32_t P = (uint32_t)carry_in; /* md position of the next payload         */
     int avail = carry_in;            /* bytes after the previous main-data end */
-    if (stream_start && len >= 10 && p0[0] == 'I' && p0[1] == 'D' && p0[2] == '3') {
-        uint32_t sz = ((uint32_t)(p0[6] & 0x7F) << 21) | ((uint32_t)(p0[7] & 0x7F) << 14) |
-                      ((uint32_t)(p0[8] & 0x7F) << 7) | (p0[9] & 0x7F);
-        cur = 10 + sz + ((p0[5] & 0x10) ? 10 : 0);
+    uint32_t cur = 0;
+    HdrWin w = load_win(p0, len, 0, lane);
+    if (stream_start && len >= 10 && win_byte(w, 0) == 'I' && win_byte(w, 1) == 'D' && win_byte(w, 2) == '3') {
+        const uint32_t sz = (win_byte(w, 6) & 0x7Fu) << 21 | (win_byte(w, 7) & 0x7Fu) << 14 |
+                            (win_byte(w, 8) & 0x7Fu) << 7 | (win_byte(w, 9) & 0x7Fu);
+        cur = 10 + sz + ((win_byte(w, 5) & 0x10u) ? 10u : 0u);
+        w = load_win(p0, len, cur, lane);
     }
     int decoded = 0;
     for (int f = 0; f < F; f++) {
+        const size_t fi = (size_t)s * F + f;
+        /* ---- sync: the next valid header at or after cur (resync over junk) */
+        int fb = -1;
+        while (cur + 4 <= len) {
+            if (w.pos != cur) w = load_win(p0, len, cur, lane);
+            const uint32_t lim = min(57u, len - cur - 4);
+            uint32_t k = 0;
+            for (; k <= lim; k++) {
+                if (win_byte(w, k) == 0xFFu) {
+                    fb = hdr_frame_bytes((uint8_t)win_byte(w, k + 1), (uint8_t)win_byte(w, k + 2));
+                    if (fb > 0) break;
+                }
+            }
+            cur += k;
+            if (fb > 0) break;
+        }
         FrameRec r;
         r.frame_off = 0; r.md_bit = 0; r.payload_md = P; r.frame_bytes = 0; r.payload_len = 0;
         r.hdr1 = r.hdr2 = r.hdr3 = 0; r.nch = 0; r.side_off = 4; r.first_gr = 0; r.sr_idx = 0; r.pad_ = 0;
         r.payload_avail = 0;
         DevInfo inf = {0, 0, 0, 0, 0, 0};
-        int fb = -1;
-        while (cur + 4 <= len) {
-            if (p0[cur] == 0xFF) {
-                fb = hdr_frame_bytes(p0[cur + 1], p0[cur + 2]);
-                if (fb > 0) break;
-            }
-            cur++;
-        }
-        /* a final frame cut short still decodes (FFmpeg: the missing bytes
-         * read as zeros) once its header and side info are present */
-        const uint32_t need = fb > 0 ? 4u + ((p0[cur + 1] & 1) ? 0u : 2u) + ((p0[cur + 3] >> 6) == 3 ? 17u : 32u) : 0u;
-        if (fb > 0 && (cur + (uint32_t)fb <= len || cur + need <= len)) {
-            const uint8_t *fp = p0 + cur;
-            int nch = (fp[3] >> 6) == 3 ? 1 : 2;
-            int crc = (fp[1] & 1) ? 0 : 2;
-            int side_bytes = nch == 1 ? 17 : 32;
-            const uint32_t have = min(len - cur, (uint32_t)fb); /* bytes of this frame present */
-            int plen = fb - 4 - crc - side_bytes;
-            const uint8_t *side = fp + 4 + crc;
-            r.frame_off = in_off[s] + cur;
-            r.frame_bytes = (uint16_t)fb;
-            r.payload_len = (uint16_t)(plen > 0 ? plen : 0);
-            r.hdr1 = fp[1]; r.hdr2 = fp[2]; r.hdr3 = fp[3];
-            r.nch = (uint8_t)nch;
-            r.side_off = (uint8_t)(4 + crc);
-            r.sr_idx = (uint8_t)((fp[2] >> 2) & 3);
-            inf.frame_bytes = fb; inf.channels = nch; inf.hz = (int)MP3D_SAMPLE_RATE[r.sr_idx];
-            inf.layer = 3; inf.bitrate_kbps = MP3D_BITRATE_L3[fp[2] >> 4];
-            const uint8_t *tg = side + side_bytes;
-            bool tag = stream_start && f == 0 && plen >= 4 && have == (uint32_t)fb &&
-                       ((tg[0] == 'X' && tg[1] == 'i' && tg[2] == 'n' && tg[3] == 'g') ||
-                        (tg[0] == 'I' && tg[1] == 'n' && tg[2] == 'f' && tg[3] == 'o'));
-            int mdb = (int)bits_at(side, 0, 9);
-            int p23[2][2] = {{0, 0}, {0, 0}};
-            bool bad = plen < 0;
-            for (int gr = 0; gr < 2; gr++)
-                for (int ch = 0; ch < 2; ch++) {
-                    uint64_t sw = 0;
-                    if (ch < nch && !bad) {
-                        const uint32_t b = side_unit_bit(nch, gr, ch);
-                        p23[gr][ch] = (int)bits_at(side, b, 12);
-                        if (bits_at(side, b + 12, 9) > 288) bad = true; /* SURVEY A.9 (5) */
-                        /* the unit's 59 side-info bits, MSB first, from bit 63;
-                         * this channel's scfsi in bits 4..1 (k_huffman) */
-                        const uint64_t v = ((uint64_t)bits_at(side, b, 20) << 39) |
-                                           ((uint64_t)bits_at(side, b + 20, 20) << 19) | bits_at(side, b + 40, 19);
-                        const uint32_t scfsi = bits_at(side, 9 + (nch == 1 ? 5 : 3) + 4 * ch, 4);
-                        sw = (v << 5) | ((uint64_t)scfsi << 1);
-                    }
-                    sideu[((size_t)s * F + f) * 4 + gr * 2 + ch] = sw;
-                }
-            if (tag) {
-                r.first_gr = REC_TAG;
-            } else if (bad) {
-                /* FFmpeg drops the frame; its reservoir restarts as the frame's
-                 * last min(512, bytes - 4) post-header bytes (mp_decode_frame) */
-                r.first_gr = REC_DROP;
-                r.payload_len = (uint16_t)(fb - 4);
-                avail = fb - 4 < MP3D_RES_BYTES ? fb - 4 : MP3D_RES_BYTES;
-                P += (uint32_t)r.payload_len;
-            } else {
-                int gr0 = 0;
-                uint32_t mdbit;
-                if (mdb <= avail) {
-                    mdbit = (P - (uint32_t)mdb) * 8u;
+        uint64_t sw = 0; /* lane q < 4: side word of unit q = gr * 2 + ch */
+        bool copy = false;
+        uint32_t src_off = 0;
+        if (fb > 0) {
+            if (w.pos != cur) w = load_win(p0, len, cur, lane);
+            const uint32_t h1 = win_byte(w, 1), h2 = win_byte(w, 2), h3 = win_byte(w, 3);
+            const int nch = (h3 >> 6) == 3 ? 1 : 2;
+            const int crc = (h1 & 1) ? 0 : 2;
+            const int side_bytes = nch == 1 ? 17 : 32;
+            const uint32_t need = 4u + (uint32_t)crc + (uint32_t)side_bytes;
+            /* a final frame cut short still decodes (FFmpeg: the missing bytes
+             * read as zeros) once its header and side info are present */
+            if (cur + (uint32_t)fb <= len || cur + need <= len) {
+                const uint32_t have = min(len - cur, (uint32_t)fb);
+                const int plen = fb - 4 - crc - side_bytes;
+                r.frame_off = in_off[s] + cur;
+                r.frame_bytes = (uint16_t)fb;
+                r.payload_len = (uint16_t)(plen > 0 ? plen : 0);
+                r.hdr1 = (uint8_t)h1; r.hdr2 = (uint8_t)h2; r.hdr3 = (uint8_t)h3;
+                r.nch = (uint8_t)nch;
+                r.side_off = (uint8_t)(4 + crc);
+                r.sr_idx = (uint8_t)((h2 >> 2) & 3);
+                inf.frame_bytes = fb; inf.channels = nch; inf.hz = (int)MP3D_SAMPLE_RATE[r.sr_idx];
+                inf.layer = 3; inf.bitrate_kbps = MP3D_BITRATE_L3[h2 >> 4];
+                /* side info: bit offsets relative to the window's dword base */
+                const uint32_t sbit = 8u * ((cur & 3u) + 4u + (uint32_t)crc);
+                const int mdb = (int)(win_bits64(w, sbit) >> 55);
+                const int q = lane & 3, qgr = q >> 1, qch = q & 1;
+                const uint32_t ub = sbit + side_unit_bit(nch, qgr, qch);
+                const uint64_t v59 = win_bits64(w, ub) >> 5;
+                const uint32_t scfsi = (uint32_t)(win_bits64(w, sbit + 9 + (nch == 1 ? 5 : 3) + 4 * qch) >> 60);
+                const bool unit_ok = lane < 4 && qch < nch;
+                const uint32_t myp23 = unit_ok ? (uint32_t)(v59 >> 47) : 0u;
+                const bool mybad = unit_ok && ((v59 >> 38) & 0x1FFu) > 288u; /* SURVEY A.9 (5) */
+                sw = unit_ok ? (v59 << 5) | ((uint64_t)scfsi << 1) : 0ull;
+                int p23[2][2];
+                p23[0][0] = __builtin_amdgcn_readlane((int)myp23, 0);
+                p23[0][1] = __builtin_amdgcn_readlane((int)myp23, 1);
+                p23[1][0] = __builtin_amdgcn_readlane((int)myp23, 2);
+                p23[1][1] = __builtin_amdgcn_readlane((int)myp23, 3);
+                const bool bad = plen < 0 || __ballot(mybad) != 0ull;
+                const uint32_t tgo = 4u + (uint32_t)crc + (uint32_t)side_bytes;
+                const bool tag = stream_start && f == 0 && plen >= 4 && have == (uint32_t)fb &&
+                                 ((win_byte(w, tgo) == 'X' && win_byte(w, tgo + 1) == 'i' && win_byte(w, tgo + 2) == 'n' &&
+                                   win_byte(w, tgo + 3) == 'g') ||
+                                  (win_byte(w, tgo) == 'I' && win_byte(w, tgo + 1) == 'n' && win_byte(w, tgo + 2) == 'f' &&
+                                   win_byte(w, tgo + 3) == 'o'));
+                if (tag) {
+                    r.first_gr = REC_TAG;
+                } else if (bad) {
+                    /* FFmpeg drops the frame; its reservoir restarts as the frame's
+                     * last min(512, bytes - 4) post-header bytes (mp_decode_frame) */
+                    r.first_gr = REC_DROP;
+                    r.payload_len = (uint16_t)(fb - 4);
+                    avail = fb - 4 < MP3D_RES_BYTES ? fb - 4 : MP3D_RES_BYTES;
+                    P += (uint32_t)r.payload_len;
                 } else {
-                    uint32_t bits = (uint32_t)avail * 8u;
-                    while (gr0 < 2 && (int)(bits >> 3) < mdb) {
-                        for (int ch = 0; ch < nch; ch++) bits += (uint32_t)p23[gr0][ch];
-                        gr0++;
+                    int gr0 = 0;
+                    uint32_t mdbit;
+                    if (mdb <= avail) {
+                        mdbit = (P - (uint32_t)mdb) * 8u;
+                    } else {
+                        uint32_t bits = (uint32_t)avail * 8u;
+                        while (gr0 < 2 && (int)(bits >> 3) < mdb) {
+                            for (int ch = 0; ch < nch; ch++) bits += (uint32_t)p23[gr0][ch];
+                            gr0++;
+                        }
+                        mdbit = (P - (uint32_t)avail) * 8u + bits - 8u * (uint32_t)mdb;
                     }
-                    mdbit = (P - (uint32_t)avail) * 8u + bits - 8u * (uint32_t)mdb;
+                    uint32_t end = mdbit;
+                    for (int gr = gr0; gr < 2; gr++)
+                        for (int ch = 0; ch < nch; ch++) end += (uint32_t)p23[gr][ch];
+                    r.md_bit = mdbit;
+                    r.first_gr = (uint8_t)gr0;
+                    P += (uint32_t)plen;
+                    const int64_t after = (int64_t)P - (int64_t)((end + 7u) >> 3);
+                    avail = after < 0 ? 0 : (int)after;
+                    inf.samples = 1152;
+                    decoded++;
                 }
-                uint32_t end = mdbit;
-                for (int gr = gr0; gr < 2; gr++)
-                    for (int ch = 0; ch < nch; ch++) end += (uint32_t)p23[gr][ch];
-                r.md_bit = mdbit;
-                r.first_gr = (uint8_t)gr0;
-                P += (uint32_t)plen;
-                int64_t after = (int64_t)P - (int64_t)((end + 7u) >> 3);
-                avail = after < 0 ? 0 : (int)after;
-                inf.samples = 1152;
-                decoded++;
-            }
-            {
-                const uint32_t body = (r.first_gr & REC_DROP) ? 4u : 4u + (uint32_t)crc + (uint32_t)side_bytes;
+                const uint32_t body = (r.first_gr & REC_DROP) ? 4u : need;
                 const uint32_t av = have > body ? have - body : 0u;
                 r.payload_avail = (uint16_t)(av < r.payload_len ? av : r.payload_len);
+                copy = !(r.first_gr & REC_TAG);
+                src_off = cur + body;
+                cur = have == (uint32_t)fb ? cur + (uint32_t)fb : len;
+            } else {
+                cur = len;
             }
-            cur = have == (uint32_t)fb ? cur + (uint32_t)fb : len;
-        } else {
-            cur = len;
         }
-        rec[(size_t)s * F + f] = r;
-        if (infos) infos[(size_t)s * F + f] = inf;
+        /* next frame's header window in flight while this payload copies */
+        if (cur + 4 <= len && f + 1 < F) w = load_win(p0, len, cur, lane);
+        if (lane == 0) {
+            rec[fi] = r;
+            if (infos) infos[fi] = inf;
+        }
+        if (lane < 4) sideu[fi * 4 + lane] = sw;
+        if (copy) {
+            const uint8_t *src = p0 + src_off;
+            const uint32_t Pm = r.payload_md, L = r.payload_avail;
+            for (uint32_t i = L + lane; i < r.payload_len; i += 64) dst[Pm + i] = 0; /* cut-short final frame */
+            const uint32_t h = min((4u - (Pm & 3u)) & 3u, L);     /* head bytes up to an aligned word */
+            const uint32_t wb = (Pm + h) >> 2, we = (Pm + L) >> 2; /* whole words [wb, we)           */
+            if ((uint32_t)lane < h) dst[Pm + lane] = src[lane];
+            if (wb < we) {
+                const uint32_t t0 = 4u * we - Pm; /* tail bytes [t0, L) */
+                if ((uint32_t)lane < L - t0) dst[Pm + t0 + lane] = src[t0 + lane];
+                const uint64_t sa0 = (uint64_t)(src + (4u * wb - Pm));
+                const uint32_t sh = (uint32_t)(sa0 & 3u) * 8u;
+                const uint32_t *swd = (const uint32_t *)(sa0 & ~(uint64_t)3);
+                for (uint32_t k = lane; k < we - wb; k += 64) {
+                    const uint32_t lo = swd[k];
+                    ((uint32_t *)dst)[wb + k] = sh ? __builtin_amdgcn_alignbit(swd[k + 1], lo, sh) : lo;
+                }
+            }
+        }
     }
+    /* carry: the last min(avail, 512) md bytes become the next call's carry-in */
+    __syncthreads();
     int c = avail < MP3D_RES_BYTES ? avail : MP3D_RES_BYTES;
     if ((uint32_t)c > P) c = (int)P;
-    carry[2 * s] = c;
-    carry[2 * s + 1] = (int)P;
-    st[s].frames += decoded;
-}
-
-/* ------------------------------------------------------------------------ */
-/* k_gather: one block per stream.  md region = [carry-in][payload 0][...]  */
-/* then the last `carry` bytes become the next call's carry-in.  Payloads   */
-/* are copied as aligned 32-bit destination words built from two aligned   */
-/* source words (alignbit) -- the byte offsets of a payload in the input  */
-/* and in md differ arbitrarily; the <= 3 edge bytes per side go as bytes  */
-/* (a neighbouring frame owns the rest of that word).  Wave w of the block */
-/* copies frames f = w mod 4.                                              */
-/* ------------------------------------------------------------------------ */
-__global__ void __launch_bounds__(256) k_gather(const uint8_t *__restrict__ in, uint8_t *__restrict__ md,
-                                                const uint64_t *__restrict__ md_off, StreamState *__restrict__ st,
-                                                const FrameRec *__restrict__ rec, const int32_t *__restrict__ carry,
-                                                int F) {
-    const int s = blockIdx.x;
-    uint8_t *dst = md + md_off[s];
-    const int cin = st[s].res_len;
-    for (int i = threadIdx.x; i < (cin + 3) / 4; i += blockDim.x)
-        ((uint32_t *)dst)[i] = ((const uint32_t *)st[s].res)[i];
-    __syncthreads(); /* carry words may spill past cin into payload 0's head */
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    for (int f = wv; f < F; f += 4) {
-        const FrameRec r = rec[(size_t)s * F + f];
-        if (!r.frame_bytes || (r.first_gr & REC_TAG)) continue;
-        /* a dropped frame's post-header bytes (CRC, side info, payload) all
-         * enter the reservoir (FFmpeg); otherwise just the payload */
-        const uint8_t *src = in + r.frame_off + ((r.first_gr & REC_DROP) ? 4 : r.side_off + (r.nch == 1 ? 17 : 32));
-        const uint32_t P = r.payload_md, L = r.payload_avail;
-        for (uint32_t i = L + lane; i < r.payload_len; i += 64) dst[P + i] = 0; /* cut-short final frame */
-        const uint32_t h = min((4u - (P & 3u)) & 3u, L); /* head bytes up to an aligned word */
-        const uint32_t wb = (P + h) >> 2, we = (P + L) >> 2; /* whole words [wb, we) */
-        if ((uint32_t)lane < h) dst[P + lane] = src[lane];
-        const uint32_t t0 = wb > we ? 0u : 4u * we - P; /* tail bytes [t0, L) */
-        if (wb < we && (uint32_t)lane < L - t0) dst[P + t0 + lane] = src[t0 + lane];
-        if (wb < we) {
-            const uint64_t sa0 = (uint64_t)(src + (4u * wb - P));
-            const uint32_t sh = (uint32_t)(sa0 & 3u) * 8u;
-            const uint32_t *sw = (const uint32_t *)(sa0 & ~(uint64_t)3);
-            for (uint32_t w = lane; w < we - wb; w += 64) {
-                const uint32_t lo = sw[w];
-                const uint32_t v = sh ? __builtin_amdgcn_alignbit(sw[w + 1], lo, sh) : lo;
-                ((uint32_t *)dst)[wb + w] = v;
-            }
-        }
+    for (int i = lane; i < c; i += 64) S.res[i] = dst[P - c + i];
+    if (lane == 0) {
+        S.res_len = c;
+        S.frames += decoded;
     }
-    __syncthreads();
-    const int cout = carry[2 * s], pend = carry[2 * s + 1];
-    for (int i = threadIdx.x; i < cout; i += blockDim.x) st[s].res[i] = dst[pend - cout + i];
-    if (threadIdx.x == 0) st[s].res_len = cout;
 }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
@@ -260,7 +286,7 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap
 /* u16 LUT (15 code tables + count1 table A, LDS), and linbits + sign bits */
 /* taken from the same window, so the big_values loop is branch-free and   */
 /* runs max(big_values) iterations per wave whatever the region tables.     */
-/* Side info arrives pre-extracted by k_scan (one u64 per unit).            */
+/* Side info arrives pre-extracted by k_demux (one u64 per unit).           */
 /* ------------------------------------------------------------------------ */
 #define HUFF_WAVES 4
 #define HUFF_ROUNDS 4                    /* 64-unit rounds per super-chunk          */
@@ -1224,15 +1250,11 @@ hipError_t upload_constants(const float *imdct12, const float *win36, const floa
     return hipSuccess;
 }
 
-void launch_scan(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len, StreamState *st, FrameRec *rec,
-                 uint64_t *sideu, int32_t *carry, void *infos, int n_streams, int F, hipStream_t strm) {
-    hipLaunchKernelGGL(k_scan, dim3((n_streams + 255) / 256), dim3(256), 0, strm, in, in_off, in_len, st, rec, sideu,
-                       carry, (DevInfo *)infos, n_streams, F);
-}
-
-void launch_gather(const uint8_t *in, uint8_t *md, const uint64_t *md_off, StreamState *st, const FrameRec *rec,
-                   const int32_t *carry, int n_streams, int F, hipStream_t strm) {
-    hipLaunchKernelGGL(k_gather, dim3(n_streams), dim3(256), 0, strm, in, md, md_off, st, rec, carry, F);
+void launch_demux(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len, uint8_t *md,
+                  const uint64_t *md_off, StreamState *st, FrameRec *rec, uint64_t *sideu, void *infos, int n_streams,
+                  int F, hipStream_t strm) {
+    hipLaunchKernelGGL(k_demux, dim3(n_streams), dim3(64), 0, strm, in, in_off, in_len, md, md_off, st, rec, sideu,
+                       (DevInfo *)infos, F);
 }
 
 void launch_huffman(const uint8_t *md, const uint64_t *md_off, const FrameRec *rec, const uint64_t *sideu,
