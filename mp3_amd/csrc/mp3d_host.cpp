@@ -198,6 +198,8 @@ static int upload_symbols() {
         isr[p][1] = (float)(1.0 / (1.0 + tn));
     }
     for (int i = 0; i < 4; i++) p2q[i] = (float)pow(2.0, i / 4.0);
+    for (int i = 0; i < 22; i++)
+        if (((MP3D_PRETAB_BITS >> (2 * i)) & 3u) != MP3D_PRETAB[i]) return MP3D_E_ARG; /* table drift */
     HIPCHK(upload_constants(&imdct12[0][0], &win36[0][0], win12, cs, ca, &isr[0][0], p2q));
     return MP3D_OK;
 }

@@ -22,6 +22,11 @@
 #define MP3D_FIFO_SLOTS 15       /* synthesis history slots carried        */
 #define MP3D_MAX_FRAME_BYTES 1441
 
+/* MPEG-1 pretab (ISO Table B.6, MP3D_PRETAB in mp3d_tables.h) as 2 bits
+ * per long band, for lane-indexed use without a memory load; checked
+ * against the table when the device is initialised (mp3d_host.cpp). */
+#define MP3D_PRETAB_BITS 0x2fe95400000ull
+
 /* Per-frame record written by k_demux. */
 struct FrameRec {
     uint64_t frame_off;  /* byte offset of the frame header in input        */

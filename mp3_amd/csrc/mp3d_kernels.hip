@@ -768,20 +768,29 @@ __device__ __forceinline__ void imdct36_w(const float *X, float *w) {
 }
 
 /* ------------------------------------------------------------------------ */
-/* k_synth: one wave (64 lanes) per stream, frames and granules in order;   */
-/* every phase exchanges data through ONE 5 KB LDS buffer, so a wave holds  */
-/* only the per-stream state (IMDCT overlap, synthesis history) in VGPRs.   */
-/*  Q  lane = line (l = lane + 64 i): requantise both channels (ISO 2.4.3.4,*/
-/*     per-band 2^(q/4) precomputed by lane = band), joint stereo paired by */
+/* k_synth: one wave (64 lanes) per stream, frames and granules in order,   */
+/* SYN_WAVES streams per workgroup sharing the read-only tables in LDS      */
+/* (line tables of all three sample rates, |is|^(4/3), long windows, the   */
+/* matrixing A fragments and the synthesis window): after the prologue the  */
+/* granule loop issues no vector-memory load but the one-granule-ahead      */
+/* prefetch of is[] / UnitMeta / FrameRec, so no s_waitcnt vmcnt drains the */
+/* PCM stores or the prefetch early.  Every phase exchanges data through   */
+/* ONE 5 KB per-wave LDS buffer; a wave keeps only the per-stream state     */
+/* (IMDCT overlap, synthesis history) in VGPRs.                             */
+/*  Q  lane = line pair: requantise both channels (ISO 2.4.3.4, per-band   */
+/*     2^(q/4) precomputed by lane = band), joint stereo paired by          */
 /*     bitstream line, scatter into LDS in short-block reordered position.  */
 /*  I  lane = (ch, sb): alias reduction (neighbours read from LDS), IMDCT   */
 /*     36 / 3x12 + window + overlap + frequency inversion -> S[ch,t][sb].   */
 /*  M  32-point matrixing X = C.S on the matrix cores (v_mfma_f32_16x16x4): */
 /*     rows m, cols (ch, t), K = sb; A = C fragments, B = S rows (LDS).     */
 /*  W  lane = (ch, j): 512-tap window over 16 slots; the 29 X values of the */
-/*     previous granule this lane needs live in registers -> int16 PCM.     */
+/*     previous granule this lane needs live in registers -> int16 PCM,     */
+/*     L/R pairs joined across the half-waves (v_permlane32_swap) into one  */
+/*     4-B store per lane and slot pair.                                    */
 /* Template SRC_XR: config-2 entry (spectra given as f32 xr, after stereo). */
 /* ------------------------------------------------------------------------ */
+#define SYN_WAVES 4
 #define SROW 36      /* LDS row stride of S (floats): 16-B rows, few conflicts */
 #define SYN_BUF 1296 /* floats: max(xr 2x576, S 36x36, X 36x36)              */
 #define XROW 36      /* LDS row stride of X: 16-B rows, conflict-free b128 writes */
@@ -803,30 +812,55 @@ __device__ __forceinline__ float pow2_quarter(int q) { /* 2^(q/4), exact table *
     return ldexpf(f, q >> 2);
 }
 
+struct SynShared {                   /* read-only, one copy per workgroup          */
+    uint32_t lvar[3][3][288];        /* tab->lvar (u16 pairs) [rate][variant]      */
+    float ce[16][16], co[16][16];    /* matrixing A: C[2m][i], C[2m+1][i], i < 16  */
+    float dw[32][16];                /* window taps per output j                   */
+    float p43[256];                  /* |is|^(4/3) for |is| < 256                  */
+    float w36[4][36];                /* long-block windows (x IMDCT output scale)  */
+    float isr[7][2];                 /* MPEG-1 intensity ratios                    */
+};
+struct SynWave {                     /* one per wave (stream)                      */
+    float buf[SYN_BUF];              /* xr -> S -> X hand-offs                     */
+    float scale[2][64];              /* 2^(q/4) per (ch, band idx): long b | 22 + 3 b + w */
+    UnitMeta m[2];
+    uint8_t is[64];                  /* intensity position per right band idx, 0xFF none */
+};
+
+#define WAIT_VMCNT0() __builtin_amdgcn_s_waitcnt(0x0F70) /* vmcnt(0), other counters free */
 
 template <bool SRC_XR>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
+__global__ void __launch_bounds__(64 * SYN_WAVES) __attribute__((amdgpu_waves_per_eu(3, 8)))
 k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, const UnitMeta *__restrict__ meta,
         const float *__restrict__ xr_in, const uint8_t *__restrict__ xr_bt, const uint8_t *__restrict__ xr_mixed,
-        const DevTables *__restrict__ tab, StreamState *__restrict__ st, int16_t *__restrict__ pcm, int F, int xr_nch,
-        int xr_sr) {
-    __shared__ __attribute__((aligned(16))) float sBuf[SYN_BUF];
-    __shared__ uint32_t sLvar[3][288]; /* tab->lvar[sr] (u16 pairs): per block variant    */
-    __shared__ float sScale[2][64];  /* 2^(q/4) per (ch, band idx): long b | 22 + 3 b + w */
-    __shared__ uint8_t sIS[64];      /* intensity position per right-channel band idx, 0xFF none */
-    __shared__ float sP43[256];      /* |is|^(4/3) for |is| < 256                      */
-    __shared__ float sW[4][36];      /* long-block windows                             */
-    __shared__ float sISR[7][2];     /* MPEG-1 intensity ratios                        */
-    __shared__ UnitMeta sM[2];
-    const int s = blockIdx.x;
-    const int lane = threadIdx.x;
+        const DevTables *__restrict__ tab, StreamState *__restrict__ st, int16_t *__restrict__ pcm, int n_streams,
+        int F, int xr_nch, int xr_sr) {
+    __shared__ __attribute__((aligned(16))) SynShared T;
+    __shared__ __attribute__((aligned(16))) SynWave Wv[SYN_WAVES];
+    {
+        const int tid = threadIdx.x;
+        for (int i = tid; i < 3 * 3 * 288; i += 64 * SYN_WAVES)
+            (&T.lvar[0][0][0])[i] = ((const uint32_t *)&tab->lvar[0][0][0])[i];
+        for (int i = tid; i < 256; i += 64 * SYN_WAVES) {
+            const int r = i >> 4, c = i & 15;
+            T.ce[r][c] = tab->dct_c[2 * r][c];
+            T.co[r][c] = tab->dct_c[2 * r + 1][c];
+            T.p43[i] = tab->pow43[i];
+        }
+        for (int i = tid; i < 32 * 16; i += 64 * SYN_WAVES) (&T.dw[0][0])[i] = (&tab->dwin[0][0])[i];
+        for (int i = tid; i < 4 * 36; i += 64 * SYN_WAVES) (&T.w36[0][0])[i] = (&c_win36[0][0])[i];
+        if (tid < 14) (&T.isr[0][0])[tid] = (&c_is_ratio[0][0])[tid];
+        __syncthreads();
+    }
+    const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); /* wave-uniform (SGPR) */
+    const int s = blockIdx.x * SYN_WAVES + wid;
+    if (s >= n_streams) return; /* after the only workgroup barrier */
+    SynWave &Wd = Wv[wid];
+    float *const sBuf = Wd.buf;
+    const int lane = threadIdx.x & 63;
     const int ch = lane >> 5;
     const int sb = lane & 31; /* phase I: subband; phase W: output j */
     constexpr int MW = (int)(sizeof(UnitMeta) / 4); /* 14 words per unit */
-
-    for (int i = lane; i < 256; i += 64) sP43[i] = tab->pow43[i];
-    if (lane < 14) (&sISR[0][0])[lane] = (&c_is_ratio[0][0])[lane];
-    for (int i = lane; i < 4 * 36; i += 64) (&sW[0][0])[i] = (&c_win36[0][0])[i];
 
     StreamState &S = st[s];
     const int wa = tab->win_a[sb], wb = tab->win_b[sb];
@@ -840,23 +874,47 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
     for (int k = 0; k < 14; k++) ha[k] = S.fifo[ch][k + 1][wa];
 #pragma unroll
     for (int k = 0; k < 15; k++) hb[k] = S.fifo[ch][k][wb];
-    int cur_sr = -1;
 
-    /* next granule's is[] words (lane owns lines 2 lane + 128 i, +1) and
-     * UnitMeta words, loaded one granule ahead of use (register prefetch) */
+    /* Per-stream buffer resources: every granule access below is a buffer
+     * instruction with a uniform byte offset in an SGPR and the lane offset
+     * in one VGPR, instead of a 64-bit address pair per lane and load. */
+    const int gb = 2 * 576 * 2;                   /* is[] bytes per granule (2 ch) */
+    const __amdgpu_buffer_rsrc_t r_is = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(is_buf + (size_t)s * F * 4 * 576), 0, F * 2 * gb, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r_meta = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(meta + (size_t)s * F * 4), 0, F * 4 * (int)sizeof(UnitMeta), 0x00020000);
+    const __amdgpu_buffer_rsrc_t r_rec = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(rec + (size_t)s * F), 0, F * (int)sizeof(FrameRec), 0x00020000);
+    const __amdgpu_buffer_rsrc_t r_pcm = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(pcm + (size_t)s * F * 2304), 0, F * 4608, 0x00020000);
+
+    /* granule prefetch, one granule ahead of use: is[] words (lane owns
+     * lines 2 lane + 128 i, +1), UnitMeta words of both channels (lanes
+     * 0 .. 27) and the granule's FrameRec words (lanes 32 .. 39) */
     uint32_t nis[2][5], nmeta = 0;
-    size_t pre_up = ~(size_t)0;
-    auto prefetch = [&](size_t up) {
-        if (SRC_XR) return;
-        const uint32_t *row = (const uint32_t *)(is_buf + up * 2 * 576);
+    auto prefetch = [&](int g) { /* g = granule index inside the stream */
+        const int lo = opaque(lane * 4);
 #pragma unroll
         for (int c = 0; c < 2; c++)
 #pragma unroll
-            for (int i = 0; i < 5; i++) nis[c][i] = (i < 4 || lane < 32) ? row[c * 288 + lane + 64 * i] : 0u;
-        nmeta = lane < 2 * MW ? ((const uint32_t *)&meta[up * 2])[lane] : 0u;
-        pre_up = up;
+            for (int i = 0; i < 4; i++)
+                nis[c][i] = __builtin_amdgcn_raw_buffer_load_b32(r_is, lo + c * 1152 + 256 * i, g * gb, 0);
+        nis[0][4] = nis[1][4] = 0u;
+        if (lane < 32) {
+            nis[0][4] = __builtin_amdgcn_raw_buffer_load_b32(r_is, lo + 1024, g * gb, 0);
+            nis[1][4] = __builtin_amdgcn_raw_buffer_load_b32(r_is, lo + 1152 + 1024, g * gb, 0);
+        }
+        nmeta = 0u;
+        if (lane < 2 * MW) nmeta = __builtin_amdgcn_raw_buffer_load_b32(r_meta, lo, g * 2 * (int)sizeof(UnitMeta), 0);
+        else if (lane >= 32 && lane < 40)
+            nmeta = __builtin_amdgcn_raw_buffer_load_b32(r_rec, lo - 128, (g >> 1) * (int)sizeof(FrameRec), 0);
     };
-    prefetch((size_t)s * F * 2);
+    if (!SRC_XR) {
+        prefetch(0);
+        /* explicit drain on the entry path, so the compiler's wait before
+         * each prefetch use is set by the loop path (stores after it) */
+        WAIT_VMCNT0();
+    }
 
     for (int f = 0; f < F; f++) {
         int nch, sr, mode = 0, mext = 0;
@@ -865,25 +923,29 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
             nch = xr_nch;
             sr = xr_sr;
         } else {
-            const FrameRec r = rec[fr];
-            if (!r.frame_bytes || (r.first_gr & (REC_TAG | REC_DROP))) continue;
-            nch = r.nch;
-            sr = r.sr_idx;
-            mode = r.hdr3 >> 6;
-            mext = (r.hdr3 >> 4) & 3;
-        }
-        if (sr != cur_sr) { /* line tables of this sample rate into LDS */
-            wave_sync();
-            for (int i = lane; i < 3 * 288; i += 64) (&sLvar[0][0])[i] = ((const uint32_t *)tab->lvar[sr])[i];
-            cur_sr = sr;
-            wave_sync();
+            /* FrameRec words 4 .. 6 from the prefetch (lanes 36 .. 38) */
+            const uint32_t r4 = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, 36);
+            const uint32_t r5 = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, 37);
+            const uint32_t r6 = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, 38);
+            const uint32_t first_gr = (r6 >> 8) & 0xFFu;
+            if (!(r4 & 0xFFFFu) || (first_gr & (REC_TAG | REC_DROP))) {
+                /* no audio in this frame: fetch the next frame's granule 0
+                 * now and wait for it here, off the common path */
+                if (f + 1 < F) prefetch(2 * (f + 1));
+                WAIT_VMCNT0();
+                continue;
+            }
+            nch = (int)(r5 >> 24);
+            sr = (int)((r6 >> 16) & 3u);
+            mode = (int)(r5 >> 22) & 3;
+            mext = (int)(r5 >> 20) & 3;
         }
         const bool active = ch < nch;
-        int16_t *out = pcm + fr * 2304;
+        const uint32_t(*lvar)[288] = T.lvar[sr];
         for (int gr = 0; gr < 2; gr++) {
             /* lane-derived indices are re-derived from an opaque copy each
              * granule so they are not hoisted and held live across the loop */
-            const int lane = opaque((int)threadIdx.x);
+            const int lane = opaque((int)(threadIdx.x & 63));
             const int ch = lane >> 5, sb = lane & 31;
             /* block structure of both channels (uniform) */
             int bt0, mx0, bt1 = 0, mx1 = 0;
@@ -896,8 +958,8 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                     bt1 = xr_bt[ux + 1];
                     mx1 = bt1 == 2 ? xr_mixed[ux + 1] : 0;
                 }
-                const uint16_t *lv0 = (const uint16_t *)sLvar[bt0 == 2 ? (mx0 ? 2 : 1) : 0];
-                const uint16_t *lv1 = (const uint16_t *)sLvar[bt1 == 2 ? (mx1 ? 2 : 1) : 0];
+                const uint16_t *lv0 = (const uint16_t *)lvar[bt0 == 2 ? (mx0 ? 2 : 1) : 0];
+                const uint16_t *lv1 = (const uint16_t *)lvar[bt1 == 2 ? (mx1 ? 2 : 1) : 0];
 #pragma unroll
                 for (int i = 0; i < 9; i++) {
                     const int l = lane + 64 * i;
@@ -906,19 +968,18 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                 }
             } else {
                 const size_t up = fr * 2 + gr;
-                if (pre_up != up) prefetch(up); /* a skipped frame broke the chain */
                 uint32_t cis[2][5];
 #pragma unroll
                 for (int c = 0; c < 2; c++)
 #pragma unroll
                     for (int i = 0; i < 5; i++) cis[c][i] = nis[c][i];
-                if (lane < 2 * MW && lane / MW < nch) ((uint32_t *)&sM[0])[lane] = nmeta;
+                if (lane < 2 * MW && lane / MW < nch) ((uint32_t *)&Wd.m[0])[lane] = nmeta;
                 wave_sync();
-                bt0 = sM[0].block_type;
-                mx0 = sM[0].mixed;
+                bt0 = Wd.m[0].block_type;
+                mx0 = Wd.m[0].mixed;
                 if (nch == 2) {
-                    bt1 = sM[1].block_type;
-                    mx1 = sM[1].mixed;
+                    bt1 = Wd.m[1].block_type;
+                    mx1 = Wd.m[1].mixed;
                 }
                 const int var[2] = {bt0 == 2 ? (mx0 ? 2 : 1) : 0, bt1 == 2 ? (mx1 ? 2 : 1) : 0};
                 const bool is_on = mode == 1 && nch == 2 && (mext & 1);
@@ -926,44 +987,74 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                 const float isq = 0.70710678118654752f;
                 /* per-band scale 2^(q/4), lane = band idx (long b | 22 + 3 b + w) */
                 for (int c = 0; c < nch; c++) {
-                    const UnitMeta &M = sM[c];
+                    const UnitMeta &M = Wd.m[c];
                     const int gain = (int)M.global_gain - 210, shift = M.scalefac_scale + 1;
                     int q;
                     if (lane < 22) {
-                        q = gain - ((M.sf[lane] + (M.preflag ? (int)MP3D_PRETAB[lane] : 0)) << shift);
+                        const int pre = M.preflag ? (int)(MP3D_PRETAB_BITS >> (2 * lane)) & 3 : 0;
+                        q = gain - ((M.sf[lane] + pre) << shift);
                     } else {
                         const int b = (lane - 22) / 3, w = lane - 22 - 3 * b;
                         int k = M.mixed ? 8 + 3 * (b - 3) + w : 3 * b + w;
                         k = k < 0 ? 0 : (k > 39 ? 39 : k);
                         q = gain - 8 * M.sbg[w < 3 ? w : 0] - (M.sf[k] << shift);
                     }
-                    sScale[c][lane] = ms_fold ? pow2_quarter(q) * isq : pow2_quarter(q);
+                    Wd.scale[c][lane] = ms_fold ? pow2_quarter(q) * isq : pow2_quarter(q);
                 }
                 wave_sync();
                 /* lane owns lines 2 lane + 128 i + e (e = 0, 1), i < 4, or i = 4
                  * for lanes < 32; xv[c][2 i + e].  Per line: one u16 table entry
                  * (scale idx | reordered position), |is|^(4/3) from LDS. */
-                const int nz[2] = {sM[0].nz_end, nch == 2 ? sM[1].nz_end : 0};
+                const int nz[2] = {Wd.m[0].nz_end, nch == 2 ? Wd.m[1].nz_end : 0};
                 float xv[2][10];
+                bool big = false; /* some |is| >= 256 (escape): global table */
 #pragma unroll
                 for (int i = 0; i < 5; i++) {
                     const int l0 = 2 * lane + 128 * i;
                     const bool ok = i < 4 || lane < 32;
 #pragma unroll
                     for (int c = 0; c < 2; c++) {
-                        const uint32_t tv2 = ok ? sLvar[var[c]][l0 >> 1] : 0u;
+                        const uint32_t tv2 = ok ? lvar[var[c]][l0 >> 1] : 0u;
 #pragma unroll
                         for (int e = 0; e < 2; e++) {
                             const int l = l0 + e;
                             int v = (int)(int16_t)(e ? (cis[c][i] >> 16) : (cis[c][i] & 0xFFFFu));
                             v = l < nz[c] ? v : 0; /* rzero lines are not stored by k_huffman */
                             const int a = v < 0 ? -v : v;
-                            float p = sP43[a < 256 ? a : 0];
-                            if (a >= 256) p = tab->pow43[a];
-                            const float mag = p * sScale[c][(e ? tv2 >> 16 : tv2) & 63u];
+                            big |= a >= 256;
+                            const float mag = T.p43[a & 255] * Wd.scale[c][(e ? tv2 >> 16 : tv2) & 63u];
                             xv[c][2 * i + e] = v < 0 ? -mag : mag;
                         }
                     }
+                }
+                if (__ballot(big)) {
+                    /* rare path: redo the escaped lines from the global table
+                     * (is[] words re-read, so cis dies in the loop above) and
+                     * wait for those loads here: the common path holds no
+                     * vector-memory wait besides the prefetch's */
+                    const uint32_t *row = (const uint32_t *)(is_buf + up * 2 * 576);
+#pragma unroll
+                    for (int i = 0; i < 5; i++) {
+                        const int l0 = 2 * lane + 128 * i;
+                        const bool ok = i < 4 || lane < 32;
+#pragma unroll
+                        for (int c = 0; c < 2; c++) {
+                            const uint32_t tv2 = ok ? lvar[var[c]][l0 >> 1] : 0u;
+                            const uint32_t wv = ok ? row[c * 288 + lane + 64 * i] : 0u;
+#pragma unroll
+                            for (int e = 0; e < 2; e++) {
+                                const int l = l0 + e;
+                                int v = (int)(int16_t)(e ? (wv >> 16) : (wv & 0xFFFFu));
+                                v = l < nz[c] ? v : 0;
+                                const int a = v < 0 ? -v : v;
+                                if (a >= 256) {
+                                    const float mag = tab->pow43[a] * Wd.scale[c][(e ? tv2 >> 16 : tv2) & 63u];
+                                    xv[c][2 * i + e] = v < 0 ? -mag : mag;
+                                }
+                            }
+                        }
+                    }
+                    WAIT_VMCNT0();
                 }
                 if (is_on) {
                     /* joint stereo with MPEG-1 intensity (ISO 2.4.3.4), paired by
@@ -975,13 +1066,13 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
 #pragma unroll
                     for (int i = 0; i < 5; i++) {
                         const int l0 = 2 * lane + 128 * i;
-                        const uint32_t tv2 = (i < 4 || lane < 32) ? sLvar[var[1]][l0 >> 1] : 0u;
+                        const uint32_t tv2 = (i < 4 || lane < 32) ? lvar[var[1]][l0 >> 1] : 0u;
                         if (xv[1][2 * i] != 0.f) nzR |= 1ull << (tv2 & 63u);
                         if (xv[1][2 * i + 1] != 0.f) nzR |= 1ull << ((tv2 >> 16) & 63u);
                     }
 #pragma unroll
                     for (int o = 1; o < 64; o <<= 1) nzR |= __shfl_xor(nzR, o);
-                    const UnitMeta &R = sM[1];
+                    const UnitMeta &R = Wd.m[1];
                     int ip = 0xFF;
                     if (lane < 22) {
                         if (bt1 != 2 || (mx1 && lane < 8)) {
@@ -1000,20 +1091,20 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                             if ((nzR & above) == 0ull && p < 7) ip = p;
                         }
                     }
-                    sIS[lane] = (uint8_t)ip;
+                    Wd.is[lane] = (uint8_t)ip;
                     wave_sync();
 #pragma unroll
                     for (int i = 0; i < 5; i++) {
                         const int l0 = 2 * lane + 128 * i;
-                        const uint32_t tv2 = (i < 4 || lane < 32) ? sLvar[var[1]][l0 >> 1] : 0u;
+                        const uint32_t tv2 = (i < 4 || lane < 32) ? lvar[var[1]][l0 >> 1] : 0u;
 #pragma unroll
                         for (int e = 0; e < 2; e++) {
                             const int k = 2 * i + e;
                             const float lv = xv[0][k], rv = xv[1][k];
-                            const int ipl = sIS[(e ? tv2 >> 16 : tv2) & 63u];
+                            const int ipl = Wd.is[(e ? tv2 >> 16 : tv2) & 63u];
                             if (ipl != 0xFF) {
-                                xv[0][k] = lv * sISR[ipl][0];
-                                xv[1][k] = lv * sISR[ipl][1];
+                                xv[0][k] = lv * T.isr[ipl][0];
+                                xv[1][k] = lv * T.isr[ipl][1];
                             } else if (mext & 2) {
                                 xv[0][k] = (lv + rv) * isq;
                                 xv[1][k] = (lv - rv) * isq;
@@ -1030,8 +1121,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                 }
                 /* the next granule's loads fly during phases I, M, W (issued
                  * after cis is consumed: fewer live registers in phase Q) */
-                if (gr == 0) prefetch(up + 1);
-                else if (f + 1 < F) prefetch(up + 1);
+                if (gr == 0 || f + 1 < F) prefetch(2 * f + gr + 1);
                 /* scatter in (short-block reordered) position */
 #pragma unroll
                 for (int i = 0; i < 5; i++) {
@@ -1043,7 +1133,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                                 if (var[c] == 0) { /* long block: in place, one 8-B store */
                                     *(float2 *)&sBuf[576 * c + l0] = make_float2(xv[c][2 * i], xv[c][2 * i + 1]);
                                 } else {
-                                    const uint32_t tv2 = sLvar[var[c]][l0 >> 1];
+                                    const uint32_t tv2 = lvar[var[c]][l0 >> 1];
                                     sBuf[576 * c + (tv2 >> 6 & 1023u)] = xv[c][2 * i];
                                     sBuf[576 * c + (tv2 >> 22)] = xv[c][2 * i + 1];
                                 }
@@ -1087,7 +1177,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                 }
                 const bool long_imdct = bt != 2 || (mixed && sb < 2);
                 if (long_imdct) {
-                    const float *wv = sW[bt == 2 ? 0 : bt];
+                    const float *wv = T.w36[bt == 2 ? 0 : bt];
                     float w[18];
                     imdct36_w(x, w);
 #pragma unroll
@@ -1148,8 +1238,8 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
              * mirrors are two 16-B runs of an S row. */
             {
                 const int q = lane >> 4, r16 = lane & 15;
-                const float4 ae = *(const float4 *)&tab->dct_c[2 * r16][4 * q];
-                const float4 ao = *(const float4 *)&tab->dct_c[2 * r16 + 1][4 * q];
+                const float4 ae = *(const float4 *)&T.ce[r16][4 * q];
+                const float4 ao = *(const float4 *)&T.co[r16][4 * q];
                 const float Ae[4] = {ae.x, ae.y, ae.z, ae.w}, Ao[4] = {ao.x, ao.y, ao.z, ao.w};
                 float Be[3][4], Bo[3][4];
 #pragma unroll
@@ -1192,7 +1282,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                 float Dw[16];
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-                    const float4 d = ((const float4 *)tab->dwin[sb])[i];
+                    const float4 d = *(const float4 *)&T.dw[sb][4 * i];
                     Dw[4 * i] = d.x; Dw[4 * i + 1] = d.y; Dw[4 * i + 2] = d.z; Dw[4 * i + 3] = d.w;
                 }
                 float xa[18], xb[18];
@@ -1202,8 +1292,10 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                     xa[t] = sBuf[pa + t * XROW];
                     xb[t] = sBuf[pb + t * XROW];
                 }
-#pragma unroll
-                for (int t = 0; t < 18; t++) {
+                /* output slots in pairs (t0, t1): lanes 0-31 hold L, lanes
+                 * 32-63 R; one half-wave swap leaves lane j with (L, R) of
+                 * slot t0 and lane 32 + j with (L, R) of slot t1 */
+                auto pcm_at = [&](int t) {
                     float o = 0.f;
 #pragma unroll
                     for (int i = 0; i < 8; i++) {
@@ -1213,9 +1305,25 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                         o = fmaf(Dw[2 * i], va, o);
                         o = fmaf(Dw[2 * i + 1], vb, o);
                     }
-                    float pv = rintf(o * 32768.f);
-                    pv = fminf(fmaxf(pv, -32768.f), 32767.f);
-                    if (active) out[(gr * 576 + t * 32 + sb) * nch + ch] = (int16_t)pv;
+                    const float p = rintf(o * 32768.f);
+                    return (int)fminf(fmaxf(p, -32768.f), 32767.f);
+                };
+                if (nch == 2) {
+                    const int vo = opaque((sb + 32 * ch) * 4), so = f * 4608 + gr * 2304;
+#pragma unroll
+                    for (int tp = 0; tp < 9; tp++) {
+                        const int p0 = pcm_at(2 * tp), p1 = pcm_at(2 * tp + 1);
+                        const auto r = __builtin_amdgcn_permlane32_swap(p0, p1, false, false);
+                        __builtin_amdgcn_raw_buffer_store_b32(((uint32_t)r[0] & 0xFFFFu) | ((uint32_t)r[1] << 16),
+                                                              r_pcm, vo + 256 * tp, so, 0);
+                    }
+                } else {
+                    const int vo = opaque(sb * 2), so = f * 4608 + gr * 1152;
+#pragma unroll
+                    for (int t = 0; t < 18; t++) {
+                        const int p = pcm_at(t);
+                        if (active) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)p, r_pcm, vo + 64 * t, so, 0);
+                    }
                 }
 #pragma unroll
                 for (int k = 0; k < 14; k++) ha[k] = active ? xa[k + 4] : ha[k];
@@ -1233,7 +1341,6 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
 #pragma unroll
     for (int k = 0; k < 15; k++) S.fifo[ch][k][wb] = hb[k];
 }
-
 /* ------------------------------------------------------------------------ */
 /* Host-side launchers                                                       */
 /* ------------------------------------------------------------------------ */
@@ -1272,14 +1379,16 @@ void launch_huffman(const uint8_t *md, const uint64_t *md_off, const FrameRec *r
 
 void launch_synth(const FrameRec *rec, const int16_t *is_buf, const UnitMeta *meta, const DevTables *tab,
                   StreamState *st, int16_t *pcm, int n_streams, int F, hipStream_t strm) {
-    hipLaunchKernelGGL(k_synth<false>, dim3(n_streams), dim3(64), 0, strm, rec, is_buf, meta, (const float *)nullptr,
-                       (const uint8_t *)nullptr, (const uint8_t *)nullptr, tab, st, pcm, F, 2, 0);
+    hipLaunchKernelGGL(k_synth<false>, dim3((n_streams + SYN_WAVES - 1) / SYN_WAVES), dim3(64 * SYN_WAVES), 0, strm, rec,
+                       is_buf, meta, (const float *)nullptr, (const uint8_t *)nullptr, (const uint8_t *)nullptr, tab, st,
+                       pcm, n_streams, F, 2, 0);
 }
 
 void launch_synth_xr(const float *xr, const uint8_t *bt, const uint8_t *mixed, const DevTables *tab, StreamState *st,
                      int16_t *pcm, int n_streams, int F, int nch, int sr, hipStream_t strm) {
-    hipLaunchKernelGGL(k_synth<true>, dim3(n_streams), dim3(64), 0, strm, (const FrameRec *)nullptr,
-                       (const int16_t *)nullptr, (const UnitMeta *)nullptr, xr, bt, mixed, tab, st, pcm, F, nch, sr);
+    hipLaunchKernelGGL(k_synth<true>, dim3((n_streams + SYN_WAVES - 1) / SYN_WAVES), dim3(64 * SYN_WAVES), 0, strm,
+                       (const FrameRec *)nullptr, (const int16_t *)nullptr, (const UnitMeta *)nullptr, xr, bt, mixed, tab,
+                       st, pcm, n_streams, F, nch, sr);
 }
 
 } // namespace mp3d
