@@ -812,6 +812,18 @@ __device__ __forceinline__ float pow2_quarter(int q) { /* 2^(q/4), exact table *
     return ldexpf(f, q >> 2);
 }
 
+/* |is|^(4/3) for 256 <= |is| <= 8206 without the 33 KB table: cube root
+ * from v_log_f32 / v_exp_f32, one Newton step, times |is|; within 2 ulp of
+ * the correctly rounded value for every such |is| (checked exhaustively in
+ * tests/test_tables.py against the same float32 recipe). */
+__device__ __forceinline__ float pow43_big(int a) {
+    const float x = (float)a;
+    float y = __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(x) * (1.0f / 3.0f));
+    const float y2 = y * y;
+    y = y - fmaf(y2, y, -x) * __builtin_amdgcn_rcpf(3.0f * y2);
+    return x * y;
+}
+
 struct SynShared {                   /* read-only, one copy per workgroup          */
     uint32_t lvar[3][3][288];        /* tab->lvar (u16 pairs) [rate][variant]      */
     float ce[16][16], co[16][16];    /* matrixing A: C[2m][i], C[2m+1][i], i < 16  */
@@ -967,47 +979,56 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                     if (nch == 2) sBuf[576 + (lv1[l] >> 6)] = xr_in[(ux + 1) * 576 + l];
                 }
             } else {
-                const size_t up = fr * 2 + gr;
                 uint32_t cis[2][5];
 #pragma unroll
                 for (int c = 0; c < 2; c++)
 #pragma unroll
                     for (int i = 0; i < 5; i++) cis[c][i] = nis[c][i];
+                /* UnitMeta into LDS for the (rare) intensity path; the common
+                 * path reads the prefetched words straight from registers */
                 if (lane < 2 * MW && lane / MW < nch) ((uint32_t *)&Wd.m[0])[lane] = nmeta;
-                wave_sync();
-                bt0 = Wd.m[0].block_type;
-                mx0 = Wd.m[0].mixed;
+                /* words 10..12: gain, block type, mixed, scalefac_scale |
+                 * preflag, sbg[3] | nz_end (UnitMeta layout) */
+                const uint32_t m10a = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, 10);
+                const uint32_t m11a = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, 11);
+                const uint32_t m12a = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, 12);
+                const uint32_t m10b = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, MW + 10);
+                const uint32_t m11b = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, MW + 11);
+                const uint32_t m12b = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, MW + 12);
+                bt0 = (int)(m10a >> 8) & 0xFF;
+                mx0 = (int)(m10a >> 16) & 0xFF;
                 if (nch == 2) {
-                    bt1 = Wd.m[1].block_type;
-                    mx1 = Wd.m[1].mixed;
+                    bt1 = (int)(m10b >> 8) & 0xFF;
+                    mx1 = (int)(m10b >> 16) & 0xFF;
                 }
                 const int var[2] = {bt0 == 2 ? (mx0 ? 2 : 1) : 0, bt1 == 2 ? (mx1 ? 2 : 1) : 0};
                 const bool is_on = mode == 1 && nch == 2 && (mext & 1);
                 const bool ms_fold = mode == 1 && nch == 2 && mext == 2; /* M/S only: 1/sqrt2 in the scale */
                 const float isq = 0.70710678118654752f;
-                /* per-band scale 2^(q/4), lane = band idx (long b | 22 + 3 b + w) */
-                for (int c = 0; c < nch; c++) {
-                    const UnitMeta &M = Wd.m[c];
-                    const int gain = (int)M.global_gain - 210, shift = M.scalefac_scale + 1;
-                    int q;
-                    if (lane < 22) {
-                        const int pre = M.preflag ? (int)(MP3D_PRETAB_BITS >> (2 * lane)) & 3 : 0;
-                        q = gain - ((M.sf[lane] + pre) << shift);
-                    } else {
-                        const int b = (lane - 22) / 3, w = lane - 22 - 3 * b;
-                        int k = M.mixed ? 8 + 3 * (b - 3) + w : 3 * b + w;
-                        k = k < 0 ? 0 : (k > 39 ? 39 : k);
-                        q = gain - 8 * M.sbg[w < 3 ? w : 0] - (M.sf[k] << shift);
-                    }
-                    Wd.scale[c][lane] = ms_fold ? pow2_quarter(q) * isq : pow2_quarter(q);
+                /* per-band scale 2^(q/4), lane = band idx (long b | 22 + 3 b + w);
+                 * the lane's scalefactor byte comes from the prefetched meta
+                 * words by one cross-lane read per channel */
+                {
+                    const bool lng = lane < 22;
+                    const int b = (lane - 22) / 3, w = lane - 22 - 3 * b;
+                    auto band_scale = [&](uint32_t g10, uint32_t g11, int cbase) {
+                        const int gain = (int)(g10 & 0xFFu) - 210, shift = (int)(g10 >> 24) + 1;
+                        const bool mixed = ((g10 >> 16) & 0xFFu) != 0u, preflag = (g11 & 0xFFu) != 0u;
+                        int j = mixed ? 8 + 3 * (b - 3) + w : 3 * b + w;
+                        j = lng ? lane : (j < 0 ? 0 : (j > 39 ? 39 : j));
+                        const uint32_t wd = (uint32_t)__shfl((int)nmeta, cbase + (j >> 2));
+                        const int sf = (int)(wd >> (8 * (j & 3))) & 0xFF;
+                        const int pre = preflag ? (int)(MP3D_PRETAB_BITS >> (2 * (lane & 31))) & 3 : 0;
+                        const int sbg = (int)(g11 >> (8 * (1 + (w < 3 ? w : 0)))) & 0xFF;
+                        const int q = lng ? gain - ((sf + pre) << shift) : gain - 8 * sbg - (sf << shift);
+                        return ms_fold ? pow2_quarter(q) * isq : pow2_quarter(q);
+                    };
+                    Wd.scale[0][lane] = band_scale(m10a, m11a, 0);
+                    if (nch == 2) Wd.scale[1][lane] = band_scale(m10b, m11b, MW);
                 }
                 wave_sync();
-                /* lane owns lines 2 lane + 128 i + e (e = 0, 1), i < 4, or i = 4
-                 * for lanes < 32; xv[c][2 i + e].  Per line: one u16 table entry
-                 * (scale idx | reordered position), |is|^(4/3) from LDS. */
-                const int nz[2] = {Wd.m[0].nz_end, nch == 2 ? Wd.m[1].nz_end : 0};
+                const int nz[2] = {(int)(m12a & 0xFFFFu), nch == 2 ? (int)(m12b & 0xFFFFu) : 0};
                 float xv[2][10];
-                bool big = false; /* some |is| >= 256 (escape): global table */
 #pragma unroll
                 for (int i = 0; i < 5; i++) {
                     const int l0 = 2 * lane + 128 * i;
@@ -1021,40 +1042,12 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                             int v = (int)(int16_t)(e ? (cis[c][i] >> 16) : (cis[c][i] & 0xFFFFu));
                             v = l < nz[c] ? v : 0; /* rzero lines are not stored by k_huffman */
                             const int a = v < 0 ? -v : v;
-                            big |= a >= 256;
-                            const float mag = T.p43[a & 255] * Wd.scale[c][(e ? tv2 >> 16 : tv2) & 63u];
+                            float p = T.p43[a & 255];
+                            if (a >= 256) p = pow43_big(a); /* escapes: no table load */
+                            const float mag = p * Wd.scale[c][(e ? tv2 >> 16 : tv2) & 63u];
                             xv[c][2 * i + e] = v < 0 ? -mag : mag;
                         }
                     }
-                }
-                if (__ballot(big)) {
-                    /* rare path: redo the escaped lines from the global table
-                     * (is[] words re-read, so cis dies in the loop above) and
-                     * wait for those loads here: the common path holds no
-                     * vector-memory wait besides the prefetch's */
-                    const uint32_t *row = (const uint32_t *)(is_buf + up * 2 * 576);
-#pragma unroll
-                    for (int i = 0; i < 5; i++) {
-                        const int l0 = 2 * lane + 128 * i;
-                        const bool ok = i < 4 || lane < 32;
-#pragma unroll
-                        for (int c = 0; c < 2; c++) {
-                            const uint32_t tv2 = ok ? lvar[var[c]][l0 >> 1] : 0u;
-                            const uint32_t wv = ok ? row[c * 288 + lane + 64 * i] : 0u;
-#pragma unroll
-                            for (int e = 0; e < 2; e++) {
-                                const int l = l0 + e;
-                                int v = (int)(int16_t)(e ? (wv >> 16) : (wv & 0xFFFFu));
-                                v = l < nz[c] ? v : 0;
-                                const int a = v < 0 ? -v : v;
-                                if (a >= 256) {
-                                    const float mag = tab->pow43[a] * Wd.scale[c][(e ? tv2 >> 16 : tv2) & 63u];
-                                    xv[c][2 * i + e] = v < 0 ? -mag : mag;
-                                }
-                            }
-                        }
-                    }
-                    WAIT_VMCNT0();
                 }
                 if (is_on) {
                     /* joint stereo with MPEG-1 intensity (ISO 2.4.3.4), paired by

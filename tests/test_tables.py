@@ -81,3 +81,25 @@ def test_tables_present_in_ffmpeg_copy():
     assert in_region(t["MP3D_BITRATE_L3"].astype("<u2").tobytes())
     assert kb.find(t["MP3D_SLEN"].tobytes()) >= 0
     assert kb.find(t["MP3D_ALIAS_C"].astype("<f4").tobytes()) >= 0
+
+
+def test_pow43_escape_recipe():
+    """k_synth computes |is|^(4/3) for 256 <= |is| <= 8206 (escape values) without
+    a table: y = exp2(log2(x) / 3), one Newton step on y^3 = x, times x
+    (pow43_big in mp3d_kernels.hip).  Emulated in float32 with the log/exp
+    results perturbed by up to 3 ulp (the hardware v_log_f32 / v_exp_f32 are
+    approximate), it stays within 2 ulp of the correctly rounded value."""
+    a = np.arange(256, 8207)
+    ref = (a.astype(np.float64) ** (4.0 / 3.0)).astype(np.float32)
+    x = a.astype(np.float32)
+    for pert in (-3, -1, 0, 1, 3):
+        lg = (np.log2(x).astype(np.float32).view(np.int32) + pert).view(np.float32)
+        y = np.exp2((lg * np.float32(1.0 / 3.0)).astype(np.float32)).astype(np.float32)
+        y = (y.view(np.int32) - pert).view(np.float32)
+        y2 = (y * y).astype(np.float32)
+        r = (y2.astype(np.float64) * y - x).astype(np.float32)  # fmaf
+        rc = (np.float32(1.0) / (np.float32(3.0) * y2)).astype(np.float32)
+        y = (y - (r * rc).astype(np.float32)).astype(np.float32)
+        p = (x * y).astype(np.float32)
+        ulp = np.abs(p.view(np.int32).astype(np.int64) - ref.view(np.int32))
+        assert ulp.max() <= 2, (pert, int(ulp.max()))
