@@ -1029,6 +1029,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                 wave_sync();
                 const int nz[2] = {(int)(m12a & 0xFFFFu), nch == 2 ? (int)(m12b & 0xFFFFu) : 0};
                 float xv[2][10];
+                bool big = false; /* some |is| >= 256 (escape) in this lane */
 #pragma unroll
                 for (int i = 0; i < 5; i++) {
                     const int l0 = 2 * lane + 128 * i;
@@ -1042,10 +1043,32 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                             int v = (int)(int16_t)(e ? (cis[c][i] >> 16) : (cis[c][i] & 0xFFFFu));
                             v = l < nz[c] ? v : 0; /* rzero lines are not stored by k_huffman */
                             const int a = v < 0 ? -v : v;
-                            float p = T.p43[a & 255];
-                            if (a >= 256) p = pow43_big(a); /* escapes: no table load */
-                            const float mag = p * Wd.scale[c][(e ? tv2 >> 16 : tv2) & 63u];
+                            big |= a >= 256;
+                            const float mag = T.p43[a & 255] * Wd.scale[c][(e ? tv2 >> 16 : tv2) & 63u];
                             xv[c][2 * i + e] = v < 0 ? -mag : mag;
+                        }
+                    }
+                }
+                if (__ballot(big)) {
+                    /* rare path (escapes |is| >= 256): patch those lines with
+                     * the in-register |is|^(4/3); one block, so the loop above
+                     * stays branch-free and its LDS reads batch */
+#pragma unroll
+                    for (int i = 0; i < 5; i++) {
+                        const int l0 = 2 * lane + 128 * i;
+#pragma unroll
+                        for (int c = 0; c < 2; c++) {
+#pragma unroll
+                            for (int e = 0; e < 2; e++) {
+                                int v = (int)(int16_t)(e ? (cis[c][i] >> 16) : (cis[c][i] & 0xFFFFu));
+                                v = l0 + e < nz[c] ? v : 0;
+                                const int a = v < 0 ? -v : v;
+                                if (a >= 256) {
+                                    const uint32_t tv2 = lvar[var[c]][l0 >> 1];
+                                    const float mag = pow43_big(a) * Wd.scale[c][(e ? tv2 >> 16 : tv2) & 63u];
+                                    xv[c][2 * i + e] = v < 0 ? -mag : mag;
+                                }
+                            }
                         }
                     }
                 }
