@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MP3D_ABI_VERSION 1
+#define MP3D_ABI_VERSION 2
 
 #if defined(__GNUC__) || defined(__clang__)
 #define MP3D_API __attribute__((visibility("default")))
@@ -113,6 +113,29 @@ MP3D_API int mp3d_batch_huffman_only(mp3d_batch *b, const uint8_t *frames, const
 MP3D_API int mp3d_batch_synth_only(mp3d_batch *b, const float *xr, const uint8_t *block_type, const uint8_t *mixed,
                           int n_streams, int frames_per_stream, int nch, int sample_rate_hz, int16_t *pcm,
                           void *hip_stream);
+
+/* ---- stream-level info: Xing/Info tag and gapless playback ------------- *
+ * Filled from the stream's leading Xing/Info frame (read by the demux kernel
+ * on the stream's first call).  Gapless trim follows FFmpeg's demuxer
+ * (libavformat/mp3dec.c): with a LAME / Lavf / Lavc encoder extension the
+ * first enc_delay + 529 decoded samples per channel are encoder/decoder
+ * delay, and when the tag also carries a frame count, samples from
+ * total_frames * 1152 + 529 - enc_padding on are padding.  The decoder
+ * always emits every decoded frame; apply the trim when concatenating.      */
+typedef struct mp3d_stream_info {
+    int has_tag;          /* a Xing/Info frame opened the stream               */
+    int has_lame;         /* ... with a LAME / Lavf / Lavc encoder extension   */
+    int enc_delay;        /* encoder delay, samples per channel (0 if none)    */
+    int enc_padding;      /* encoder padding, samples per channel (0 if none)  */
+    int total_frames;     /* Xing frame count (-1 if absent)                   */
+    int skip_samples;     /* gapless: leading samples to drop (0 if none)      */
+    long long end_sample; /* gapless: index of the first padding sample, -1    */
+} mp3d_stream_info;
+
+/* out[n_streams]; valid once the call that decoded a stream's first frame
+ * has completed (synchronises the handle's stream).                       */
+MP3D_API int mp3d_batch_stream_info(mp3d_batch *b, int n_streams, mp3d_stream_info *out);
+MP3D_API int mp3d_dec_stream_info(mp3d_dec *dec, mp3d_stream_info *out);
 
 /* ---- diagnostics -------------------------------------------------------- */
 MP3D_API const char *mp3d_strerror(int err);

@@ -28,13 +28,24 @@ class FrameInfo(ctypes.Structure):
                 ("layer", ctypes.c_int), ("bitrate_kbps", ctypes.c_int), ("samples", ctypes.c_int)]
 
 
+class StreamInfo(ctypes.Structure):
+    """mp3d_stream_info: leading Xing/Info tag and FFmpeg-style gapless trim."""
+    _fields_ = [("has_tag", ctypes.c_int), ("has_lame", ctypes.c_int), ("enc_delay", ctypes.c_int),
+                ("enc_padding", ctypes.c_int), ("total_frames", ctypes.c_int), ("skip_samples", ctypes.c_int),
+                ("end_sample", ctypes.c_longlong)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 FRAME_INFO_DT = np.dtype([("frame_bytes", np.int32), ("channels", np.int32), ("hz", np.int32),
                           ("layer", np.int32), ("bitrate_kbps", np.int32), ("samples", np.int32)])
 
 EXPORTS = ["mp3d_dec_create", "mp3d_dec_create_on", "mp3d_dec_destroy", "mp3d_dec_reset", "mp3d_decode_frame",
            "mp3d_batch_create", "mp3d_batch_destroy", "mp3d_batch_reset", "mp3d_batch_decode", "mp3d_batch_sync",
            "mp3d_batch_huffman_only", "mp3d_batch_synth_only", "mp3d_strerror", "mp3d_last_hip_error",
-           "mp3d_abi_version", "mp3d_batch_set_timing", "mp3d_batch_kernel_times"]
+           "mp3d_abi_version", "mp3d_batch_set_timing", "mp3d_batch_kernel_times", "mp3d_batch_stream_info",
+           "mp3d_dec_stream_info"]
 
 _lib = None
 
@@ -70,6 +81,8 @@ def lib():
         L.mp3d_strerror.restype = ctypes.c_char_p
         L.mp3d_batch_set_timing.argtypes = [vp, i]
         L.mp3d_batch_kernel_times.argtypes = [vp, vp]
+        L.mp3d_batch_stream_info.argtypes = [vp, i, vp]
+        L.mp3d_dec_stream_info.argtypes = [vp, ctypes.POINTER(StreamInfo)]
         _lib = L
     return _lib
 
@@ -129,8 +142,18 @@ class Decoder:
         n = _check(lib().mp3d_decode_frame(self._h, buf, len(buf), pcm.ctypes.data, ctypes.byref(info)))
         return n, pcm[: n * max(info.channels, 1)], info
 
-    def decode_stream(self, data):
-        """Decode a whole byte stream; returns int16 [channels, samples]."""
+    def stream_info(self):
+        """StreamInfo of the stream decoded so far (Xing/Info tag, gapless)."""
+        info = StreamInfo()
+        _check(lib().mp3d_dec_stream_info(self._h, ctypes.byref(info)))
+        return info
+
+    def decode_stream(self, data, gapless=False):
+        """Decode a whole byte stream; returns int16 [channels, samples].
+        gapless=True drops encoder delay / padding as the stream's LAME tag
+        says (gapless_trim)."""
+        if gapless:
+            return gapless_trim(self.decode_stream(data), self.stream_info())
         data = bytes(data)
         pos, out, nch = 0, [], 0
         while pos < len(data):
@@ -206,6 +229,12 @@ class BatchDecoder:
                                        ctypes.c_void_p(stream) if stream else None))
         return pcm, infos
 
+    def stream_info(self, n_streams):
+        """[StreamInfo] of the first n_streams streams (after a decode call)."""
+        arr = (StreamInfo * int(n_streams))()
+        _check(lib().mp3d_batch_stream_info(self._h, int(n_streams), ctypes.cast(arr, ctypes.c_void_p)))
+        return list(arr)
+
     def huffman_only(self, frames, offsets, sizes, frames_per_stream):
         off, sz = self._geom(offsets, sizes)
         n, F = off.size, int(frames_per_stream)
@@ -241,3 +270,16 @@ def pcm_to_planar(pcm_frames, infos):
     if not rows:
         return np.zeros((0, 0), np.int16)
     return np.concatenate(rows).T.copy()
+
+
+def gapless_trim(planar, info):
+    """Apply a stream's gapless trim (StreamInfo or its dict) to planar PCM
+    [channels, samples] holding every decoded sample from the stream start:
+    FFmpeg semantics (libavformat/mp3dec.c) -- drop the first skip_samples,
+    and everything from end_sample on when the tag gives a frame count."""
+    get = info.get if isinstance(info, dict) else (lambda k: getattr(info, k))
+    if not get("has_lame"):
+        return planar
+    end = get("end_sample")
+    stop = planar.shape[1] if end is None or end < 0 else min(int(end), planar.shape[1])
+    return planar[:, int(get("skip_samples")):stop]

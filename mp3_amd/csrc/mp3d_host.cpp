@@ -549,6 +549,32 @@ extern "C" int mp3d_batch_synth_only(mp3d_batch *b, const float *xr, const uint8
     return MP3D_OK;
 }
 
+static void tag_to_info(uint32_t tag, uint32_t frames, mp3d_stream_info *o) {
+    memset(o, 0, sizeof(*o));
+    o->has_tag = (tag & MP3D_TAG_SEEN) != 0;
+    o->has_lame = (tag & MP3D_TAG_LAME) != 0;
+    o->total_frames = (tag & MP3D_TAG_FRAMES) ? (int)frames : -1;
+    o->end_sample = -1;
+    if (o->has_lame) {
+        o->enc_delay = (int)((tag >> 12) & 0xFFFu);
+        o->enc_padding = (int)(tag & 0xFFFu);
+        o->skip_samples = o->enc_delay + 529; /* FFmpeg: start_pad + 528 + 1 */
+        if (o->total_frames > 0) o->end_sample = (long long)o->total_frames * 1152 + 529 - o->enc_padding;
+    }
+}
+
+extern "C" int mp3d_batch_stream_info(mp3d_batch *b, int n, mp3d_stream_info *out) {
+    if (!b || !out || n <= 0) return MP3D_E_ARG;
+    if (n > b->max_streams) return MP3D_E_CAPACITY;
+    HIPCHK(hipSetDevice(b->device));
+    std::vector<uint32_t> tag((size_t)n * 2);
+    HIPCHK(hipStreamSynchronize(b->own));
+    HIPCHK(hipMemcpy2D(tag.data(), 2 * sizeof(uint32_t), &b->st[0].tag_info, sizeof(StreamState),
+                       2 * sizeof(uint32_t), n, hipMemcpyDeviceToHost));
+    for (int i = 0; i < n; i++) tag_to_info(tag[2 * i], tag[2 * i + 1], &out[i]);
+    return MP3D_OK;
+}
+
 /* ------------------------------------------------------------------------ */
 /* Per-frame decoder                                                         */
 /* ------------------------------------------------------------------------ */
@@ -587,6 +613,11 @@ extern "C" void mp3d_dec_reset(mp3d_dec *d) {
     if (!d) return;
     (void)mp3d_batch_reset(d->b);
     d->frames = 0;
+}
+
+extern "C" int mp3d_dec_stream_info(mp3d_dec *d, mp3d_stream_info *out) {
+    if (!d || !out) return MP3D_E_ARG;
+    return mp3d_batch_stream_info(d->b, 1, out);
 }
 
 static int host_frame_bytes(const uint8_t *p) {

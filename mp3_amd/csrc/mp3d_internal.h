@@ -21,6 +21,9 @@
 #define MP3D_RES_BYTES 512       /* carried main-data history per stream   */
 #define MP3D_FIFO_SLOTS 15       /* synthesis history slots carried        */
 #define MP3D_MAX_FRAME_BYTES 1441
+#define MP3D_TAG_SEEN (1u << 31)
+#define MP3D_TAG_LAME (1u << 30)
+#define MP3D_TAG_FRAMES (1u << 29)
 
 /* MPEG-1 pretab (ISO Table B.6, MP3D_PRETAB in mp3d_tables.h) as 2 bits
  * per long band, for lane-indexed use without a memory load; checked
@@ -64,7 +67,11 @@ struct StreamState {
     uint8_t res[MP3D_RES_BYTES];           /* main-data carry (oldest first) */
     int32_t res_len;                       /* bytes valid in res             */
     int32_t frames;                        /* frames decoded so far          */
-    int32_t pad_[2];
+    /* leading Xing/Info frame (k_demux; 0 = none seen): bit 31 tag, bit 30
+     * LAME/Lavf/Lavc extension, bit 29 frame count present, bits 12..23
+     * encoder delay, bits 0..11 encoder padding; tag_frames = Xing count */
+    uint32_t tag_info;
+    uint32_t tag_frames;
     float overlap[2][32][18];              /* IMDCT overlap                  */
     float fifo[2][MP3D_FIFO_SLOTS][32];    /* last 15 matrixing outputs X    */
 };

@@ -98,6 +98,39 @@ __device__ __forceinline__ uint64_t win_bits64(const HdrWin &w, uint32_t b) {
     return sh ? (hi << sh) | ((uint64_t)x2 >> (32 - sh)) : hi;
 }
 
+/* Xing/Info tag + LAME encoder extension of a stream's first frame, as
+ * FFmpeg's demuxer reads it (libavformat/mp3dec.c mp3_parse_info_tag):
+ * "Xing"/"Info", BE32 flags, optional frame count (1), byte count (2), TOC
+ * (4, 100 B), quality (8); then a 9-byte encoder string and, 21 bytes after
+ * its start, BE24 = encoder delay << 12 | padding, honoured only for
+ * "LAME" / "Lavf" / "Lavc" encoders.  t points at "Xing"/"Info", n bytes of
+ * the frame follow it.  Returns StreamState.tag_info. */
+__device__ uint32_t parse_info_tag(const uint8_t *t, uint32_t n, uint32_t &frames) {
+    auto be32 = [&](uint32_t o) {
+        return (uint32_t)t[o] << 24 | (uint32_t)t[o + 1] << 16 | (uint32_t)t[o + 2] << 8 | t[o + 3];
+    };
+    uint32_t info = MP3D_TAG_SEEN;
+    if (n < 8) return info;
+    const uint32_t flags = be32(4);
+    uint32_t o = 8;
+    if (flags & 1u) {
+        if (o + 4 > n) return info;
+        frames = be32(o);
+        info |= MP3D_TAG_FRAMES;
+        o += 4;
+    }
+    if (flags & 2u) o += 4;
+    if (flags & 4u) o += 100;
+    if (flags & 8u) o += 4;
+    if (o + 24 > n) return info;
+    const uint32_t ver = be32(o);
+    if (ver == 0x4C414D45u /* LAME */ || ver == 0x4C617666u /* Lavf */ || ver == 0x4C617663u /* Lavc */) {
+        const uint32_t v = (uint32_t)t[o + 21] << 16 | (uint32_t)t[o + 22] << 8 | t[o + 23];
+        info |= MP3D_TAG_LAME | (v & 0xFFFFFFu);
+    }
+    return info;
+}
+
 __global__ void __launch_bounds__(64) k_demux(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
                                               const uint32_t *__restrict__ in_len, uint8_t *__restrict__ md,
                                               const uint64_t *__restrict__ md_off, StreamState *__restrict__ st,
@@ -196,6 +229,7 @@ __global__ void __launch_bounds__(64) k_demux(const uint8_t *__restrict__ in, co
                                    win_byte(w, tgo + 3) == 'o'));
                 if (tag) {
                     r.first_gr = REC_TAG;
+                    if (lane == 0) S.tag_info = parse_info_tag(p0 + cur + tgo, (uint32_t)fb - tgo, S.tag_frames);
                 } else if (bad) {
                     /* FFmpeg drops the frame; its reservoir restarts as the frame's
                      * last min(512, bytes - 4) post-header bytes (mp_decode_frame) */

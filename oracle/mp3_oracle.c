@@ -696,6 +696,45 @@ ORC_API int orc_is_info_frame(const uint8_t *buf, long len) {
     return (!memcmp(t, "Xing", 4) || !memcmp(t, "Info", 4));
 }
 
+/* Gapless info of a stream's leading Xing/Info frame, restating FFmpeg's
+ * demuxer (libavformat/mp3dec.c mp3_parse_info_tag, the FFmpeg inside the
+ * golden decoder): "Xing"/"Info" at 4 + side-info bytes,
+ * BE32 flags, [frames] [bytes] [100-B TOC] [quality], 9-byte encoder
+ * string, then 12 bytes on a BE24 delay << 12 | padding, honoured for LAME
+ * / Lavf / Lavc.  out[0..4] = has_lame, enc_delay, enc_padding, frames
+ * (-1 absent), skip_samples (delay + 529).  Returns 1 if a tag was found. */
+ORC_API int orc_parse_info_tag(const uint8_t *buf, long len, int *out) {
+    long pos = orc_skip_id3v2(buf, len);
+    out[0] = out[1] = out[2] = out[4] = 0;
+    out[3] = -1;
+    while (pos + 4 <= len) {
+        orc_hdr h;
+        if (orc_parse_header(buf + pos, &h) > 0) break;
+        pos++;
+    }
+    if (pos + 4 > len || !orc_is_info_frame(buf + pos, len - pos)) return 0;
+    orc_hdr h;
+    const int fb = orc_parse_header(buf + pos, &h);
+    const uint8_t *t = buf + pos + 4 + h.crc_bytes + h.side_bytes;
+    const long n = fb - (4 + h.crc_bytes + h.side_bytes);
+#define BE32(o) ((uint32_t)t[o] << 24 | (uint32_t)t[(o) + 1] << 16 | (uint32_t)t[(o) + 2] << 8 | t[(o) + 3])
+    const uint32_t flags = BE32(4);
+    long o = 8;
+    if (flags & 1) { out[3] = (int)BE32(o); o += 4; }
+    if (flags & 2) o += 4;
+    if (flags & 4) o += 100;
+    if (flags & 8) o += 4;
+    if (o + 24 <= n && (!memcmp(t + o, "LAME", 4) || !memcmp(t + o, "Lavf", 4) || !memcmp(t + o, "Lavc", 4))) {
+        const uint32_t v = (uint32_t)t[o + 21] << 16 | (uint32_t)t[o + 22] << 8 | t[o + 23];
+        out[0] = 1;
+        out[1] = (int)(v >> 12);
+        out[2] = (int)(v & 4095);
+        out[4] = out[1] + 529;
+    }
+#undef BE32
+    return 1;
+}
+
 /* Decode a whole stream into planar float PCM [nch][max_frames*1152].
  * Skips an ID3v2 tag and a leading Xing/Info frame (as FFmpeg's demuxer).
  * Returns number of audio frames decoded. */

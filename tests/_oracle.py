@@ -35,8 +35,19 @@ def lib():
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.orc_skip_id3v2.argtypes = [ctypes.c_char_p, ctypes.c_long]
         L.orc_skip_id3v2.restype = ctypes.c_long
+        L.orc_parse_info_tag.argtypes = [ctypes.c_char_p, ctypes.c_long, ctypes.c_void_p]
         _lib = L
     return _lib
+
+
+def info_tag(data: bytes):
+    """(found, dict) of the stream's leading Xing/Info + LAME tag (gapless)."""
+    out = np.zeros(5, np.int32)
+    found = lib().orc_parse_info_tag(data, len(data), out.ctypes.data)
+    keys = ("has_lame", "enc_delay", "enc_padding", "total_frames", "skip_samples")
+    d = dict(zip(keys, (int(x) for x in out)))
+    d["end_sample"] = d["total_frames"] * 1152 + 529 - d["enc_padding"] if d["has_lame"] and d["total_frames"] > 0 else -1
+    return bool(found), d
 
 
 def decode_stream(data: bytes, max_frames=100000):

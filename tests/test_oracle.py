@@ -62,3 +62,26 @@ def test_integer_stage_roundtrip(cfg, seed):
                 assert np.array_equal(sf[gr, ch], truth[f, gr, ch]["sf"]), (f, gr, ch)
                 assert side[gr, ch, 0] == truth[f, gr, ch]["part2_3_length"]
                 assert side[gr, ch, 16] == side[gr, ch, 0]
+
+
+def test_oracle_gapless_matches_ffmpeg_tagged_output():
+    """The LAME tag of the real file (Lavc56.30: delay 576, padding 0, 21
+    frames) read as FFmpeg's demuxer does: trimming delay + 529 samples from
+    the oracle's full decode reproduces the FFmpeg output of the tagged file
+    (23 087 samples) within 1 LSB."""
+    import mp3_amd
+    data, _ = _golden.case("keypress_128k_js")
+    ref = np.load(_golden.GOLDEN / "keypress_128k_js.tagged.pcm16.npy")
+    found, tag = _oracle.info_tag(data)
+    assert found and tag["has_lame"] and tag["enc_delay"] == 576 and tag["enc_padding"] == 0
+    assert tag["total_frames"] == 21 and tag["skip_samples"] == 1105
+    pcm, _ = _oracle.decode_stream(data)
+    ours = mp3_amd.gapless_trim(_golden.to_int16(pcm), tag)
+    assert ours.shape == ref.shape, (ours.shape, ref.shape)
+    assert int(np.abs(ours.astype(np.int32) - ref.astype(np.int32)).max()) <= 1
+
+
+def test_oracle_no_tag_no_trim():
+    data, _ = _golden.case("c3_s0")
+    found, tag = _oracle.info_tag(data)
+    assert not found and not tag["has_lame"] and tag["skip_samples"] == 0
