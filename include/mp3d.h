@@ -77,6 +77,10 @@ MP3D_API void mp3d_dec_destroy(mp3d_dec *dec);
 MP3D_API void mp3d_dec_reset(mp3d_dec *dec);
 MP3D_API int mp3d_decode_frame(mp3d_dec *dec, const uint8_t *buf, size_t bytes, int16_t *pcm /* <= 2304 */,
                       mp3d_frame_info *info);
+/* the same with float32 PCM (FFmpeg's float convention: full scale 1.0,
+ * not clipped; the int16 output is clamp(rint(x * 32768)) of these values) */
+MP3D_API int mp3d_decode_frame_f32(mp3d_dec *dec, const uint8_t *buf, size_t bytes, float *pcm /* <= 2304 */,
+                          mp3d_frame_info *info);
 
 /* ---- batched decoder (many concurrent streams on one GPU) -------------- *
  * A batch handle keeps per-stream decoder state resident in HBM across
@@ -98,6 +102,10 @@ MP3D_API int mp3d_batch_reset(mp3d_batch *b); /* forget all per-stream state    
 MP3D_API int mp3d_batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets, const uint32_t *sizes,
                       int n_streams, int frames_per_stream, int16_t *pcm, mp3d_frame_info *infos,
                       void *hip_stream);
+/* float32 PCM sink: pcm [n_streams][frames_per_stream][2304] float */
+MP3D_API int mp3d_batch_decode_f32(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets,
+                          const uint32_t *sizes, int n_streams, int frames_per_stream, float *pcm,
+                          mp3d_frame_info *infos, void *hip_stream);
 MP3D_API int mp3d_batch_sync(mp3d_batch *b);
 
 /* ---- staged entry points (parity taps / BASELINE config 2) ------------- *

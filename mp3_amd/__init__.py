@@ -42,6 +42,7 @@ FRAME_INFO_DT = np.dtype([("frame_bytes", np.int32), ("channels", np.int32), ("h
                           ("layer", np.int32), ("bitrate_kbps", np.int32), ("samples", np.int32)])
 
 EXPORTS = ["mp3d_dec_create", "mp3d_dec_create_on", "mp3d_dec_destroy", "mp3d_dec_reset", "mp3d_decode_frame",
+           "mp3d_decode_frame_f32", "mp3d_batch_decode_f32",
            "mp3d_batch_create", "mp3d_batch_destroy", "mp3d_batch_reset", "mp3d_batch_decode", "mp3d_batch_sync",
            "mp3d_batch_huffman_only", "mp3d_batch_synth_only", "mp3d_strerror", "mp3d_last_hip_error",
            "mp3d_abi_version", "mp3d_batch_set_timing", "mp3d_batch_kernel_times", "mp3d_batch_stream_info",
@@ -74,6 +75,8 @@ def lib():
         L.mp3d_batch_destroy.restype = None
         L.mp3d_batch_reset.argtypes = [vp]
         L.mp3d_batch_decode.argtypes = [vp, vp, u64p, u32p, i, i, vp, vp, vp]
+        L.mp3d_batch_decode_f32.argtypes = [vp, vp, u64p, u32p, i, i, vp, vp, vp]
+        L.mp3d_decode_frame_f32.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t, vp, ctypes.POINTER(FrameInfo)]
         L.mp3d_batch_sync.argtypes = [vp]
         L.mp3d_batch_huffman_only.argtypes = [vp, vp, u64p, u32p, i, i, vp, vp, vp]
         L.mp3d_batch_synth_only.argtypes = [vp, vp, vp, vp, i, i, i, i, vp, vp]
@@ -134,12 +137,14 @@ class Decoder:
     def reset(self):
         lib().mp3d_dec_reset(self._h)
 
-    def decode_frame(self, buf):
-        """Returns (samples_per_channel, pcm int16 [samples*channels], FrameInfo)."""
-        pcm = np.zeros(2304, np.int16)
+    def decode_frame(self, buf, f32=False):
+        """Returns (samples_per_channel, pcm [samples*channels], FrameInfo);
+        pcm is int16, or float32 (full scale 1.0, unclipped) with f32=True."""
+        pcm = np.zeros(2304, np.float32 if f32 else np.int16)
         info = FrameInfo()
         buf = bytes(buf)
-        n = _check(lib().mp3d_decode_frame(self._h, buf, len(buf), pcm.ctypes.data, ctypes.byref(info)))
+        fn = lib().mp3d_decode_frame_f32 if f32 else lib().mp3d_decode_frame
+        n = _check(fn(self._h, buf, len(buf), pcm.ctypes.data, ctypes.byref(info)))
         return n, pcm[: n * max(info.channels, 1)], info
 
     def stream_info(self):
@@ -148,17 +153,17 @@ class Decoder:
         _check(lib().mp3d_dec_stream_info(self._h, ctypes.byref(info)))
         return info
 
-    def decode_stream(self, data, gapless=False):
-        """Decode a whole byte stream; returns int16 [channels, samples].
-        gapless=True drops encoder delay / padding as the stream's LAME tag
-        says (gapless_trim)."""
+    def decode_stream(self, data, gapless=False, f32=False):
+        """Decode a whole byte stream; returns int16 (float32 with f32=True)
+        [channels, samples].  gapless=True drops encoder delay / padding as
+        the stream's LAME tag says (gapless_trim)."""
         if gapless:
-            return gapless_trim(self.decode_stream(data), self.stream_info())
+            return gapless_trim(self.decode_stream(data, f32=f32), self.stream_info())
         data = bytes(data)
         pos, out, nch = 0, [], 0
         while pos < len(data):
             try:
-                n, pcm, info = self.decode_frame(data[pos:])
+                n, pcm, info = self.decode_frame(data[pos:], f32=f32)
             except MP3DError:
                 break
             if info.frame_bytes <= 0:
@@ -168,7 +173,7 @@ class Decoder:
                 nch = info.channels
                 out.append(pcm.reshape(n, nch))
         if not out:
-            return np.zeros((0, 0), np.int16)
+            return np.zeros((0, 0), np.float32 if f32 else np.int16)
         return np.concatenate(out).T.copy()
 
 
@@ -212,21 +217,21 @@ class BatchDecoder:
             raise ValueError("offsets/sizes shape mismatch")
         return off, sz
 
-    def decode(self, frames, offsets, sizes, frames_per_stream, pcm=None, infos=None, stream=None):
+    def decode(self, frames, offsets, sizes, frames_per_stream, pcm=None, infos=None, stream=None, f32=False):
         """frames: bytes/np.uint8/torch.uint8; pcm: None (allocate host) or
-        int16 array/tensor [n, F, 2304]; infos: None or FRAME_INFO_DT array /
-        int32 tensor [n, F, 6].  Returns (pcm, infos)."""
+        int16 (float32 with f32=True) array/tensor [n, F, 2304]; infos: None
+        or FRAME_INFO_DT array / int32 tensor [n, F, 6].  Returns (pcm, infos)."""
         off, sz = self._geom(offsets, sizes)
         n, F = off.size, int(frames_per_stream)
         if pcm is None:
-            pcm = np.zeros((n, F, 2304), np.int16)
+            pcm = np.zeros((n, F, 2304), np.float32 if f32 else np.int16)
         if infos is None:
             infos = np.zeros((n, F), FRAME_INFO_DT)
         fp, k1 = _ptr(frames)
         pp, k2 = _ptr(pcm)
         ip, k3 = _ptr(infos)
-        _check(lib().mp3d_batch_decode(self._h, fp, off.ctypes.data, sz.ctypes.data, n, F, pp, ip,
-                                       ctypes.c_void_p(stream) if stream else None))
+        fn = lib().mp3d_batch_decode_f32 if f32 else lib().mp3d_batch_decode
+        _check(fn(self._h, fp, off.ctypes.data, sz.ctypes.data, n, F, pp, ip, ctypes.c_void_p(stream) if stream else None))
         return pcm, infos
 
     def stream_info(self, n_streams):
@@ -260,7 +265,8 @@ class BatchDecoder:
 
 
 def pcm_to_planar(pcm_frames, infos):
-    """[F, 2304] int16 + infos [F] -> [channels, samples] for frames with audio."""
+    """[F, 2304] int16/float32 + infos [F] -> [channels, samples] for frames
+    with audio."""
     rows = []
     nch = 0
     for f in range(pcm_frames.shape[0]):
@@ -268,7 +274,7 @@ def pcm_to_planar(pcm_frames, infos):
             nch = int(infos[f]["channels"])
             rows.append(pcm_frames[f, : 1152 * nch].reshape(1152, nch))
     if not rows:
-        return np.zeros((0, 0), np.int16)
+        return np.zeros((0, 0), pcm_frames.dtype)
     return np.concatenate(rows).T.copy()
 
 

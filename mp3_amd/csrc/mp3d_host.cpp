@@ -27,7 +27,7 @@ void launch_demux(const uint8_t *, const uint64_t *, const uint32_t *, uint8_t *
                   FrameRec *, uint64_t *, void *, int, int, hipStream_t);
 void launch_huffman(const uint8_t *, const uint64_t *, const FrameRec *, const uint64_t *, const DevTables *, int16_t *,
                     UnitMeta *, int, int, int, hipStream_t);
-void launch_synth(const FrameRec *, const int16_t *, const UnitMeta *, const DevTables *, StreamState *, int16_t *, int,
+void launch_synth(const FrameRec *, const int16_t *, const UnitMeta *, const DevTables *, StreamState *, void *, bool, int,
                   int, hipStream_t);
 void launch_synth_xr(const float *, const uint8_t *, const uint8_t *, const DevTables *, StreamState *, int16_t *, int,
                      int, int, int, hipStream_t);
@@ -433,15 +433,16 @@ static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offse
     return MP3D_OK;
 }
 
-extern "C" int mp3d_batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets, const uint32_t *sizes,
-                                 int n, int F, int16_t *pcm, mp3d_frame_info *infos, void *hip_stream) {
+/* decode into int16 (f32 = false) or float32 PCM, both [n][F][2304] */
+static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets, const uint32_t *sizes, int n,
+                        int F, void *pcm, bool f32, mp3d_frame_info *infos, void *hip_stream) {
     if (!b || !pcm) return MP3D_E_ARG;
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : b->own;
     bool sync_needed = false;
     int r = run_front(b, frames, offsets, sizes, n, F, s, &sync_needed);
     if (r) return r;
-    size_t pcm_bytes = (size_t)n * F * 2304 * sizeof(int16_t);
-    int16_t *dpcm = pcm;
+    size_t pcm_bytes = (size_t)n * F * 2304 * (f32 ? sizeof(float) : sizeof(int16_t));
+    void *dpcm = pcm;
     bool pcm_host = !is_device_ptr(pcm);
     if (pcm_host) {
         r = grow((void **)&b->d_pcm, &b->pcm_cap, pcm_bytes);
@@ -451,7 +452,7 @@ extern "C" int mp3d_batch_decode(mp3d_batch *b, const uint8_t *frames, const uin
         HIPCHK(hipMemcpyAsync(dpcm, pcm, pcm_bytes, hipMemcpyHostToDevice, s));
     }
     DeviceCtx &dc = g_dev[b->device];
-    launch_synth(b->rec, b->is_buf, b->meta, dc.tables, b->st, dpcm, n, F, s);
+    launch_synth(b->rec, b->is_buf, b->meta, dc.tables, b->st, dpcm, f32, n, F, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[3], s));
     HIPCHK(hipGetLastError());
     if (pcm_host) {
@@ -469,6 +470,17 @@ extern "C" int mp3d_batch_decode(mp3d_batch *b, const uint8_t *frames, const uin
     }
     if (sync_needed) HIPCHK(hipStreamSynchronize(s));
     return MP3D_OK;
+}
+
+extern "C" int mp3d_batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets, const uint32_t *sizes,
+                                 int n, int F, int16_t *pcm, mp3d_frame_info *infos, void *hip_stream) {
+    return batch_decode(b, frames, offsets, sizes, n, F, pcm, false, infos, hip_stream);
+}
+
+extern "C" int mp3d_batch_decode_f32(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets,
+                                     const uint32_t *sizes, int n, int F, float *pcm, mp3d_frame_info *infos,
+                                     void *hip_stream) {
+    return batch_decode(b, frames, offsets, sizes, n, F, pcm, true, infos, hip_stream);
 }
 
 extern "C" int mp3d_batch_huffman_only(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets,
@@ -627,8 +639,7 @@ static int host_frame_bytes(const uint8_t *p) {
     return 144000 * (int)MP3D_BITRATE_L3[bi] / (int)MP3D_SAMPLE_RATE[si] + ((p[2] >> 1) & 1);
 }
 
-extern "C" int mp3d_decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, int16_t *pcm,
-                                 mp3d_frame_info *info) {
+static int decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, void *pcm, bool f32, mp3d_frame_info *info) {
     if (!d || !buf) return MP3D_E_ARG;
     mp3d_frame_info tmp;
     if (!info) info = &tmp;
@@ -651,15 +662,24 @@ extern "C" int mp3d_decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, 
     }
     uint64_t off = 0;
     uint32_t sz = (uint32_t)fb;
-    int16_t out[2304];
+    float out[2304]; /* large enough for either sample type */
     mp3d_frame_info fi;
-    int r = mp3d_batch_decode(d->b, buf + pos, &off, &sz, 1, 1, out, &fi, nullptr);
+    int r = batch_decode(d->b, buf + pos, &off, &sz, 1, 1, out, f32, &fi, nullptr);
     if (r) return r;
     d->frames++;
     *info = fi;
     info->frame_bytes = (int)pos + fi.frame_bytes;
-    if (fi.samples && pcm) memcpy(pcm, out, sizeof(int16_t) * 1152 * fi.channels);
+    if (fi.samples && pcm) memcpy(pcm, out, (f32 ? sizeof(float) : sizeof(int16_t)) * 1152 * fi.channels);
     return fi.samples;
+}
+
+extern "C" int mp3d_decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, int16_t *pcm, mp3d_frame_info *info) {
+    return decode_frame(d, buf, bytes, pcm, false, info);
+}
+
+extern "C" int mp3d_decode_frame_f32(mp3d_dec *d, const uint8_t *buf, size_t bytes, float *pcm,
+                                     mp3d_frame_info *info) {
+    return decode_frame(d, buf, bytes, pcm, true, info);
 }
 
 /* ------------------------------------------------------------------------ */

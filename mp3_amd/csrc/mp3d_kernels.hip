@@ -875,11 +875,13 @@ struct SynWave {                     /* one per wave (stream)                   
 
 #define WAIT_VMCNT0() __builtin_amdgcn_s_waitcnt(0x0F70) /* vmcnt(0), other counters free */
 
-template <bool SRC_XR>
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+template <bool SRC_XR, bool F32>
 __global__ void __launch_bounds__(64 * SYN_WAVES) __attribute__((amdgpu_waves_per_eu(3, 8)))
 k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, const UnitMeta *__restrict__ meta,
         const float *__restrict__ xr_in, const uint8_t *__restrict__ xr_bt, const uint8_t *__restrict__ xr_mixed,
-        const DevTables *__restrict__ tab, StreamState *__restrict__ st, int16_t *__restrict__ pcm, int n_streams,
+        const DevTables *__restrict__ tab, StreamState *__restrict__ st, void *__restrict__ pcm, int n_streams,
         int F, int xr_nch, int xr_sr) {
     __shared__ __attribute__((aligned(16))) SynShared T;
     __shared__ __attribute__((aligned(16))) SynWave Wv[SYN_WAVES];
@@ -931,8 +933,9 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
         (void *)(meta + (size_t)s * F * 4), 0, F * 4 * (int)sizeof(UnitMeta), 0x00020000);
     const __amdgpu_buffer_rsrc_t r_rec = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(rec + (size_t)s * F), 0, F * (int)sizeof(FrameRec), 0x00020000);
+    constexpr int PB = F32 ? 4 : 2; /* bytes per output sample: f32 or int16 */
     const __amdgpu_buffer_rsrc_t r_pcm = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(pcm + (size_t)s * F * 2304), 0, F * 4608, 0x00020000);
+        (void *)((uint8_t *)pcm + (size_t)s * F * 2304 * PB), 0, F * 2304 * PB, 0x00020000);
 
     /* granule prefetch, one granule ahead of use: is[] words (lane owns
      * lines 2 lane + 128 i, +1), UnitMeta words of both channels (lanes
@@ -1345,7 +1348,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                 /* output slots in pairs (t0, t1): lanes 0-31 hold L, lanes
                  * 32-63 R; one half-wave swap leaves lane j with (L, R) of
                  * slot t0 and lane 32 + j with (L, R) of slot t1 */
-                auto pcm_at = [&](int t) {
+                auto out_at = [&](int t) {
                     float o = 0.f;
 #pragma unroll
                     for (int i = 0; i < 8; i++) {
@@ -1355,11 +1358,35 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                         o = fmaf(Dw[2 * i], va, o);
                         o = fmaf(Dw[2 * i + 1], vb, o);
                     }
-                    const float p = rintf(o * 32768.f);
+                    return o;
+                };
+                auto pcm_at = [&](int t) {
+                    const float p = rintf(out_at(t) * 32768.f);
                     return (int)fminf(fmaxf(p, -32768.f), 32767.f);
                 };
-                if (nch == 2) {
-                    const int vo = opaque((sb + 32 * ch) * 4), so = f * 4608 + gr * 2304;
+                const int so = f * 2304 * PB + gr * 576 * nch * PB;
+                if (F32) {
+                    /* float sink: the same sums, unscaled and unclipped (FFmpeg's
+                     * float decoder convention); (L, R) = 8 B per lane and slot */
+                    if (nch == 2) {
+                        const int vo = opaque((sb + 32 * ch) * 8);
+#pragma unroll
+                        for (int tp = 0; tp < 9; tp++) {
+                            const float o0 = out_at(2 * tp), o1 = out_at(2 * tp + 1);
+                            const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(o0), __float_as_uint(o1),
+                                                                            false, false);
+                            __builtin_amdgcn_raw_buffer_store_b64((u32x2){r[0], r[1]}, r_pcm, vo + 512 * tp, so, 0);
+                        }
+                    } else {
+                        const int vo = opaque(sb * 4);
+#pragma unroll
+                        for (int t = 0; t < 18; t++) {
+                            const float o = out_at(t);
+                            if (active) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), r_pcm, vo + 128 * t, so, 0);
+                        }
+                    }
+                } else if (nch == 2) {
+                    const int vo = opaque((sb + 32 * ch) * 4);
 #pragma unroll
                     for (int tp = 0; tp < 9; tp++) {
                         const int p0 = pcm_at(2 * tp), p1 = pcm_at(2 * tp + 1);
@@ -1368,7 +1395,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                                                               r_pcm, vo + 256 * tp, so, 0);
                     }
                 } else {
-                    const int vo = opaque(sb * 2), so = f * 4608 + gr * 1152;
+                    const int vo = opaque(sb * 2);
 #pragma unroll
                     for (int t = 0; t < 18; t++) {
                         const int p = pcm_at(t);
@@ -1428,17 +1455,21 @@ void launch_huffman(const uint8_t *md, const uint64_t *md_off, const FrameRec *r
 }
 
 void launch_synth(const FrameRec *rec, const int16_t *is_buf, const UnitMeta *meta, const DevTables *tab,
-                  StreamState *st, int16_t *pcm, int n_streams, int F, hipStream_t strm) {
-    hipLaunchKernelGGL(k_synth<false>, dim3((n_streams + SYN_WAVES - 1) / SYN_WAVES), dim3(64 * SYN_WAVES), 0, strm, rec,
-                       is_buf, meta, (const float *)nullptr, (const uint8_t *)nullptr, (const uint8_t *)nullptr, tab, st,
-                       pcm, n_streams, F, 2, 0);
+                  StreamState *st, void *pcm, bool f32, int n_streams, int F, hipStream_t strm) {
+    const dim3 grid((n_streams + SYN_WAVES - 1) / SYN_WAVES), block(64 * SYN_WAVES);
+    if (f32)
+        hipLaunchKernelGGL((k_synth<false, true>), grid, block, 0, strm, rec, is_buf, meta, (const float *)nullptr,
+                           (const uint8_t *)nullptr, (const uint8_t *)nullptr, tab, st, pcm, n_streams, F, 2, 0);
+    else
+        hipLaunchKernelGGL((k_synth<false, false>), grid, block, 0, strm, rec, is_buf, meta, (const float *)nullptr,
+                           (const uint8_t *)nullptr, (const uint8_t *)nullptr, tab, st, pcm, n_streams, F, 2, 0);
 }
 
 void launch_synth_xr(const float *xr, const uint8_t *bt, const uint8_t *mixed, const DevTables *tab, StreamState *st,
                      int16_t *pcm, int n_streams, int F, int nch, int sr, hipStream_t strm) {
-    hipLaunchKernelGGL(k_synth<true>, dim3((n_streams + SYN_WAVES - 1) / SYN_WAVES), dim3(64 * SYN_WAVES), 0, strm,
-                       (const FrameRec *)nullptr, (const int16_t *)nullptr, (const UnitMeta *)nullptr, xr, bt, mixed, tab,
-                       st, pcm, n_streams, F, nch, sr);
+    hipLaunchKernelGGL((k_synth<true, false>), dim3((n_streams + SYN_WAVES - 1) / SYN_WAVES), dim3(64 * SYN_WAVES), 0,
+                       strm, (const FrameRec *)nullptr, (const int16_t *)nullptr, (const UnitMeta *)nullptr, xr, bt,
+                       mixed, tab, st, (void *)pcm, n_streams, F, nch, sr);
 }
 
 } // namespace mp3d
