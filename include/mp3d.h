@@ -145,6 +145,38 @@ typedef struct mp3d_stream_info {
 MP3D_API int mp3d_batch_stream_info(mp3d_batch *b, int n_streams, mp3d_stream_info *out);
 MP3D_API int mp3d_dec_stream_info(mp3d_dec *dec, mp3d_stream_info *out);
 
+/* ---- one long stream at full-GPU speed (frame-parallel) ---------------- *
+ * Decodes a whole stream (data[0 .. bytes), host or device) by splitting it
+ * into segments of L output frames that run as concurrent virtual streams
+ * of one batch call.  Each segment starts a few frames early (payloads of
+ * >= 511 bytes, the largest main_data_begin, before its first frame but one),
+ * so its output is bit-identical to a sequential decode; the warm-up frames'
+ * output is discarded.  The handle (mp3d_batch_create) needs max_streams
+ * >= 1 and max_frames >= L + 11: the warm-up is 4 frames at 128 kbps
+ * stereo and at most 11 (32 kbps); more max_streams runs more segments per
+ * kernel launch.
+ * pcm     [max_frames][2304] int16, or float with f32 != 0; host or device.
+ *         Row j is frame slot j of the stream, zero for slots without
+ *         audio (Xing/Info frame, dropped frame); a mono row holds 1152
+ *         samples and zeros.
+ * infos   [max_frames] or NULL, host or device.
+ * n_frames   out: frame slots found (MP3D_E_CAPACITY if > max_frames).
+ * sinfo   stream info (Xing/Info tag, gapless trim) or NULL.
+ * Synchronous; the batch's per-stream state is clobbered (reset it before
+ * using the handle for ordinary batch calls).                              */
+MP3D_API int mp3d_batch_decode_long(mp3d_batch *b, const uint8_t *data, size_t bytes, int L, void *pcm, int f32,
+                                    long long max_frames, mp3d_frame_info *infos, long long *n_frames,
+                                    mp3d_stream_info *sinfo);
+
+/* Host-side plan of mp3d_batch_decode_long (no GPU needed): the stream's
+ * frame slots (frame_off[n_frames], byte offset of each frame header) and
+ * the first frame of each segment's warm-up (seg_start[ceil(n_frames / L)]);
+ * either array may be NULL.  max_warmup = max over segments of
+ * k * L - seg_start[k].  data must be host memory.  A caller can shard the
+ * segments of one stream over several GPUs with it.                        */
+MP3D_API int mp3d_long_plan(const uint8_t *data, size_t bytes, int L, long long max_frames, uint64_t *frame_off,
+                            long long *seg_start, long long *n_frames, int *max_warmup);
+
 /* ---- diagnostics -------------------------------------------------------- */
 MP3D_API const char *mp3d_strerror(int err);
 MP3D_API int mp3d_last_hip_error(void);

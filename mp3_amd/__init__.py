@@ -46,7 +46,8 @@ EXPORTS = ["mp3d_dec_create", "mp3d_dec_create_on", "mp3d_dec_destroy", "mp3d_de
            "mp3d_batch_create", "mp3d_batch_destroy", "mp3d_batch_reset", "mp3d_batch_decode", "mp3d_batch_sync",
            "mp3d_batch_huffman_only", "mp3d_batch_synth_only", "mp3d_strerror", "mp3d_last_hip_error",
            "mp3d_abi_version", "mp3d_batch_set_timing", "mp3d_batch_kernel_times", "mp3d_batch_stream_info",
-           "mp3d_dec_stream_info"]
+           "mp3d_dec_stream_info", "mp3d_batch_decode_long",
+           "mp3d_long_plan"]
 
 _lib = None
 
@@ -86,6 +87,10 @@ def lib():
         L.mp3d_batch_kernel_times.argtypes = [vp, vp]
         L.mp3d_batch_stream_info.argtypes = [vp, i, vp]
         L.mp3d_dec_stream_info.argtypes = [vp, ctypes.POINTER(StreamInfo)]
+        L.mp3d_batch_decode_long.argtypes = [vp, vp, ctypes.c_size_t, i, vp, i, ctypes.c_longlong, vp,
+                                             ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(StreamInfo)]
+        L.mp3d_long_plan.argtypes = [ctypes.c_char_p, ctypes.c_size_t, i, ctypes.c_longlong, vp, vp,
+                                     ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_int)]
         _lib = L
     return _lib
 
@@ -240,6 +245,29 @@ class BatchDecoder:
         _check(lib().mp3d_batch_stream_info(self._h, int(n_streams), ctypes.cast(arr, ctypes.c_void_p)))
         return list(arr)
 
+    def decode_long(self, data, segment_frames=32, max_frames=None, pcm=None, infos=None, f32=False):
+        """Frame-parallel decode of ONE long stream (mp3d_batch_decode_long):
+        segments of segment_frames output frames run as concurrent virtual
+        streams, bit-identical to a sequential decode.  data: bytes /
+        np.uint8 / torch.uint8 (host or device).  pcm: None (allocate host)
+        or [max_frames, 2304] int16 (float32 with f32=True) array/tensor.
+        Returns (pcm[:n], infos[:n], StreamInfo)."""
+        nbytes = data.numel() if hasattr(data, "numel") else len(data)
+        if max_frames is None:
+            max_frames = max_frame_slots(nbytes)
+        if pcm is None:
+            pcm = np.zeros((max_frames, 2304), np.float32 if f32 else np.int16)
+        if infos is None:
+            infos = np.zeros(max_frames, FRAME_INFO_DT)
+        dp, k1 = _ptr(data)
+        pp, k2 = _ptr(pcm)
+        ip, k3 = _ptr(infos)
+        n = ctypes.c_longlong()
+        si = StreamInfo()
+        _check(lib().mp3d_batch_decode_long(self._h, dp, nbytes, int(segment_frames), pp, int(f32), int(max_frames),
+                                            ip, ctypes.byref(n), ctypes.byref(si)))
+        return pcm[: n.value], infos[: n.value], si
+
     def huffman_only(self, frames, offsets, sizes, frames_per_stream):
         off, sz = self._geom(offsets, sizes)
         n, F = off.size, int(frames_per_stream)
@@ -262,6 +290,29 @@ class BatchDecoder:
         _check(lib().mp3d_batch_synth_only(self._h, xp, bp, mp, n, F, int(nch), int(hz), pp,
                                            ctypes.c_void_p(stream) if stream else None))
         return pcm
+
+
+def max_frame_slots(nbytes):
+    """Upper bound on the frame slots in nbytes of stream (the smallest
+    Layer III frame is 96 B: 32 kbps at 48 kHz)."""
+    return int(nbytes) // 96 + 2
+
+
+def long_plan(data, segment_frames=32, max_frames=None):
+    """Host-side segment plan of BatchDecoder.decode_long (mp3d_long_plan;
+    no GPU needed).  Returns (frame_off [n] uint64, seg_start [K] int64,
+    max_warmup)."""
+    data = bytes(data)
+    if max_frames is None:
+        max_frames = max_frame_slots(len(data))
+    L = int(segment_frames)
+    off = np.zeros(max_frames, np.uint64)
+    seg = np.zeros(max_frames // max(L, 1) + 2, np.int64)
+    n, w = ctypes.c_longlong(), ctypes.c_int()
+    _check(lib().mp3d_long_plan(data, len(data), L, int(max_frames), off.ctypes.data, seg.ctypes.data,
+                                ctypes.byref(n), ctypes.byref(w)))
+    k = (n.value + L - 1) // L
+    return off[: n.value], seg[:k], w.value
 
 
 def pcm_to_planar(pcm_frames, infos):

@@ -31,6 +31,8 @@ void launch_synth(const FrameRec *, const int16_t *, const UnitMeta *, const Dev
                   int, hipStream_t);
 void launch_synth_xr(const float *, const uint8_t *, const uint8_t *, const DevTables *, StreamState *, int16_t *, int,
                      int, int, int, hipStream_t);
+void launch_gather_frames(const void *, void *, const void *, void *, const int *, int, int, int, int, int,
+                          hipStream_t);
 } // namespace mp3d
 
 using namespace mp3d;
@@ -585,6 +587,180 @@ extern "C" int mp3d_batch_stream_info(mp3d_batch *b, int n, mp3d_stream_info *ou
                        2 * sizeof(uint32_t), n, hipMemcpyDeviceToHost));
     for (int i = 0; i < n; i++) tag_to_info(tag[2 * i], tag[2 * i + 1], &out[i]);
     return MP3D_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Segmented decode of one long stream               */
+/* ------------------------------------------------------------------------ */
+static int host_frame_bytes(const uint8_t *p);
+
+/* Frame slots of a stream exactly as k_demux enumerates them: ID3v2 skip,
+ * resync on the next valid header, a cut-short final frame kept while its
+ * header and side info are present.  payload = bytes after the side info. */
+static void walk_frames(const uint8_t *p, size_t len, std::vector<uint64_t> &off, std::vector<uint32_t> &payload) {
+    size_t cur = 0;
+    if (len >= 10 && p[0] == 'I' && p[1] == 'D' && p[2] == '3')
+        cur = 10 + (((size_t)(p[6] & 0x7F) << 21) | ((size_t)(p[7] & 0x7F) << 14) | ((size_t)(p[8] & 0x7F) << 7) |
+                    (p[9] & 0x7F)) +
+              ((p[5] & 0x10) ? 10 : 0);
+    while (cur + 4 <= len) {
+        int fb = -1;
+        for (; cur + 4 <= len; cur++)
+            if ((fb = host_frame_bytes(p + cur)) > 0) break;
+        if (fb <= 0) break;
+        const int nch = (p[cur + 3] >> 6) == 3 ? 1 : 2;
+        const size_t need = 4 + ((p[cur + 1] & 1) ? 0 : 2) + (nch == 1 ? 17 : 32);
+        if (cur + fb > len && cur + need > len) break;
+        off.push_back(cur);
+        payload.push_back(fb > (int)need ? (uint32_t)(fb - need) : 0u);
+        cur = cur + fb <= len ? cur + fb : len;
+    }
+}
+
+/* Split the stream into segments of L output frames decoded as independent
+ * virtual streams of one batch call.  Segment k (k >= 1) starts at frame
+ * a_k < kL, chosen so that the payloads of frames [a_k, kL - 2) hold >= 511
+ * bytes (the largest main_data_begin).  Why that suffices (k_demux's
+ * reservoir rule): the bytes available after a frame, P + plen - end, do not
+ * depend on the history once the frame's main-data start P - mdb is inside
+ * the virtual stream's md region, i.e. from frame kL - 2 on; frame kL - 1
+ * then decodes from real bytes with the sequential decoder's reservoir
+ * decision, and its second granule alone feeds frame kL's IMDCT overlap and
+ * synthesis FIFO (15 slots < 18 per granule).  Output frames [kL, (k+1)L)
+ * are therefore bit-exact with a sequential decode of the whole stream;
+ * warm-up output is dropped. */
+static int long_plan(const uint8_t *p, size_t bytes, int L, long long max_frames, std::vector<uint64_t> &off,
+                     std::vector<long long> &a, int *wmax) {
+    std::vector<uint32_t> pay;
+    walk_frames(p, bytes, off, pay);
+    const long long N = (long long)off.size();
+    if (N > max_frames) return MP3D_E_CAPACITY;
+    const long long K = (N + L - 1) / L;
+    a.assign(K, 0);
+    *wmax = 0;
+    for (long long k = 0; k < K; k++) {
+        long long j = std::max(0LL, k * L - 2), acc = 0;
+        while (j > 0 && acc < MP3D_RES_BYTES - 1) acc += pay[--j];
+        a[k] = j;
+        *wmax = std::max(*wmax, (int)(k * L - j));
+    }
+    return MP3D_OK;
+}
+
+extern "C" int mp3d_long_plan(const uint8_t *data, size_t bytes, int L, long long max_frames, uint64_t *frame_off,
+                              long long *seg_start, long long *n_frames, int *max_warmup) {
+    if (!data || L <= 0 || max_frames < 0 || !n_frames) return MP3D_E_ARG;
+    std::vector<uint64_t> off;
+    std::vector<long long> a;
+    int wmax = 0;
+    *n_frames = 0;
+    const int r = long_plan(data, bytes, L, max_frames, off, a, &wmax);
+    if (r) return r;
+    *n_frames = (long long)off.size();
+    if (frame_off) std::copy(off.begin(), off.end(), frame_off);
+    if (seg_start) std::copy(a.begin(), a.end(), seg_start);
+    if (max_warmup) *max_warmup = wmax;
+    return MP3D_OK;
+}
+
+static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets, const uint32_t *sizes, int n,
+                        int F, void *pcm, bool f32, mp3d_frame_info *infos, void *hip_stream);
+
+extern "C" int mp3d_batch_decode_long(mp3d_batch *b, const uint8_t *data, size_t bytes, int L, void *pcm, int f32,
+                                      long long max_frames, mp3d_frame_info *infos, long long *n_frames,
+                                      mp3d_stream_info *sinfo) {
+    if (!b || !data || !pcm || L <= 0 || max_frames <= 0 || !n_frames) return MP3D_E_ARG;
+    *n_frames = 0;
+    HIPCHK(hipSetDevice(b->device));
+    const bool dev_in = is_device_ptr(data);
+    std::vector<uint8_t> host_copy;
+    const uint8_t *hp = data;
+    if (dev_in) { /* the frame walk runs on the host */
+        host_copy.resize(bytes);
+        HIPCHK(hipMemcpy(host_copy.data(), data, bytes, hipMemcpyDeviceToHost));
+        hp = host_copy.data();
+    }
+    std::vector<uint64_t> off;
+    std::vector<long long> a;
+    int wmax = 0;
+    long long N = 0;
+    {
+        const int r = long_plan(hp, bytes, L, max_frames, off, a, &wmax);
+        if (r) return r;
+        N = (long long)off.size();
+    }
+    *n_frames = N;
+    if (N == 0) return MP3D_OK;
+    const long long K = (long long)a.size();
+    const int F = L + wmax;
+    if (F > b->max_frames) return MP3D_E_CAPACITY;
+    hipStream_t s = b->own;
+    const uint8_t *din = data;
+    if (!dev_in) {
+        int r = grow((void **)&b->d_in, &b->in_cap, bytes + 64);
+        if (r) return r;
+        HIPCHK(hipMemcpyAsync(b->d_in, data, bytes, hipMemcpyHostToDevice, s));
+        din = b->d_in;
+    }
+    const size_t row = 2304 * (f32 ? sizeof(float) : sizeof(int16_t));
+    const bool pcm_dev = is_device_ptr(pcm), inf_dev = infos && is_device_ptr(infos);
+    const int chunk = b->max_streams;
+    void *seg_pcm = nullptr, *out_pcm = nullptr;
+    int *d_a = nullptr;
+    std::vector<int> a32;
+    mp3d_frame_info *out_inf = nullptr;
+    int rc = MP3D_OK;
+#define LCHK(x)                                                                                                        \
+    do {                                                                                                               \
+        hipError_t _e = (x);                                                                                           \
+        if (_e != hipSuccess) {                                                                                        \
+            g_last_hip = (int)_e;                                                                                      \
+            rc = MP3D_E_HIP;                                                                                           \
+            goto done;                                                                                                 \
+        }                                                                                                              \
+    } while (0)
+    LCHK(hipMalloc(&seg_pcm, (size_t)std::min<long long>(chunk, K) * F * row));
+    LCHK(hipMalloc(&d_a, sizeof(int) * K));
+    a32.assign(a.begin(), a.end());
+    LCHK(hipMemcpyAsync(d_a, a32.data(), sizeof(int) * K, hipMemcpyHostToDevice, s));
+    out_pcm = pcm_dev ? pcm : nullptr;
+    if (!pcm_dev) LCHK(hipMalloc(&out_pcm, (size_t)N * row));
+    if (infos) {
+        out_inf = inf_dev ? infos : nullptr;
+        if (!inf_dev) LCHK(hipMalloc(&out_inf, sizeof(mp3d_frame_info) * (size_t)N));
+    }
+    for (long long k0 = 0; k0 < K; k0 += chunk) {
+        const int ns = (int)std::min<long long>(chunk, K - k0);
+        std::vector<uint64_t> so(ns);
+        std::vector<uint32_t> ss(ns);
+        for (int i = 0; i < ns; i++) {
+            const long long k = k0 + i, e = std::min(N, (k + 1) * L);
+            so[i] = k == 0 ? 0 : off[a[k]];
+            ss[i] = (uint32_t)((e < N ? off[e] : bytes) - so[i]);
+        }
+        /* fresh decoder state for every virtual stream */
+        LCHK(hipMemsetAsync(b->st, 0, sizeof(StreamState) * ns, s));
+        rc = batch_decode(b, din, so.data(), ss.data(), ns, F, seg_pcm, f32 != 0, nullptr, s);
+        if (rc) goto done;
+        if (k0 == 0 && sinfo) rc = mp3d_batch_stream_info(b, 1, sinfo);
+        if (rc) goto done;
+        const long long j0 = k0 * L, j1 = std::min(N, (k0 + ns) * L);
+        launch_gather_frames(seg_pcm, (uint8_t *)out_pcm + (size_t)j0 * row, b->d_infos, out_inf ? out_inf + j0 : nullptr,
+                             d_a + k0, L, F, (int)k0, (int)(j1 - j0), (int)row, s);
+        LCHK(hipGetLastError());
+    }
+    if (!pcm_dev) LCHK(hipMemcpyAsync(pcm, out_pcm, (size_t)N * row, hipMemcpyDeviceToHost, s));
+    if (infos && !inf_dev) LCHK(hipMemcpyAsync(infos, out_inf, sizeof(mp3d_frame_info) * (size_t)N, hipMemcpyDeviceToHost, s));
+    LCHK(hipStreamSynchronize(s));
+done:
+#undef LCHK
+    (void)hipStreamSynchronize(s);
+    if (seg_pcm) (void)hipFree(seg_pcm);
+    if (d_a) (void)hipFree(d_a);
+    if (!pcm_dev && out_pcm) (void)hipFree(out_pcm);
+    if (infos && !inf_dev && out_inf) (void)hipFree(out_inf);
+    b->last_n = -1; /* geometry cache: the virtual streams are not the caller's */
+    return rc;
 }
 
 /* ------------------------------------------------------------------------ */

@@ -1419,6 +1419,27 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
     for (int k = 0; k < 15; k++) S.fifo[ch][k][wb] = hb[k];
 }
 /* ------------------------------------------------------------------------ */
+/* k_gather_frames: segmented long-stream decode (mp3d_batch_decode_long).  */
+/* Output frame j of the long stream is frame (j - a[k]) of virtual stream  */
+/* k - k0 (k = j / L) in the batch output; copies its PCM row (16-B words)   */
+/* and frame info (zero-filled: rows without audio, the unused half of a   */
+/* mono row).  One workgroup per output frame.                              */
+/* ------------------------------------------------------------------------ */
+__global__ void __launch_bounds__(256) k_gather_frames(const uint4 *__restrict__ src, uint4 *__restrict__ dst,
+                                                       const DevInfo *__restrict__ isrc, DevInfo *__restrict__ idst,
+                                                       const int *__restrict__ a, int L, int F, int k0, int row16) {
+    const int jl = blockIdx.x;           /* output frame relative to segment k0's first */
+    const int k = jl / L;                /* segment relative to k0                      */
+    const int j = (k0 + k) * L + jl % L; /* global output frame                         */
+    const size_t sf = (size_t)k * F + (j - a[k]);
+    const DevInfo inf = isrc[sf];
+    const int lim = inf.samples == 0 ? 0 : inf.channels == 1 ? row16 / 2 : row16; /* mono: 1152 samples */
+    for (int i = threadIdx.x; i < row16; i += blockDim.x)
+        dst[(size_t)jl * row16 + i] = i < lim ? src[sf * row16 + i] : make_uint4(0u, 0u, 0u, 0u);
+    if (idst && threadIdx.x == 0) idst[jl] = isrc[sf];
+}
+
+/* ------------------------------------------------------------------------ */
 /* Host-side launchers                                                       */
 /* ------------------------------------------------------------------------ */
 hipError_t upload_constants(const float *imdct12, const float *win36, const float *win12,
@@ -1470,6 +1491,12 @@ void launch_synth_xr(const float *xr, const uint8_t *bt, const uint8_t *mixed, c
     hipLaunchKernelGGL((k_synth<true, false>), dim3((n_streams + SYN_WAVES - 1) / SYN_WAVES), dim3(64 * SYN_WAVES), 0,
                        strm, (const FrameRec *)nullptr, (const int16_t *)nullptr, (const UnitMeta *)nullptr, xr, bt,
                        mixed, tab, st, (void *)pcm, n_streams, F, nch, sr);
+}
+
+void launch_gather_frames(const void *src, void *dst, const void *isrc, void *idst, const int *a, int L, int F, int k0,
+                          int n_out, int bytes_per_row, hipStream_t strm) {
+    hipLaunchKernelGGL(k_gather_frames, dim3(n_out), dim3(256), 0, strm, (const uint4 *)src, (uint4 *)dst,
+                       (const DevInfo *)isrc, (DevInfo *)idst, a, L, F, k0, bytes_per_row / 16);
 }
 
 } // namespace mp3d
