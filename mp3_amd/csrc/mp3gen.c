@@ -1,5 +1,6 @@
 /*
- * mp3gen.c -- seeded synthetic MPEG-1 Layer III stream generator.
+ * mp3gen.c -- seeded synthetic MPEG-1 / MPEG-2 / MPEG-2.5 Layer III stream
+ * generator.
  *
  * Produces VALID bitstreams (header, side info, bit reservoir, scalefactors,
  * Huffman big_values / count1 regions) from seeded random quantised spectra,
@@ -8,8 +9,17 @@
  * CPU oracle and the FFmpeg golden vectors.  It is the input generator for
  * BASELINE.json configs 3-5 and for the parity tests.
  *
- * It is an encoder of the ISO 11172-3 bitstream syntax (2.4.1) -- the
- * reverse of the hot path, sharing only the standard's constant tables.
+ * It is an encoder of the ISO 11172-3 bitstream syntax (2.4.1), and of the
+ * ISO 13818-3 low-sampling-frequency (LSF) syntax for sample-rate indices
+ * 3..8 (MPEG-2 22.05/24/16 kHz, MPEG-2.5 11.025/12/8 kHz: one granule per
+ * frame, 8-bit main_data_begin, 9-bit scalefac_compress with the LSF slen /
+ * nr_of_sfb tables, LSF intensity positions) -- the reverse of the hot path,
+ * sharing only the standards' constant tables.
+ *
+ * Scalefactor layout of gunit.sf and of the truth records ("canonical", the
+ * layout of the decoder's UnitMeta.sf): long band b at b; short band b
+ * window w at 3 b + w; mixed blocks: long bands at b (8 of them MPEG-1, 6
+ * LSF), short band b >= 3 window w at 8 + 3 (b - 3) + w.
  */
 #include <math.h>
 #include <stdint.h>
@@ -57,7 +67,7 @@ static void bw_put(bw_t *w, uint32_t v, int n) {
 
 /* ---------------- configuration ------------------------------------------ */
 typedef struct {
-    int sr_idx;        /* 0..2, or -1: random per stream                    */
+    int sr_idx;        /* 0..8 (3..8 LSF), -1: random 0..2, -2: random 3..8  */
     int bitrate_idx;   /* 1..14 CBR, or 0: VBR (random index per frame)     */
     int mode;          /* 0..3, or -1: random per stream                    */
     int mode_ext;      /* joint stereo mode_ext 0..3, or -1: random/frame   */
@@ -79,6 +89,8 @@ typedef struct {
     int window_switching, block_type, mixed, table_select[3], subblock_gain[3];
     int region0_count, region1_count, preflag, scalefac_scale, count1table_select;
     int scalefac_compress, global_gain, big_values, part2_3_length, scfsi;
+    int lsf, is_right;      /* LSF unit / right channel of an intensity frame */
+    int slen[4], nsf[4];    /* LSF scalefactor groups (slen bits, count)      */
     int16_t is[576];
     uint8_t sf[40];
     int count1; /* number of count1 quadruples */
@@ -113,7 +125,11 @@ static int quad_bits(int sel, const int16_t *q, bw_t *w) {
 static void region_ends(const gunit *u, int sr_idx, int *r1, int *r2) {
     int bv2 = u->big_values * 2;
     if (u->window_switching) {
-        *r1 = 36; *r2 = 576;
+        /* FFmpeg: region0 of window-switched units is 36 lines, except 54
+         * for LSF long-type at 22.05..12 kHz and 72 for short at 8 kHz */
+        if (u->block_type == 2) *r1 = sr_idx == 8 ? 72 : 36;
+        else *r1 = sr_idx <= 2 ? 36 : sr_idx == 8 ? 108 : 54;
+        *r2 = 576;
     } else {
         int b1 = u->region0_count + 1, b2 = u->region0_count + u->region1_count + 2;
         if (b2 > 22) b2 = 22;
@@ -125,10 +141,23 @@ static void region_ends(const gunit *u, int sr_idx, int *r1, int *r2) {
 }
 
 /* Scalefactor bits (part 2) in the FFmpeg/our sf[] layout. */
+/* canonical sf index of the i-th coded LSF scalefactor */
+static int lsf_sf_index(const gunit *u, int i) {
+    return (u->window_switching && u->block_type == 2 && u->mixed && i >= 6) ? i + 2 : i;
+}
+
 static int part2_bits(const gunit *u, const uint8_t *sf_gr0, bw_t *w) {
-    int slen1 = MP3D_SLEN[0][u->scalefac_compress], slen2 = MP3D_SLEN[1][u->scalefac_compress];
+    int slen1 = MP3D_SLEN[0][u->scalefac_compress & 15], slen2 = MP3D_SLEN[1][u->scalefac_compress & 15];
     int bits = 0, j = 0;
     (void)sf_gr0;
+    if (u->lsf) {
+        for (int k = 0; k < 4; k++)
+            for (int i = 0; i < u->nsf[k]; i++, j++) {
+                bits += u->slen[k];
+                if (w && u->slen[k]) bw_put(w, u->sf[lsf_sf_index(u, j)], u->slen[k]);
+            }
+        return bits;
+    }
     if (u->window_switching && u->block_type == 2) {
         int n = u->mixed ? 17 : 18;
         for (int i = 0; i < n; i++) { bits += slen1; if (w) bw_put(w, u->sf[j], slen1); j++; }
@@ -222,9 +251,57 @@ static void fill_spectrum(rng_t *r, gunit *u, int sr_idx, double scale, int is_b
      * rzero, so keep it -- it is legal syntax and exercises the decoder. */
 }
 
+/* FFmpeg lsf_sf_expand: slen[] from a scalefac_compress sub-range */
+static void lsf_expand(int *slen, int sf, int n1, int n2, int n3) {
+    if (n3) { slen[3] = sf % n3; sf /= n3; } else slen[3] = 0;
+    if (n2) { slen[2] = sf % n2; sf /= n2; } else slen[2] = 0;
+    slen[1] = sf % n1;
+    slen[0] = sf / n1;
+}
+
+/* LSF scalefac_compress -> slen[4], nr_of_sfb[4], preflag (ISO 13818-3
+ * 2.4.3.2; FFmpeg mp_decode_layer3) */
+static void lsf_groups(gunit *u) {
+    int sf = u->scalefac_compress, t2;
+    int tindex = u->window_switching && u->block_type == 2 ? (u->mixed ? 2 : 1) : 0;
+    u->preflag = 0;
+    if (u->is_right) {
+        sf >>= 1;
+        if (sf < 180) { lsf_expand(u->slen, sf, 6, 6, 0); t2 = 3; }
+        else if (sf < 244) { lsf_expand(u->slen, sf - 180, 4, 4, 0); t2 = 4; }
+        else { lsf_expand(u->slen, sf - 244, 3, 0, 0); t2 = 5; }
+    } else {
+        if (sf < 400) { lsf_expand(u->slen, sf, 5, 4, 4); t2 = 0; }
+        else if (sf < 500) { lsf_expand(u->slen, sf - 400, 5, 4, 0); t2 = 1; }
+        else { lsf_expand(u->slen, sf - 500, 3, 0, 0); t2 = 2; u->preflag = 1; }
+    }
+    for (int k = 0; k < 4; k++) u->nsf[k] = MP3D_LSF_NSF[t2][tindex][k];
+}
+
+/* slen of canonical sf index j of an LSF unit (0 if not coded) */
+static int lsf_slen_at(const gunit *u, int j) {
+    int i = 0;
+    for (int k = 0; k < 4; k++)
+        for (int n = 0; n < u->nsf[k]; n++, i++)
+            if (lsf_sf_index(u, i) == j) return u->slen[k];
+    return 0;
+}
+
 static void fill_scalefactors(rng_t *r, gunit *u, const gunit *gr0, int is_bound_sfb_long, int is_ch1,
                               int sr_idx) {
     (void)sr_idx;
+    if (u->lsf) {
+        /* 9-bit scalefac_compress; the IS right channel's carries
+         * intensity_scale in bit 0 and its range selects the IS slen table */
+        u->scalefac_compress = rng_int(r, 0, 511);
+        lsf_groups(u);
+        memset(u->sf, 0, sizeof(u->sf));
+        int i = 0;
+        for (int k = 0; k < 4; k++)
+            for (int n = 0; n < u->nsf[k]; n++, i++)
+                u->sf[lsf_sf_index(u, i)] = (uint8_t)(u->slen[k] ? rng_int(r, 0, (1 << u->slen[k]) - 1) : 0);
+        return;
+    }
     u->scalefac_compress = rng_int(r, 0, 15);
     int slen1 = MP3D_SLEN[0][u->scalefac_compress], slen2 = MP3D_SLEN[1][u->scalefac_compress];
     memset(u->sf, 0, sizeof(u->sf));
@@ -258,8 +335,12 @@ static uint16_t crc16_bits(uint16_t crc, const uint8_t *p, int nbytes) {
     return crc;
 }
 
+/* frame bytes: 144000 * kbps / Hz (MPEG-1), 72000 * kbps / Hz (LSF) */
+static int frame_num(int br_idx, int sr_idx) {
+    return sr_idx < 3 ? 144000 * MP3D_BITRATE_L3[br_idx] : 72000 * MP3D_BITRATE_L3_LSF[br_idx];
+}
 static int frame_len(int br_idx, int sr_idx, int pad) {
-    return 144000 * MP3D_BITRATE_L3[br_idx] / (int)MP3D_SAMPLE_RATE[sr_idx] + pad;
+    return frame_num(br_idx, sr_idx) / (int)MP3D_SAMPLE_RATE[sr_idx] + pad;
 }
 
 /* Pick IS boundary (first line of the intensity region of channel 1) on a
@@ -270,7 +351,7 @@ static int pick_is_bound(rng_t *r, const gunit *u, int sr_idx) {
          * window-grouped bitstream order */
         int b0 = u->mixed ? 3 : 0;
         int band = rng_int(r, b0 + 1, 12);
-        int line = u->mixed ? 36 : 0;
+        int line = u->mixed ? (sr_idx == 8 ? 72 : 36) : 0;
         for (int i = b0; i < band; i++) line += 3 * MP3D_SFB_SHORT_WIDTH[sr_idx][i];
         return line;
     }
@@ -282,6 +363,27 @@ static int pick_is_bound(rng_t *r, const gunit *u, int sr_idx) {
 
 /* Set the scalefactors of the IS bands of channel 1 to random is_pos. */
 static void set_is_positions(rng_t *r, gunit *u, int sr_idx, int bound) {
+    if (u->lsf) {
+        /* LSF: any coded value; FFmpeg treats is_pos >= 16 as "not IS" */
+        if (u->window_switching && u->block_type == 2) {
+            int b0 = u->mixed ? 3 : 0, line = u->mixed ? (sr_idx == 8 ? 72 : 36) : 0;
+            for (int i = b0; i < 12; i++) {
+                for (int w = 0; w < 3; w++) {
+                    int j = u->mixed ? 8 + 3 * (i - 3) + w : 3 * i + w, sl = lsf_slen_at(u, j);
+                    if (line >= bound && sl) u->sf[j] = (uint8_t)rng_int(r, 0, (1 << sl) - 1);
+                }
+                line += 3 * MP3D_SFB_SHORT_WIDTH[sr_idx][i];
+            }
+        } else {
+            int line = 0;
+            for (int i = 0; i < 21; i++) {
+                int sl = lsf_slen_at(u, i);
+                if (line >= bound && sl) u->sf[i] = (uint8_t)rng_int(r, 0, (1 << sl) - 1);
+                line += MP3D_SFB_LONG_WIDTH[sr_idx][i];
+            }
+        }
+        return;
+    }
     int slen1 = MP3D_SLEN[0][u->scalefac_compress], slen2 = MP3D_SLEN[1][u->scalefac_compress];
     if (u->window_switching && u->block_type == 2) {
         int b0 = u->mixed ? 3 : 0, line = u->mixed ? 36 : 0, j = u->mixed ? 8 : 0;
@@ -318,12 +420,14 @@ GEN_API long mp3gen_stream(const gen_cfg *cfg, uint64_t seed, int n_frames, uint
                            uint32_t *frame_off, gen_truth *truth) {
     rng_t R;
     rng_seed(&R, seed);
-    int sr_idx = cfg->sr_idx >= 0 ? cfg->sr_idx : rng_int(&R, 0, 2);
+    int sr_idx = cfg->sr_idx >= 0 ? cfg->sr_idx : cfg->sr_idx == -2 ? rng_int(&R, 3, 8) : rng_int(&R, 0, 2);
     int mode = cfg->mode >= 0 ? cfg->mode : rng_int(&R, 0, 3);
     int nch = mode == 3 ? 1 : 2;
     int crc = rng_int(&R, 0, 99) < cfg->crc_pct;
-    int side_bytes = nch == 1 ? 17 : 32;
-    int max_res = cfg->max_reservoir > 511 ? 511 : cfg->max_reservoir;
+    const int lsf = sr_idx >= 3, ngr = lsf ? 1 : 2;
+    int side_bytes = lsf ? (nch == 1 ? 9 : 17) : (nch == 1 ? 17 : 32);
+    const int res_cap = lsf ? 255 : 511; /* main_data_begin: 8 / 9 bits */
+    int max_res = cfg->max_reservoir > res_cap ? res_cap : cfg->max_reservoir;
     /* main-data byte stream: payloads concatenated, pre-filled with noise
      * (ancillary bytes must never be read by a correct decoder) */
     long md_cap = (long)n_frames * 1441 + 4096;
@@ -348,7 +452,7 @@ GEN_API long mp3gen_stream(const gen_cfg *cfg, uint64_t seed, int n_frames, uint
         int br = cfg->bitrate_idx > 0 ? cfg->bitrate_idx : rng_int(&R, 1, 14);
         /* ISO padding: keep the average frame length exact */
         int hz = (int)MP3D_SAMPLE_RATE[sr_idx];
-        int rem = (144000 * MP3D_BITRATE_L3[br]) % hz;
+        int rem = frame_num(br, sr_idx) % hz;
         pad_acc += rem;
         int pad = 0;
         if (pad_acc >= hz) { pad = 1; pad_acc -= hz; }
@@ -359,8 +463,8 @@ GEN_API long mp3gen_stream(const gen_cfg *cfg, uint64_t seed, int n_frames, uint
         flen[f] = fb; fbr[f] = br; fpad[f] = pad; fmext[f] = mext; fmd[f] = md_pos;
 
         /* block types for the two granules (shared by channels) */
-        int bts[2], mixeds[2];
-        for (int gr = 0; gr < 2; gr++) {
+        int bts[2] = {0, 0}, mixeds[2] = {0, 0};
+        for (int gr = 0; gr < ngr; gr++) {
             int mx = 0;
             if (bt_state == 0) {
                 if (rng_int(&R, 0, 99) < cfg->short_pct) bt_state = 1;
@@ -384,10 +488,12 @@ GEN_API long mp3gen_stream(const gen_cfg *cfg, uint64_t seed, int n_frames, uint
         uint8_t unit_bytes_ok = 0;
         for (int attempt = 0; attempt < 40 && !unit_bytes_ok; attempt++) {
             total_bits = 0;
-            for (int gr = 0; gr < 2; gr++)
+            for (int gr = 0; gr < ngr; gr++)
                 for (int ch = 0; ch < nch; ch++) {
                     gunit *u = &U[gr][ch];
                     memset(u, 0, sizeof(*u));
+                    u->lsf = lsf;
+                    u->is_right = lsf && mode == 1 && (mext & 1) && ch == 1;
                     u->block_type = bts[gr];
                     u->window_switching = bts[gr] != 0;
                     u->mixed = bts[gr] == 2 ? mixeds[gr] : 0;
@@ -423,7 +529,7 @@ GEN_API long mp3gen_stream(const gen_cfg *cfg, uint64_t seed, int n_frames, uint
             int hi = R_avail < max_res ? R_avail : max_res;
             if (hi > used - 1) hi = used - 1;
             int bad = 0;
-            for (int gr = 0; gr < 2; gr++)
+            for (int gr = 0; gr < ngr; gr++)
                 for (int ch = 0; ch < nch; ch++) if (U[gr][ch].part2_3_length > 4095) bad = 1;
             if (!bad && used >= 1 && lo <= hi && total_bits <= target + 400) unit_bytes_ok = 1;
             else {
@@ -434,10 +540,13 @@ GEN_API long mp3gen_stream(const gen_cfg *cfg, uint64_t seed, int n_frames, uint
         }
         if (!unit_bytes_ok) { /* fall back to silence units */
             total_bits = 0;
-            for (int gr = 0; gr < 2; gr++)
+            for (int gr = 0; gr < ngr; gr++)
                 for (int ch = 0; ch < nch; ch++) {
                     memset(&U[gr][ch], 0, sizeof(gunit));
                     U[gr][ch].global_gain = 150;
+                    U[gr][ch].lsf = lsf;
+                    U[gr][ch].is_right = lsf && mode == 1 && (mext & 1) && ch == 1;
+                    if (lsf) lsf_groups(&U[gr][ch]);
                 }
         }
         int used = (total_bits + 7) / 8;
@@ -449,7 +558,7 @@ GEN_API long mp3gen_stream(const gen_cfg *cfg, uint64_t seed, int n_frames, uint
         if (mdb > R_avail) mdb = R_avail < lo ? lo : R_avail; /* never reached for valid input */
         /* write main data */
         bw_t w = {md, md_cap * 8, (md_pos - mdb) * 8};
-        for (int gr = 0; gr < 2; gr++)
+        for (int gr = 0; gr < ngr; gr++)
             for (int ch = 0; ch < nch; ch++) {
                 long p0 = w.pos;
                 unit_bits(&U[gr][ch], sr_idx, U[0][ch].sf, &w);
@@ -463,16 +572,21 @@ GEN_API long mp3gen_stream(const gen_cfg *cfg, uint64_t seed, int n_frames, uint
         uint8_t *sp = side[f];
         memset(sp, 0, 32);
         bw_t sw = {sp, side_bytes * 8, 0};
-        bw_put(&sw, (uint32_t)mdb, 9);
-        bw_put(&sw, 0, nch == 1 ? 5 : 3);
-        for (int ch = 0; ch < nch; ch++) bw_put(&sw, (uint32_t)U[1][ch].scfsi, 4);
-        for (int gr = 0; gr < 2; gr++)
+        if (lsf) {
+            bw_put(&sw, (uint32_t)mdb, 8);
+            bw_put(&sw, 0, nch == 1 ? 1 : 2);
+        } else {
+            bw_put(&sw, (uint32_t)mdb, 9);
+            bw_put(&sw, 0, nch == 1 ? 5 : 3);
+            for (int ch = 0; ch < nch; ch++) bw_put(&sw, (uint32_t)U[1][ch].scfsi, 4);
+        }
+        for (int gr = 0; gr < ngr; gr++)
             for (int ch = 0; ch < nch; ch++) {
                 gunit *u = &U[gr][ch];
                 bw_put(&sw, (uint32_t)u->part2_3_length, 12);
                 bw_put(&sw, (uint32_t)u->big_values, 9);
                 bw_put(&sw, (uint32_t)u->global_gain, 8);
-                bw_put(&sw, (uint32_t)u->scalefac_compress, 4);
+                bw_put(&sw, (uint32_t)u->scalefac_compress, lsf ? 9 : 4);
                 bw_put(&sw, (uint32_t)u->window_switching, 1);
                 if (u->window_switching) {
                     bw_put(&sw, (uint32_t)u->block_type, 2);
@@ -485,7 +599,7 @@ GEN_API long mp3gen_stream(const gen_cfg *cfg, uint64_t seed, int n_frames, uint
                     bw_put(&sw, (uint32_t)u->region0_count, 4);
                     bw_put(&sw, (uint32_t)u->region1_count, 3);
                 }
-                bw_put(&sw, (uint32_t)u->preflag, 1);
+                if (!lsf) bw_put(&sw, (uint32_t)u->preflag, 1); /* LSF: implied by scalefac_compress */
                 bw_put(&sw, (uint32_t)u->scalefac_scale, 1);
                 bw_put(&sw, (uint32_t)u->count1table_select, 1);
                 if (truth) {
@@ -501,7 +615,8 @@ GEN_API long mp3gen_stream(const gen_cfg *cfg, uint64_t seed, int n_frames, uint
                 }
             }
         if (truth && nch == 1)
-            for (int gr = 0; gr < 2; gr++) memset(&truth[((long)f * 2 + gr) * 2 + 1], 0, sizeof(gen_truth));
+            for (int gr = 0; gr < ngr; gr++) memset(&truth[((long)f * 2 + gr) * 2 + 1], 0, sizeof(gen_truth));
+        if (truth && lsf) memset(&truth[((long)f * 2 + 1) * 2], 0, 2 * sizeof(gen_truth)); /* no granule 1 */
         md_pos += plen;
     }
     /* assemble frames */
@@ -511,9 +626,11 @@ GEN_API long mp3gen_stream(const gen_cfg *cfg, uint64_t seed, int n_frames, uint
         if (o + fb > cap) { o = -1; break; }
         uint8_t *p = out + o;
         if (frame_off) frame_off[f] = (uint32_t)o;
+        /* version bits: 3 MPEG-1, 2 MPEG-2, 0 MPEG-2.5; layer bits 01 = III */
+        const int ver = sr_idx < 3 ? 3 : sr_idx < 6 ? 2 : 0;
         p[0] = 0xFF;
-        p[1] = (uint8_t)(0xFA | (crc ? 0 : 1));
-        p[2] = (uint8_t)((fbr[f] << 4) | (sr_idx << 2) | (fpad[f] << 1));
+        p[1] = (uint8_t)(0xE0 | (ver << 3) | 0x2 | (crc ? 0 : 1));
+        p[2] = (uint8_t)((fbr[f] << 4) | ((sr_idx % 3) << 2) | (fpad[f] << 1));
         p[3] = (uint8_t)((mode << 6) | (fmext[f] << 4) | 0x4 /* original */);
         int hdr = 4;
         if (crc) {
@@ -538,8 +655,10 @@ GEN_API int mp3gen_cfg_size(void) { return (int)sizeof(gen_cfg); }
 /* Upper bound on bytes for n_frames of a configuration. */
 GEN_API long mp3gen_max_bytes(const gen_cfg *cfg, int n_frames) {
     int maxfb = 0;
-    for (int sr = 0; sr < 3; sr++) {
+    for (int sr = 0; sr < 9; sr++) {
         if (cfg->sr_idx >= 0 && sr != cfg->sr_idx) continue;
+        if (cfg->sr_idx == -1 && sr >= 3) continue;
+        if (cfg->sr_idx == -2 && sr < 3) continue;
         for (int br = 1; br <= 14; br++) {
             if (cfg->bitrate_idx > 0 && br != cfg->bitrate_idx) continue;
             int fb = frame_len(br, sr, 1);

@@ -32,26 +32,33 @@
 typedef struct {
     int protection_absent, bitrate_idx, sr_idx, padding, mode, mode_ext;
     int nch, kbps, hz, frame_bytes, side_bytes, crc_bytes;
+    int lsf, ngr; /* MPEG-2 / 2.5 low sampling frequency: 1 granule / frame */
 } orc_hdr;
 
-/* Returns frame length in bytes, or -1 if `p` is not an MPEG-1 Layer III
- * header with a non-free-format bitrate. */
+/* Returns frame length in bytes, or -1 if `p` is not a Layer III header
+ * (MPEG-1, MPEG-2 or MPEG-2.5; ISO 11172-3 2.4.2.3, 13818-3 2.4.2.3) with
+ * a non-free-format bitrate.  sr_idx = sampling_frequency + 3 (MPEG-2) or
+ * + 6 (MPEG-2.5), FFmpeg's sample_rate_index. */
 ORC_API int orc_parse_header(const uint8_t *p, orc_hdr *h) {
-    if (p[0] != 0xFF || (p[1] & 0xFE) != 0xFA) return -1; /* sync, ID=1, layer III */
+    if (p[0] != 0xFF || (p[1] & 0xE0) != 0xE0) return -1; /* 11-bit sync */
+    const int ver = (p[1] >> 3) & 3, layer = (p[1] >> 1) & 3;
+    if (ver == 1 || layer != 1) return -1; /* reserved version; Layer III only */
     int bi = p[2] >> 4, si = (p[2] >> 2) & 3;
     if (bi == 0 || bi == 15 || si == 3) return -1;
+    h->lsf = ver != 3;
+    h->ngr = h->lsf ? 1 : 2;
     h->protection_absent = p[1] & 1;
     h->bitrate_idx = bi;
-    h->sr_idx = si;
+    h->sr_idx = si + (ver == 3 ? 0 : ver == 2 ? 3 : 6);
     h->padding = (p[2] >> 1) & 1;
     h->mode = p[3] >> 6;
     h->mode_ext = (p[3] >> 4) & 3;
     h->nch = h->mode == 3 ? 1 : 2;
-    h->kbps = MP3D_BITRATE_L3[bi];
-    h->hz = (int)MP3D_SAMPLE_RATE[si];
-    h->frame_bytes = 144000 * h->kbps / h->hz + h->padding;
+    h->kbps = h->lsf ? MP3D_BITRATE_L3_LSF[bi] : MP3D_BITRATE_L3[bi];
+    h->hz = (int)MP3D_SAMPLE_RATE[h->sr_idx];
+    h->frame_bytes = (h->lsf ? 72000 : 144000) * h->kbps / h->hz + h->padding;
     h->crc_bytes = h->protection_absent ? 0 : 2;
-    h->side_bytes = h->nch == 1 ? 17 : 32;
+    h->side_bytes = h->lsf ? (h->nch == 1 ? 9 : 17) : (h->nch == 1 ? 17 : 32);
     return h->frame_bytes;
 }
 
@@ -83,6 +90,7 @@ typedef struct {
     int window_switching, block_type, mixed, table_select[3], subblock_gain[3];
     int region0_count, region1_count, preflag, scalefac_scale, count1table_select;
     int scfsi;
+    int lsf, is_right; /* LSF unit; right channel of an intensity-stereo LSF frame */
 } orc_gr;
 
 typedef struct {
@@ -90,21 +98,29 @@ typedef struct {
     orc_gr gr[2][2]; /* [granule][channel] */
 } orc_side;
 
-static void orc_parse_side(const uint8_t *p, int nch, orc_side *s) {
-    orc_bits b = {p, (nch == 1 ? 17 : 32) * 8, 0};
-    s->main_data_begin = (int)orc_get(&b, 9);
-    orc_get(&b, nch == 1 ? 5 : 3); /* private bits */
+/* Side info; LSF (13818-3 2.4.1.7): 8-bit main_data_begin, 1 / 2 private
+ * bits, no scfsi, one granule, 9-bit scalefac_compress, no preflag bit
+ * (implied by scalefac_compress, set in orc_read_scalefactors). */
+static void orc_parse_side(const uint8_t *p, const orc_hdr *h, orc_side *s) {
+    const int nch = h->nch, lsf = h->lsf;
+    orc_bits b = {p, h->side_bytes * 8, 0};
+    memset(s->gr, 0, sizeof(s->gr));
+    s->main_data_begin = (int)orc_get(&b, lsf ? 8 : 9);
+    orc_get(&b, lsf ? nch : (nch == 1 ? 5 : 3)); /* private bits */
     int scfsi[2] = {0, 0};
-    for (int ch = 0; ch < nch; ch++) scfsi[ch] = (int)orc_get(&b, 4);
-    for (int gr = 0; gr < 2; gr++)
+    if (!lsf)
+        for (int ch = 0; ch < nch; ch++) scfsi[ch] = (int)orc_get(&b, 4);
+    for (int gr = 0; gr < h->ngr; gr++)
         for (int ch = 0; ch < nch; ch++) {
             orc_gr *g = &s->gr[gr][ch];
             memset(g, 0, sizeof(*g));
+            g->lsf = lsf;
+            g->is_right = lsf && h->mode == 1 && (h->mode_ext & 1) && ch == 1;
             g->scfsi = gr == 1 ? scfsi[ch] : 0;
             g->part2_3_length = (int)orc_get(&b, 12);
             g->big_values = (int)orc_get(&b, 9);
             g->global_gain = (int)orc_get(&b, 8);
-            g->scalefac_compress = (int)orc_get(&b, 4);
+            g->scalefac_compress = (int)orc_get(&b, lsf ? 9 : 4);
             g->window_switching = (int)orc_get(&b, 1);
             if (g->window_switching) {
                 g->block_type = (int)orc_get(&b, 2);
@@ -117,7 +133,7 @@ static void orc_parse_side(const uint8_t *p, int nch, orc_side *s) {
                 g->region0_count = (int)orc_get(&b, 4);
                 g->region1_count = (int)orc_get(&b, 3);
             }
-            g->preflag = (int)orc_get(&b, 1);
+            g->preflag = lsf ? 0 : (int)orc_get(&b, 1);
             g->scalefac_scale = (int)orc_get(&b, 1);
             g->count1table_select = (int)orc_get(&b, 1);
         }
@@ -238,7 +254,43 @@ ORC_API int orc_state_bytes(void) { return (int)sizeof(orc_dec); }
 /*   short: sf[3*b + w], b = 0..11 (+3 zeros for band 12)                     */
 /*   mixed: sf[0..7] long bands 0..7, then sf[8 + 3*(b-3) + w], b = 3..11     */
 /* ------------------------------------------------------------------------ */
-static void orc_read_scalefactors(orc_bits *b, const orc_gr *g, const uint8_t *sf_gr0, uint8_t *sf) {
+/* FFmpeg lsf_sf_expand */
+static void orc_lsf_expand(int *slen, int sf, int n1, int n2, int n3) {
+    if (n3) { slen[3] = sf % n3; sf /= n3; } else slen[3] = 0;
+    if (n2) { slen[2] = sf % n2; sf /= n2; } else slen[2] = 0;
+    slen[1] = sf % n1;
+    slen[0] = sf / n1;
+}
+
+/* LSF scalefactors (13818-3 2.4.3.2, FFmpeg mp_decode_layer3): slen[4] and
+ * nr_of_sfb from the 9-bit scalefac_compress (intensity right channel: its
+ * half, other tables); preflag = scalefac_compress >= 500.  Read in coding
+ * order, stored in the canonical layout (mixed: short bands from sf[8]). */
+static void orc_read_scalefactors_lsf(orc_bits *b, orc_gr *g, uint8_t *sf) {
+    int slen[4], t2, sfc = g->scalefac_compress;
+    const int tindex = g->window_switching && g->block_type == 2 ? (g->mixed ? 2 : 1) : 0;
+    if (g->is_right) {
+        sfc >>= 1;
+        if (sfc < 180) { orc_lsf_expand(slen, sfc, 6, 6, 0); t2 = 3; }
+        else if (sfc < 244) { orc_lsf_expand(slen, sfc - 180, 4, 4, 0); t2 = 4; }
+        else { orc_lsf_expand(slen, sfc - 244, 3, 0, 0); t2 = 5; }
+    } else {
+        if (sfc < 400) { orc_lsf_expand(slen, sfc, 5, 4, 4); t2 = 0; }
+        else if (sfc < 500) { orc_lsf_expand(slen, sfc - 400, 5, 4, 0); t2 = 1; }
+        else { orc_lsf_expand(slen, sfc - 500, 3, 0, 0); t2 = 2; g->preflag = 1; }
+    }
+    memset(sf, 0, 40);
+    int j = 0;
+    for (int k = 0; k < 4; k++)
+        for (int i = 0; i < MP3D_LSF_NSF[t2][tindex][k]; i++, j++)
+            sf[tindex == 2 && j >= 6 ? j + 2 : j] = (uint8_t)orc_get(b, slen[k]);
+}
+
+static void orc_read_scalefactors(orc_bits *b, orc_gr *g, const uint8_t *sf_gr0, uint8_t *sf) {
+    if (g->lsf) {
+        orc_read_scalefactors_lsf(b, g, sf);
+        return;
+    }
     int slen1 = MP3D_SLEN[0][g->scalefac_compress], slen2 = MP3D_SLEN[1][g->scalefac_compress];
     memset(sf, 0, 40);
     int j = 0;
@@ -266,7 +318,10 @@ static long orc_huffman(orc_bits *b, const orc_gr *g, int sr_idx, long end_bit, 
     int bv2 = g->big_values * 2;
     int r1, r2; /* region ends (lines) */
     if (g->window_switching) {
-        r1 = 36;
+        /* FFmpeg: 36 lines; LSF long-type units 54 (not at 8 kHz); short
+         * units at MPEG-2.5 8 kHz 72 */
+        if (g->block_type == 2) r1 = sr_idx == 8 ? 72 : 36;
+        else r1 = sr_idx <= 2 ? 36 : sr_idx == 8 ? 108 : 54;
         r2 = 576;
     } else {
         int b1 = g->region0_count + 1, b2 = g->region0_count + g->region1_count + 2;
@@ -329,7 +384,7 @@ static void orc_requant(const orc_gr *g, int sr_idx, const uint8_t *sf, const in
     int shift = g->scalefac_scale + 1;
     int long_end, short_start;
     if (g->window_switching && g->block_type == 2) {
-        long_end = g->mixed ? 8 : 0;
+        long_end = g->mixed ? (g->lsf ? 6 : 8) : 0; /* FFmpeg: 6 long bands in LSF mixed blocks */
         short_start = g->mixed ? 3 : 0;
     } else {
         long_end = 22;
@@ -345,6 +400,7 @@ static void orc_requant(const orc_gr *g, int sr_idx, const uint8_t *sf, const in
             xr[line] = v == 0 ? 0.0 : (v < 0 ? -g_pow43[-v] : g_pow43[v]) * s;
         }
     }
+    if (g->mixed && long_end < 22) j = 8; /* canonical layout: short bands from sf[8] */
     for (int i = short_start; i < 13 && long_end < 22; i++) {
         for (int w = 0; w < 3; w++) {
             int q = gain - (g->subblock_gain[w] << 3) - (sf[j++] << shift);
@@ -359,6 +415,26 @@ static void orc_requant(const orc_gr *g, int sr_idx, const uint8_t *sf, const in
 
 /* Joint stereo, ISO 2.4.3.4 (M/S and MPEG-1 intensity), in bitstream
  * (pre-reorder) order, walking bands from the top as FFmpeg compute_stereo. */
+/* Intensity ratios of one is_pos: MPEG-1 tan(is_pos pi / 12) (legal below 7);
+ * LSF (13818-3 2.4.3.2, FFmpeg is_table_lsf) i0 = 2^(-1/4) (scalefac_compress
+ * bit 0 = 0) or 2^(-1/2): odd is_pos -> (i0^((is_pos + 1) / 2), 1), even ->
+ * (1, i0^(is_pos / 2)); FFmpeg treats is_pos >= 16 as "no intensity". */
+static int orc_is_ratio(const orc_gr *g1, int p, double *v1, double *v2) {
+    if (!g1->lsf) {
+        if (p >= 7) return 0;
+        double t = tan(p * M_PI / 12.0);
+        *v1 = t / (1.0 + t);
+        *v2 = 1.0 / (1.0 + t);
+        return 1;
+    }
+    if (p >= 16) return 0;
+    const int j = g1->scalefac_compress & 1;
+    const double f = pow(2.0, -(j + 1) * ((p + 1) >> 1) / 4.0);
+    *v1 = (p & 1) ? f : 1.0;
+    *v2 = (p & 1) ? 1.0 : f;
+    return 1;
+}
+
 static void orc_stereo(const orc_gr *g1, int sr_idx, int mode_ext, const uint8_t *sf1, double *l, double *r) {
     const double isq = 1.0 / sqrt(2.0);
     if (!(mode_ext & 1)) {
@@ -372,7 +448,7 @@ static void orc_stereo(const orc_gr *g1, int sr_idx, int mode_ext, const uint8_t
     }
     int long_end, short_start;
     if (g1->window_switching && g1->block_type == 2) {
-        long_end = g1->mixed ? 8 : 0;
+        long_end = g1->mixed ? (g1->lsf ? 6 : 8) : 0;
         short_start = g1->mixed ? 3 : 0;
     } else {
         long_end = 22;
@@ -380,21 +456,22 @@ static void orc_stereo(const orc_gr *g1, int sr_idx, int mode_ext, const uint8_t
     }
     int pos = 576;
     int nz_short[3] = {0, 0, 0};
-    int k = (13 - short_start) * 3 + long_end - 3;
+    /* FFmpeg's index walk; sf1 is in the canonical layout, where a mixed
+     * block's short bands start at 8 whatever its long_end */
+    int k = (13 - short_start) * 3 + (g1->mixed && long_end < 22 ? 8 : long_end) - 3;
     for (int i = 12; i >= short_start; i--) {
         if (i != 11) k -= 3;
         int len = MP3D_SFB_SHORT_WIDTH[sr_idx][i];
         for (int w = 2; w >= 0; w--) {
             pos -= len;
             int do_is = 0;
+            double v1 = 0, v2 = 0;
             if (!nz_short[w]) {
                 for (int j = 0; j < len; j++)
                     if (r[pos + j] != 0.0) { nz_short[w] = 1; break; }
-                if (!nz_short[w] && sf1[k + w] < 7) do_is = 1;
+                if (!nz_short[w]) do_is = orc_is_ratio(g1, sf1[k + w], &v1, &v2);
             }
             if (do_is) {
-                double t = tan(sf1[k + w] * M_PI / 12.0);
-                double v1 = t / (1.0 + t), v2 = 1.0 / (1.0 + t);
                 for (int j = 0; j < len; j++) {
                     double x = l[pos + j];
                     l[pos + j] = x * v1;
@@ -414,16 +491,14 @@ static void orc_stereo(const orc_gr *g1, int sr_idx, int mode_ext, const uint8_t
         int len = MP3D_SFB_LONG_WIDTH[sr_idx][i];
         pos -= len;
         int do_is = 0;
+        double v1 = 0, v2 = 0;
         if (!nz) {
             for (int j = 0; j < len; j++)
                 if (r[pos + j] != 0.0) { nz = 1; break; }
             int kk = i == 21 ? 20 : i;
-            if (!nz && sf1[kk] < 7) do_is = 1;
+            if (!nz) do_is = orc_is_ratio(g1, sf1[kk], &v1, &v2);
         }
         if (do_is) {
-            int kk = i == 21 ? 20 : i;
-            double t = tan(sf1[kk] * M_PI / 12.0);
-            double v1 = t / (1.0 + t), v2 = 1.0 / (1.0 + t);
             for (int j = 0; j < len; j++) {
                 double x = l[pos + j];
                 l[pos + j] = x * v1;
@@ -444,7 +519,7 @@ static void orc_stereo(const orc_gr *g1, int sr_idx, int mode_ext, const uint8_t
 static void orc_reorder(int block_type, int mixed, int sr_idx, double *xr) {
     if (block_type != 2) return;
     double tmp[576];
-    int start = mixed ? 36 : 0, b0 = mixed ? 3 : 0;
+    int start = mixed ? (sr_idx == 8 ? 72 : 36) : 0, b0 = mixed ? 3 : 0; /* FFmpeg reorder_block */
     int p = start;
     for (int i = b0; i < 13; i++) {
         int len = MP3D_SFB_SHORT_WIDTH[sr_idx][i];
@@ -532,7 +607,8 @@ static void orc_granule_to_pcm(orc_dec *d, int ch, int block_type, int mixed, in
 /* ------------------------------------------------------------------------ */
 /* One frame.  buf points at the sync word; bytes >= frame length.           */
 /* pcm: planar double [2][1152] (may be NULL).  Returns samples/channel     */
-/* (1152), 0 for a frame that produced no audio, <0 on error.               */
+/* (1152, or 576 for LSF), 0 for a frame that produced no audio, <0 on     */
+/* error.                                                                   */
 /* ------------------------------------------------------------------------ */
 ORC_API int orc_decode_frame_f64(orc_dec *d, const uint8_t *buf, int bytes, double *pcm, orc_info *info) {
     orc_hdr h;
@@ -549,8 +625,8 @@ ORC_API int orc_decode_frame_f64(orc_dec *d, const uint8_t *buf, int bytes, doub
     d->hdr = h;
     const uint8_t *side = buf + 4 + h.crc_bytes;
     orc_side *s = &d->side;
-    orc_parse_side(side, h.nch, s);
-    for (int gr = 0; gr < 2; gr++)
+    orc_parse_side(side, &h, s);
+    for (int gr = 0; gr < h.ngr; gr++)
         for (int ch = 0; ch < h.nch; ch++)
             if (s->gr[gr][ch].big_values > 288) {
                 /* dropped; FFmpeg mp_decode_frame then keeps
@@ -582,7 +658,7 @@ ORC_API int orc_decode_frame_f64(orc_dec *d, const uint8_t *buf, int bytes, doub
         /* reservoir underflow: FFmpeg skips whole granules until the missing
          * bytes are covered (mp_decode_layer3), zero spectra meanwhile. */
         long bits = (long)avail * 8;
-        while (gr0 < 2 && (bits >> 3) < mdb) {
+        while (gr0 < h.ngr && (bits >> 3) < mdb) {
             for (int ch = 0; ch < h.nch; ch++) bits += s->gr[gr0][ch].part2_3_length;
             gr0++;
         }
@@ -593,10 +669,11 @@ ORC_API int orc_decode_frame_f64(orc_dec *d, const uint8_t *buf, int bytes, doub
     double pcm_local[2][1152];
     memset(d->is, 0, sizeof(d->is));
     memset(d->sf, 0, sizeof(d->sf));
+    memset(d->xr, 0, sizeof(d->xr));
     memset(d->used_bits, 0, sizeof(d->used_bits));
     int ms_only = h.mode == 1 && (h.mode_ext & 2) && !(h.mode_ext & 1);
     (void)ms_only;
-    for (int gr = 0; gr < 2; gr++) {
+    for (int gr = 0; gr < h.ngr; gr++) {
         for (int ch = 0; ch < h.nch; ch++) {
             orc_gr *g = &s->gr[gr][ch];
             if (gr < gr0) {
@@ -636,10 +713,10 @@ ORC_API int orc_decode_frame_f64(orc_dec *d, const uint8_t *buf, int bytes, doub
         d->hist_len = total;
     }
     if (pcm) {
-        for (int ch = 0; ch < h.nch; ch++) memcpy(pcm + 1152 * ch, pcm_local[ch], sizeof(double) * 1152);
+        for (int ch = 0; ch < h.nch; ch++) memcpy(pcm + 1152 * ch, pcm_local[ch], sizeof(double) * 576 * h.ngr);
     }
     d->frames++;
-    return 1152;
+    return 576 * h.ngr;
 }
 
 /* float32 planar output convenience wrapper */
@@ -649,7 +726,7 @@ ORC_API int orc_decode_frame(orc_dec *d, const uint8_t *buf, int bytes, float *p
     if (r > 0 && pcm) {
         int nch = d->hdr.nch;
         for (int ch = 0; ch < nch; ch++)
-            for (int i = 0; i < 1152; i++) pcm[1152 * ch + i] = (float)tmp[ch][i];
+            for (int i = 0; i < r; i++) pcm[1152 * ch + i] = (float)tmp[ch][i];
     }
     return r;
 }
@@ -660,8 +737,9 @@ ORC_API void orc_get_taps(const orc_dec *d, int16_t *is /*[2][2][576]*/, uint8_t
     if (sf) memcpy(sf, d->sf, sizeof(d->sf));
     if (xr)
         for (int i = 0; i < 2 * 2 * 576; i++) xr[i] = (float)((const double *)d->xr)[i];
-    if (side)
-        for (int gr = 0; gr < 2; gr++)
+    if (side) {
+        memset(side, 0, sizeof(int32_t) * 2 * 2 * 20);
+        for (int gr = 0; gr < d->hdr.ngr; gr++)
             for (int ch = 0; ch < 2; ch++) {
                 const orc_gr *g = &d->side.gr[gr][ch];
                 int32_t *o = side + (gr * 2 + ch) * 20;
@@ -674,6 +752,7 @@ ORC_API void orc_get_taps(const orc_dec *d, int16_t *is /*[2][2][576]*/, uint8_t
                 o[16] = d->used_bits[gr][ch];
                 o[17] = g->subblock_gain[0]; o[18] = g->subblock_gain[1]; o[19] = g->subblock_gain[2];
             }
+    }
 }
 
 /* ------------------------------------------------------------------------ */
@@ -701,11 +780,13 @@ ORC_API int orc_is_info_frame(const uint8_t *buf, long len) {
  * golden decoder): "Xing"/"Info" at 4 + side-info bytes,
  * BE32 flags, [frames] [bytes] [100-B TOC] [quality], 9-byte encoder
  * string, then 12 bytes on a BE24 delay << 12 | padding, honoured for LAME
- * / Lavf / Lavc.  out[0..4] = has_lame, enc_delay, enc_padding, frames
- * (-1 absent), skip_samples (delay + 529).  Returns 1 if a tag was found. */
+ * / Lavf / Lavc.  out[0..5] = has_lame, enc_delay, enc_padding, frames
+ * (-1 absent), skip_samples (delay + 529), samples per frame (1152 / 576
+ * LSF).  Returns 1 if a tag was found. */
 ORC_API int orc_parse_info_tag(const uint8_t *buf, long len, int *out) {
     long pos = orc_skip_id3v2(buf, len);
     out[0] = out[1] = out[2] = out[4] = 0;
+    out[5] = 1152;
     out[3] = -1;
     while (pos + 4 <= len) {
         orc_hdr h;
@@ -715,6 +796,7 @@ ORC_API int orc_parse_info_tag(const uint8_t *buf, long len, int *out) {
     if (pos + 4 > len || !orc_is_info_frame(buf + pos, len - pos)) return 0;
     orc_hdr h;
     const int fb = orc_parse_header(buf + pos, &h);
+    out[5] = 576 * h.ngr;
     const uint8_t *t = buf + pos + 4 + h.crc_bytes + h.side_bytes;
     const long n = fb - (4 + h.crc_bytes + h.side_bytes);
 #define BE32(o) ((uint32_t)t[o] << 24 | (uint32_t)t[(o) + 1] << 16 | (uint32_t)t[(o) + 2] << 8 | t[(o) + 3])
@@ -735,13 +817,16 @@ ORC_API int orc_parse_info_tag(const uint8_t *buf, long len, int *out) {
     return 1;
 }
 
-/* Decode a whole stream into planar float PCM [nch][max_frames*1152].
- * Skips an ID3v2 tag and a leading Xing/Info frame (as FFmpeg's demuxer).
- * Returns number of audio frames decoded. */
-ORC_API long orc_decode_stream(const uint8_t *buf, long len, float *pcm, long max_frames, int *nch_out, int *hz_out) {
+/* Decode a whole stream into planar float PCM [nch][max_frames*1152]
+ * (frames packed back to back: 1152 samples per MPEG-1 frame, 576 per LSF
+ * frame).  Skips an ID3v2 tag and a leading Xing/Info frame (as FFmpeg's
+ * demuxer).  Returns audio frames decoded; *samples_out = samples per
+ * channel written. */
+ORC_API long orc_decode_stream_n(const uint8_t *buf, long len, float *pcm, long max_frames, int *nch_out, int *hz_out,
+                                 long *samples_out) {
     orc_dec *d = orc_create();
     long pos = orc_skip_id3v2(buf, len);
-    long nf = 0;
+    long nf = 0, ns = 0;
     int first = 1;
     int nch = 0, hz = 0;
     float tmp[2][1152];
@@ -749,39 +834,39 @@ ORC_API long orc_decode_stream(const uint8_t *buf, long len, float *pcm, long ma
         orc_hdr h;
         int fb = orc_parse_header(buf + pos, &h);
         if (fb < 0) { pos++; continue; }
+        int r;
+        orc_info info;
         if (pos + fb > len) {
             /* a final frame cut short: FFmpeg still decodes it, the missing
              * bytes reading as zeros */
-            if (len - pos < 4 + h.crc_bytes + h.side_bytes || nf >= max_frames) break;
+            if (len - pos < 4 + h.crc_bytes + h.side_bytes) break;
             uint8_t *pad = (uint8_t *)calloc((size_t)fb, 1);
             memcpy(pad, buf + pos, (size_t)(len - pos));
-            orc_info info;
-            int r = orc_decode_frame(d, pad, fb, &tmp[0][0], &info);
+            r = orc_decode_frame(d, pad, fb, &tmp[0][0], &info);
             free(pad);
-            if (r > 0) {
-                nch = info.channels;
-                hz = info.hz;
-                for (int ch = 0; ch < nch; ch++)
-                    memcpy(pcm + (size_t)ch * max_frames * 1152 + nf * 1152, tmp[ch], sizeof(float) * 1152);
-                nf++;
-            }
-            break;
+            pos = len;
+        } else {
+            if (first && orc_is_info_frame(buf + pos, len - pos)) { pos += fb; first = 0; continue; }
+            r = orc_decode_frame(d, buf + pos, fb, &tmp[0][0], &info);
+            pos += fb;
         }
-        if (first && orc_is_info_frame(buf + pos, len - pos)) { pos += fb; first = 0; continue; }
         first = 0;
-        orc_info info;
-        int r = orc_decode_frame(d, buf + pos, fb, &tmp[0][0], &info);
-        pos += fb;
         if (r <= 0) continue;
         nch = info.channels;
         hz = info.hz;
-        for (int ch = 0; ch < nch; ch++) memcpy(pcm + (size_t)ch * max_frames * 1152 + nf * 1152, tmp[ch], sizeof(float) * 1152);
+        for (int ch = 0; ch < nch; ch++) memcpy(pcm + (size_t)ch * max_frames * 1152 + ns, tmp[ch], sizeof(float) * r);
+        ns += r;
         nf++;
     }
     if (nch_out) *nch_out = nch;
     if (hz_out) *hz_out = hz;
+    if (samples_out) *samples_out = ns;
     orc_destroy(d);
     return nf;
+}
+
+ORC_API long orc_decode_stream(const uint8_t *buf, long len, float *pcm, long max_frames, int *nch_out, int *hz_out) {
+    return orc_decode_stream_n(buf, len, pcm, max_frames, nch_out, hz_out, NULL);
 }
 
 /* ------------------------------------------------------------------------ */

@@ -30,8 +30,9 @@ def compare(name, ours, ref):
     checking our frame count (edge cases: tests/golden/manifest.json notes)."""
     import numpy as np
     meta = manifest()[name]
-    want = meta.get("our_frames") or ref.shape[1] // 1152
-    assert ours.shape[1] == want * 1152, (name, ours.shape, want)
+    spf = meta.get("spf", 1152)  # samples per frame: 576 for MPEG-2 / 2.5 LSF
+    want = meta.get("our_frames") or ref.shape[1] // spf
+    assert ours.shape[1] == want * spf, (name, ours.shape, want)
     k = min(ours.shape[1], ref.shape[1])
     d = np.abs(ours[:, :k].astype(np.int32) - ref[:, :k].astype(np.int32))
     return int(d.max()), float((d == 0).mean())

@@ -31,6 +31,11 @@ def lib():
         L.orc_decode_stream.argtypes = [ctypes.c_char_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_long,
                                         ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         L.orc_decode_stream.restype = ctypes.c_long
+        L.orc_decode_stream_n.argtypes = [ctypes.c_char_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_long,
+                                          ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                          ctypes.POINTER(ctypes.c_long)]
+        L.orc_decode_stream_n.restype = ctypes.c_long
+        L.orc_is_info_frame.argtypes = [ctypes.c_char_p, ctypes.c_long]
         L.orc_synth_only.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.orc_skip_id3v2.argtypes = [ctypes.c_char_p, ctypes.c_long]
@@ -42,21 +47,24 @@ def lib():
 
 def info_tag(data: bytes):
     """(found, dict) of the stream's leading Xing/Info + LAME tag (gapless)."""
-    out = np.zeros(5, np.int32)
+    out = np.zeros(6, np.int32)
     found = lib().orc_parse_info_tag(data, len(data), out.ctypes.data)
     keys = ("has_lame", "enc_delay", "enc_padding", "total_frames", "skip_samples")
     d = dict(zip(keys, (int(x) for x in out)))
-    d["end_sample"] = d["total_frames"] * 1152 + 529 - d["enc_padding"] if d["has_lame"] and d["total_frames"] > 0 else -1
+    spf = int(out[5])  # samples per frame: 1152, or 576 for MPEG-2/2.5
+    d["end_sample"] = d["total_frames"] * spf + 529 - d["enc_padding"] if d["has_lame"] and d["total_frames"] > 0 else -1
     return bool(found), d
 
 
 def decode_stream(data: bytes, max_frames=100000):
-    """Planar float32 [nch, frames*1152] (ID3v2 and Xing/Info frame skipped)."""
+    """Planar float32 [nch, samples] (ID3v2 and Xing/Info frame skipped;
+    1152 samples per MPEG-1 frame, 576 per MPEG-2/2.5 frame)."""
     L = lib()
     out = np.zeros((2, max_frames * 1152), np.float32)
-    nch, hz = ctypes.c_int(), ctypes.c_int()
-    nf = L.orc_decode_stream(data, len(data), out.ctypes.data, max_frames, ctypes.byref(nch), ctypes.byref(hz))
-    return out[: nch.value, : nf * 1152], hz.value
+    nch, hz, ns = ctypes.c_int(), ctypes.c_int(), ctypes.c_long()
+    L.orc_decode_stream_n(data, len(data), out.ctypes.data, max_frames, ctypes.byref(nch), ctypes.byref(hz),
+                          ctypes.byref(ns))
+    return out[: nch.value, : ns.value], hz.value
 
 
 class Decoder:

@@ -31,12 +31,24 @@ def test_quad_tables():
 
 
 def test_band_tables():
-    for s in range(3):
+    assert t["MP3D_SFB_LONG_WIDTH"].shape == (9, 22) and t["MP3D_SFB_SHORT_WIDTH"].shape == (9, 13)
+    for s in range(9):
         assert int(t["MP3D_SFB_LONG_WIDTH"][s].sum()) == 576
         assert int(t["MP3D_SFB_SHORT_WIDTH"][s].sum()) == 192
-        # first 8 long bands always cover 36 lines (mixed-block boundary)
-        assert int(t["MP3D_SFB_LONG_WIDTH"][s][:8].sum()) == 36
-        assert int(t["MP3D_SFB_SHORT_WIDTH"][s][:3].sum()) * 3 == 36
+        # the mixed-block boundary: 8 (MPEG-1) / 6 (LSF) long bands cover the
+        # lines of 3 short bands x 3 windows (36; 72 at MPEG-2.5 8 kHz)
+        nl = 8 if s < 3 else 6
+        edge = int(t["MP3D_SFB_LONG_WIDTH"][s][:nl].sum())
+        assert edge == int(t["MP3D_SFB_SHORT_WIDTH"][s][:3].sum()) * 3 == (72 if s == 8 else 36)
+
+
+def test_lsf_tables():
+    assert list(t["MP3D_SAMPLE_RATE"]) == [44100, 48000, 32000, 22050, 24000, 16000, 11025, 12000, 8000]
+    nsf = t["MP3D_LSF_NSF"].astype(int)
+    # every slen table covers 21 long bands, 12 short bands x 3 windows, or
+    # 6 long + 9 short bands x 3 (mixed)
+    for row in nsf:
+        assert [int(row[b].sum()) for b in range(3)] == [21, 36, 33]
 
 
 def test_synthesis_window_shape():
@@ -75,10 +87,12 @@ def test_tables_present_in_ffmpeg_copy():
     assert in_region(t["MP3D_QUAD_CODE"][0].tobytes()) and in_region(t["MP3D_QUAD_LEN"][0].tobytes())
     assert in_region(t["MP3D_SYNTH_WINDOW_Q16"].astype("<i4").tobytes())
     assert in_region(t["MP3D_PRETAB"].tobytes())
-    for s in range(3):
-        assert in_region(t["MP3D_SFB_LONG_WIDTH"][s].tobytes())
-        assert in_region(t["MP3D_SFB_SHORT_WIDTH"][s].tobytes())
+    # whole 9-rate blocks (MPEG-1 + LSF), as FFmpeg's band_size_long / _short
+    assert in_region(t["MP3D_SFB_LONG_WIDTH"].tobytes())
+    assert in_region(t["MP3D_SFB_SHORT_WIDTH"].tobytes())
+    assert in_region(t["MP3D_LSF_NSF"].tobytes())  # FFmpeg lsf_nsf_table
     assert in_region(t["MP3D_BITRATE_L3"].astype("<u2").tobytes())
+    assert in_region(t["MP3D_BITRATE_L3_LSF"].astype("<u2").tobytes())
     assert kb.find(t["MP3D_SLEN"].tobytes()) >= 0
     assert kb.find(t["MP3D_ALIAS_C"].astype("<f4").tobytes()) >= 0
 
