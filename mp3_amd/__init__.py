@@ -317,13 +317,15 @@ def long_plan(data, segment_frames=32, max_frames=None):
 
 def pcm_to_planar(pcm_frames, infos):
     """[F, 2304] int16/float32 + infos [F] -> [channels, samples] for frames
-    with audio."""
+    with audio (1152 samples per channel, 576 for an MPEG-2 / 2.5 LSF frame,
+    interleaved at the start of the frame's row)."""
     rows = []
     nch = 0
     for f in range(pcm_frames.shape[0]):
-        if infos[f]["samples"]:
+        n = int(infos[f]["samples"])
+        if n:
             nch = int(infos[f]["channels"])
-            rows.append(pcm_frames[f, : 1152 * nch].reshape(1152, nch))
+            rows.append(pcm_frames[f, : n * nch].reshape(n, nch))
     if not rows:
         return np.zeros((0, 0), pcm_frames.dtype)
     return np.concatenate(rows).T.copy()

@@ -22,7 +22,7 @@
 
 namespace mp3d {
 hipError_t upload_constants(const float *, const float *, const float *, const float *, const float *, const float *,
-                            const float *);
+                            const float *, const float *);
 void launch_demux(const uint8_t *, const uint64_t *, const uint32_t *, uint8_t *, const uint64_t *, StreamState *,
                   FrameRec *, uint64_t *, void *, int, int, hipStream_t);
 void launch_huffman(const uint8_t *, const uint64_t *, const FrameRec *, const uint64_t *, const DevTables *, int16_t *,
@@ -142,7 +142,10 @@ static void build_tables(DevTables &t) {
             t.dwin[j][2 * i + 1] = (float)(sbn * D[64 * i + 32 + j]);
         }
     }
-    for (int sr = 0; sr < 3; sr++) {
+    for (int sr = 0; sr < 9; sr++) {
+        /* mixed blocks: long bands below line 36 (72 at MPEG-2.5 8 kHz, whose
+         * bands are twice as wide): 8 MPEG-1 bands, 6 LSF bands (FFmpeg) */
+        const int mix_end = sr == 8 ? 72 : 36;
         int lb[576], sidx[576], sdst[576];
         int l = 0;
         for (int b = 0; b < 22; b++)
@@ -160,14 +163,14 @@ static void build_tables(DevTables &t) {
         for (int i = 0; i < 576; i++) {
             t.lvar[sr][0][i] = (uint16_t)(lb[i] | i << 6);
             t.lvar[sr][1][i] = (uint16_t)(sidx[i] | sdst[i] << 6);
-            t.lvar[sr][2][i] = i < 36 ? t.lvar[sr][0][i] : t.lvar[sr][1][i];
+            t.lvar[sr][2][i] = i < mix_end ? t.lvar[sr][0][i] : t.lvar[sr][1][i];
         }
     }
     build_huffman_lut(t);
 }
 
 static int upload_symbols() {
-    float imdct12[6][6], win36[4][36], win12[12], cs[8], ca[8], isr[7][2], p2q[4];
+    float imdct12[6][6], win36[4][36], win12[12], cs[8], ca[8], isr[7][2], p2q[4], isl[2][16][2];
     for (int k = 0; k < 6; k++)
         for (int o = 0; o < 6; o++) {
             int i = o < 3 ? o : 6 + (o - 3);
@@ -199,10 +202,19 @@ static int upload_symbols() {
         isr[p][0] = (float)(tn / (1.0 + tn));
         isr[p][1] = (float)(1.0 / (1.0 + tn));
     }
+    /* LSF intensity (13818-3 2.4.3.2; FFmpeg is_table_lsf): is_pos p with
+     * intensity_scale j -> (2^(-(j+1) ((p+1)/2) / 4), 1) for odd p, swapped
+     * for even p (L = x * [0], R = x * [1]) */
+    for (int j = 0; j < 2; j++)
+        for (int p = 0; p < 16; p++) {
+            const float f = (float)pow(2.0, -(j + 1) * ((p + 1) >> 1) / 4.0);
+            isl[j][p][0] = (p & 1) ? f : 1.f;
+            isl[j][p][1] = (p & 1) ? 1.f : f;
+        }
     for (int i = 0; i < 4; i++) p2q[i] = (float)pow(2.0, i / 4.0);
     for (int i = 0; i < 22; i++)
         if (((MP3D_PRETAB_BITS >> (2 * i)) & 3u) != MP3D_PRETAB[i]) return MP3D_E_ARG; /* table drift */
-    HIPCHK(upload_constants(&imdct12[0][0], &win36[0][0], win12, cs, ca, &isr[0][0], p2q));
+    HIPCHK(upload_constants(&imdct12[0][0], &win36[0][0], win12, cs, ca, &isr[0][0], p2q, &isl[0][0][0]));
     return MP3D_OK;
 }
 
@@ -563,7 +575,7 @@ extern "C" int mp3d_batch_synth_only(mp3d_batch *b, const float *xr, const uint8
     return MP3D_OK;
 }
 
-static void tag_to_info(uint32_t tag, uint32_t frames, mp3d_stream_info *o) {
+static void tag_to_info(uint32_t tag, uint32_t frames, int kind, mp3d_stream_info *o) {
     memset(o, 0, sizeof(*o));
     o->has_tag = (tag & MP3D_TAG_SEEN) != 0;
     o->has_lame = (tag & MP3D_TAG_LAME) != 0;
@@ -573,7 +585,7 @@ static void tag_to_info(uint32_t tag, uint32_t frames, mp3d_stream_info *o) {
         o->enc_delay = (int)((tag >> 12) & 0xFFFu);
         o->enc_padding = (int)(tag & 0xFFFu);
         o->skip_samples = o->enc_delay + 529; /* FFmpeg: start_pad + 528 + 1 */
-        if (o->total_frames > 0) o->end_sample = (long long)o->total_frames * 1152 + 529 - o->enc_padding;
+        if (o->total_frames > 0) o->end_sample = (long long)o->total_frames * (kind == 2 ? 576 : 1152) + 529 - o->enc_padding;
     }
 }
 
@@ -581,18 +593,21 @@ extern "C" int mp3d_batch_stream_info(mp3d_batch *b, int n, mp3d_stream_info *ou
     if (!b || !out || n <= 0) return MP3D_E_ARG;
     if (n > b->max_streams) return MP3D_E_CAPACITY;
     HIPCHK(hipSetDevice(b->device));
-    std::vector<uint32_t> tag((size_t)n * 2);
+    /* StreamState tag_info, tag_frames, kind: three consecutive words */
+    std::vector<uint32_t> tag((size_t)n * 3);
     HIPCHK(hipStreamSynchronize(b->own));
-    HIPCHK(hipMemcpy2D(tag.data(), 2 * sizeof(uint32_t), &b->st[0].tag_info, sizeof(StreamState),
-                       2 * sizeof(uint32_t), n, hipMemcpyDeviceToHost));
-    for (int i = 0; i < n; i++) tag_to_info(tag[2 * i], tag[2 * i + 1], &out[i]);
+    HIPCHK(hipMemcpy2D(tag.data(), 3 * sizeof(uint32_t), &b->st[0].tag_info, sizeof(StreamState),
+                       3 * sizeof(uint32_t), n, hipMemcpyDeviceToHost));
+    for (int i = 0; i < n; i++) tag_to_info(tag[3 * i], tag[3 * i + 1], (int)tag[3 * i + 2], &out[i]);
     return MP3D_OK;
 }
 
 /* ------------------------------------------------------------------------ */
 /* Segmented decode of one long stream               */
 /* ------------------------------------------------------------------------ */
-static int host_frame_bytes(const uint8_t *p);
+static int host_frame_bytes(const uint8_t *p, int kind);
+static int host_frame_kind(const uint8_t *p);
+static int host_frame_head(const uint8_t *p);
 
 /* Frame slots of a stream exactly as k_demux enumerates them: ID3v2 skip,
  * resync on the next valid header, a cut-short final frame kept while its
@@ -603,13 +618,14 @@ static void walk_frames(const uint8_t *p, size_t len, std::vector<uint64_t> &off
         cur = 10 + (((size_t)(p[6] & 0x7F) << 21) | ((size_t)(p[7] & 0x7F) << 14) | ((size_t)(p[8] & 0x7F) << 7) |
                     (p[9] & 0x7F)) +
               ((p[5] & 0x10) ? 10 : 0);
+    int kind = 0; /* MPEG family lock, as k_demux */
     while (cur + 4 <= len) {
         int fb = -1;
         for (; cur + 4 <= len; cur++)
-            if ((fb = host_frame_bytes(p + cur)) > 0) break;
+            if ((fb = host_frame_bytes(p + cur, kind)) > 0) break;
         if (fb <= 0) break;
-        const int nch = (p[cur + 3] >> 6) == 3 ? 1 : 2;
-        const size_t need = 4 + ((p[cur + 1] & 1) ? 0 : 2) + (nch == 1 ? 17 : 32);
+        kind = host_frame_kind(p + cur);
+        const size_t need = (size_t)host_frame_head(p + cur);
         if (cur + fb > len && cur + need > len) break;
         off.push_back(cur);
         payload.push_back(fb > (int)need ? (uint32_t)(fb - need) : 0u);
@@ -769,6 +785,7 @@ done:
 struct mp3d_dec {
     mp3d_batch *b = nullptr;
     long frames = 0;
+    int kind = 0; /* MPEG family of the stream's first frame (StreamState.kind) */
 };
 
 extern "C" int mp3d_dec_create_on(int device, mp3d_dec **out) {
@@ -801,6 +818,7 @@ extern "C" void mp3d_dec_reset(mp3d_dec *d) {
     if (!d) return;
     (void)mp3d_batch_reset(d->b);
     d->frames = 0;
+    d->kind = 0;
 }
 
 extern "C" int mp3d_dec_stream_info(mp3d_dec *d, mp3d_stream_info *out) {
@@ -808,11 +826,24 @@ extern "C" int mp3d_dec_stream_info(mp3d_dec *d, mp3d_stream_info *out) {
     return mp3d_batch_stream_info(d->b, 1, out);
 }
 
-static int host_frame_bytes(const uint8_t *p) {
-    if (p[0] != 0xFF || (p[1] & 0xFE) != 0xFA) return -1;
-    int bi = p[2] >> 4, si = (p[2] >> 2) & 3;
+/* Layer III frame bytes of the header at p, or -1 (k_demux hdr_frame_bytes):
+ * MPEG-1 and MPEG-2 / 2.5 LSF; kind 0 any family, 1 MPEG-1 only, 2 LSF only */
+static int host_frame_kind(const uint8_t *p) { return ((p[1] >> 3) & 3) == 3 ? 1 : 2; }
+static int host_frame_bytes(const uint8_t *p, int kind) {
+    const int ver = (p[1] >> 3) & 3;
+    if (p[0] != 0xFF || (p[1] & 0xE0) != 0xE0 || ((p[1] >> 1) & 3) != 1 || ver == 1) return -1;
+    const int bi = p[2] >> 4, si = (p[2] >> 2) & 3;
     if (bi == 0 || bi == 15 || si == 3) return -1;
-    return 144000 * (int)MP3D_BITRATE_L3[bi] / (int)MP3D_SAMPLE_RATE[si] + ((p[2] >> 1) & 1);
+    const int k = host_frame_kind(p);
+    if (kind && k != kind) return -1;
+    const int hz = (int)MP3D_SAMPLE_RATE[si + (ver == 3 ? 0 : ver == 2 ? 3 : 6)];
+    return (k == 1 ? 144000 * (int)MP3D_BITRATE_L3[bi] : 72000 * (int)MP3D_BITRATE_L3_LSF[bi]) / hz +
+           ((p[2] >> 1) & 1);
+}
+/* header + CRC + side-info bytes */
+static int host_frame_head(const uint8_t *p) {
+    const bool mono = (p[3] >> 6) == 3, lsf = host_frame_kind(p) == 2;
+    return 4 + ((p[1] & 1) ? 0 : 2) + (lsf ? (mono ? 9 : 17) : (mono ? 17 : 32));
 }
 
 static int decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, void *pcm, bool f32, mp3d_frame_info *info) {
@@ -828,7 +859,7 @@ static int decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, void *pcm
     }
     int fb = -1;
     while (pos + 4 <= bytes) {
-        fb = host_frame_bytes(buf + pos);
+        fb = host_frame_bytes(buf + pos, d->kind);
         if (fb > 0) break;
         pos++;
     }
@@ -843,9 +874,10 @@ static int decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, void *pcm
     int r = batch_decode(d->b, buf + pos, &off, &sz, 1, 1, out, f32, &fi, nullptr);
     if (r) return r;
     d->frames++;
+    if (fi.frame_bytes) d->kind = host_frame_kind(buf + pos);
     *info = fi;
     info->frame_bytes = (int)pos + fi.frame_bytes;
-    if (fi.samples && pcm) memcpy(pcm, out, (f32 ? sizeof(float) : sizeof(int16_t)) * 1152 * fi.channels);
+    if (fi.samples && pcm) memcpy(pcm, out, (f32 ? sizeof(float) : sizeof(int16_t)) * (size_t)fi.samples * fi.channels);
     return fi.samples;
 }
 

@@ -41,8 +41,9 @@ struct FrameRec {
     uint8_t nch;
     uint8_t side_off;    /* 4 or 6 (CRC)                                     */
     uint8_t first_gr;    /* first decoded granule (reservoir underflow)      */
-    uint8_t sr_idx;
-    uint8_t pad_;
+    uint8_t sr_idx;      /* 0..2 MPEG-1, 3..5 MPEG-2, 6..8 MPEG-2.5 (LSF)    */
+    uint8_t lsf;         /* 1: MPEG-2 / 2.5 low sampling frequency frame,    */
+                         /*    one granule (ISO 13818-3)                     */
     uint16_t payload_avail; /* payload bytes present (< payload_len: the final
                              * frame was cut short; the rest reads as zeros) */
 };
@@ -59,7 +60,9 @@ struct __attribute__((aligned(8))) UnitMeta {
     uint16_t nz_end;     /* lines produced by big_values + count1          */
     uint16_t part2_3_length;
     uint16_t used_bits;  /* bits consumed (== part2_3_length when valid)   */
-    uint16_t pad_;
+    uint16_t flags;      /* bit 0: granule lost to a reservoir underflow;  */
+                         /* bit 1: LSF intensity_scale (scalefac_compress  */
+                         /* bit 0 of an intensity frame's right channel)   */
 };
 
 /* Persistent per-stream decoder state. */
@@ -72,6 +75,11 @@ struct StreamState {
      * encoder delay, bits 0..11 encoder padding; tag_frames = Xing count */
     uint32_t tag_info;
     uint32_t tag_frames;
+    /* MPEG version family, fixed by the stream's first frame (k_demux):
+     * 0 none yet, 1 MPEG-1, 2 MPEG-2 / 2.5 LSF.  Headers of the other
+     * family are skipped as junk; k_synth runs one variant per family. */
+    int32_t kind;
+    int32_t pad_[3];
     float overlap[2][32][18];              /* IMDCT overlap                  */
     float fifo[2][MP3D_FIFO_SLOTS][32];    /* last 15 matrixing outputs X    */
 };
@@ -92,10 +100,10 @@ struct DevTables {
     float pow43[8208];         /* |is|^(4/3), |is| <= 8206               */
     float dct_c[32][32];       /* C[m][sb] = cos(m (2 sb + 1) pi / 64)  */
     float dwin[32][16];        /* per output j: signed window taps       */
-    /* per (sample rate, block variant long / short / mixed, bitstream
+    /* per (sample-rate index 0..8, block variant long / short / mixed, bitstream
      * line): bits 0..5 scale index (long band b, or 22 + 3 b + w for short
      * band b window w), bits 6..15 position after the short reorder      */
-    uint16_t lvar[3][3][576];
+    uint16_t lvar[9][3][576];
     uint8_t win_a[32];         /* V[j] = sgn * X[a[j]]                   */
     uint8_t win_b[32];         /* V[32 + j] = sgn * X[b[j]]              */
     uint16_t lut[MP3D_LUT_MAX];

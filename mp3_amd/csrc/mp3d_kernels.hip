@@ -32,6 +32,7 @@ __constant__ float c_alias_cs[8];
 __constant__ float c_alias_ca[8];
 __constant__ float c_is_ratio[7][2];  /* MPEG-1 intensity: k/(1+k), 1/(1+k) */
 __constant__ float c_pow2q[4];        /* 2^(i/4) */
+__constant__ float c_is_lsf[2][16][2];/* LSF intensity [intensity_scale][is_pos]: L, R */
 
 struct DevInfo { /* mirrors mp3d_frame_info (include/mp3d.h) */
     int32_t frame_bytes, channels, hz, layer, bitrate_kbps, samples;
@@ -43,16 +44,31 @@ struct DevInfo { /* mirrors mp3d_frame_info (include/mp3d.h) */
 /* ------------------------------------------------------------------------ */
 /* Header / side-info helpers (ISO 2.4.1.3, 2.4.1.7)                          */
 /* ------------------------------------------------------------------------ */
-__device__ __forceinline__ int hdr_frame_bytes(uint8_t b1, uint8_t b2) {
-    if ((b1 & 0xFE) != 0xFA) return -1;
-    int bi = b2 >> 4, si = (b2 >> 2) & 3;
-    if (bi == 0 || bi == 15 || si == 3) return -1;
-    return 144000 * (int)MP3D_BITRATE_L3[bi] / (int)MP3D_SAMPLE_RATE[si] + ((b2 >> 1) & 1);
+/* Layer III header bytes 1, 2 (after 0xFF) -> frame bytes, or -1.  MPEG-1
+ * (ISO 11172-3 2.4.2.3) and MPEG-2 / 2.5 LSF (ISO 13818-3: 72000 instead of
+ * 144000, LSF bitrates); kind = the stream's family (StreamState.kind: 0
+ * any, 1 MPEG-1, 2 LSF) -- headers of the other family are not frames. */
+__device__ __forceinline__ int hdr_kind(uint32_t b1) { return ((b1 >> 3) & 3) == 3 ? 1 : 2; }
+__device__ __forceinline__ int hdr_sr_idx(uint32_t b1, uint32_t b2) {
+    const uint32_t ver = (b1 >> 3) & 3, si = (b2 >> 2) & 3;
+    return (int)si + (ver == 3 ? 0 : ver == 2 ? 3 : 6);
+}
+__device__ __forceinline__ int hdr_frame_bytes(uint32_t b1, uint32_t b2, int kind) {
+    if ((b1 & 0xE0) != 0xE0 || ((b1 >> 1) & 3) != 1 || ((b1 >> 3) & 3) == 1) return -1;
+    const int bi = (int)(b2 >> 4);
+    if (bi == 0 || bi == 15 || ((b2 >> 2) & 3) == 3) return -1;
+    const int k = hdr_kind(b1);
+    if (kind && k != kind) return -1;
+    const int hz = (int)MP3D_SAMPLE_RATE[hdr_sr_idx(b1, b2)];
+    return (k == 1 ? 144000 * (int)MP3D_BITRATE_L3[bi] : 72000 * (int)MP3D_BITRATE_L3_LSF[bi]) / hz +
+           (int)((b2 >> 1) & 1);
 }
 
-/* bit offset of unit (gr, ch) inside the side info */
-__device__ __forceinline__ uint32_t side_unit_bit(int nch, int gr, int ch) {
-    return 9 + (nch == 1 ? 5 : 3) + 4 * nch + 59 * (gr * nch + ch);
+/* bit offset of unit (gr, ch) inside the side info: MPEG-1 9-bit
+ * main_data_begin, private bits, scfsi, 59-bit units; LSF 8-bit
+ * main_data_begin, 1 / 2 private bits, one granule of 63-bit units */
+__device__ __forceinline__ uint32_t side_unit_bit(int nch, int gr, int ch, bool lsf) {
+    return lsf ? 8 + nch + 63 * ch : 9 + (nch == 1 ? 5 : 3) + 4 * nch + 59 * (gr * nch + ch);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -144,6 +160,7 @@ __global__ void __launch_bounds__(64) k_demux(const uint8_t *__restrict__ in, co
     StreamState &S = st[s];
     const int carry_in = S.res_len;
     const bool stream_start = S.frames == 0;
+    int kind = S.kind; /* MPEG family lock (0 until the first frame) */
     for (int i = lane; i < (carry_in + 3) / 4; i += 64) ((uint32_t *)dst)[i] = ((const uint32_t *)S.res)[i];
     __threadfence_block(); /* carry words may spill past carry_in into payload 0's head */
 
@@ -168,7 +185,7 @@ __global__ void __launch_bounds__(64) k_demux(const uint8_t *__restrict__ in, co
             uint32_t k = 0;
             for (; k <= lim; k++) {
                 if (win_byte(w, k) == 0xFFu) {
-                    fb = hdr_frame_bytes((uint8_t)win_byte(w, k + 1), (uint8_t)win_byte(w, k + 2));
+                    fb = hdr_frame_bytes(win_byte(w, k + 1), win_byte(w, k + 2), kind);
                     if (fb > 0) break;
                 }
             }
@@ -177,7 +194,7 @@ __global__ void __launch_bounds__(64) k_demux(const uint8_t *__restrict__ in, co
         }
         FrameRec r;
         r.frame_off = 0; r.md_bit = 0; r.payload_md = P; r.frame_bytes = 0; r.payload_len = 0;
-        r.hdr1 = r.hdr2 = r.hdr3 = 0; r.nch = 0; r.side_off = 4; r.first_gr = 0; r.sr_idx = 0; r.pad_ = 0;
+        r.hdr1 = r.hdr2 = r.hdr3 = 0; r.nch = 0; r.side_off = 4; r.first_gr = 0; r.sr_idx = 0; r.lsf = 0;
         r.payload_avail = 0;
         DevInfo inf = {0, 0, 0, 0, 0, 0};
         uint64_t sw = 0; /* lane q < 4: side word of unit q = gr * 2 + ch */
@@ -188,7 +205,10 @@ __global__ void __launch_bounds__(64) k_demux(const uint8_t *__restrict__ in, co
             const uint32_t h1 = win_byte(w, 1), h2 = win_byte(w, 2), h3 = win_byte(w, 3);
             const int nch = (h3 >> 6) == 3 ? 1 : 2;
             const int crc = (h1 & 1) ? 0 : 2;
-            const int side_bytes = nch == 1 ? 17 : 32;
+            const bool lsf = hdr_kind(h1) == 2;
+            const int ngr = lsf ? 1 : 2;
+            const int side_bytes = lsf ? (nch == 1 ? 9 : 17) : (nch == 1 ? 17 : 32);
+            kind = hdr_kind(h1);
             const uint32_t need = 4u + (uint32_t)crc + (uint32_t)side_bytes;
             /* a final frame cut short still decodes (FFmpeg: the missing bytes
              * read as zeros) once its header and side info are present */
@@ -201,20 +221,39 @@ __global__ void __launch_bounds__(64) k_demux(const uint8_t *__restrict__ in, co
                 r.hdr1 = (uint8_t)h1; r.hdr2 = (uint8_t)h2; r.hdr3 = (uint8_t)h3;
                 r.nch = (uint8_t)nch;
                 r.side_off = (uint8_t)(4 + crc);
-                r.sr_idx = (uint8_t)((h2 >> 2) & 3);
+                r.sr_idx = (uint8_t)hdr_sr_idx(h1, h2);
+                r.lsf = (uint8_t)lsf;
                 inf.frame_bytes = fb; inf.channels = nch; inf.hz = (int)MP3D_SAMPLE_RATE[r.sr_idx];
-                inf.layer = 3; inf.bitrate_kbps = MP3D_BITRATE_L3[h2 >> 4];
+                inf.layer = 3; inf.bitrate_kbps = lsf ? MP3D_BITRATE_L3_LSF[h2 >> 4] : MP3D_BITRATE_L3[h2 >> 4];
                 /* side info: bit offsets relative to the window's dword base */
                 const uint32_t sbit = 8u * ((cur & 3u) + 4u + (uint32_t)crc);
-                const int mdb = (int)(win_bits64(w, sbit) >> 55);
+                const int mdb = (int)(win_bits64(w, sbit) >> (lsf ? 56 : 55));
                 const int q = lane & 3, qgr = q >> 1, qch = q & 1;
-                const uint32_t ub = sbit + side_unit_bit(nch, qgr, qch);
-                const uint64_t v59 = win_bits64(w, ub) >> 5;
-                const uint32_t scfsi = (uint32_t)(win_bits64(w, sbit + 9 + (nch == 1 ? 5 : 3) + 4 * qch) >> 60);
-                const bool unit_ok = lane < 4 && qch < nch;
+                const uint32_t ub = sbit + side_unit_bit(nch, qgr, qch, lsf);
+                const bool unit_ok = lane < 4 && qch < nch && qgr < ngr;
+                uint64_t v59;
+                uint32_t low5; /* side word bits 4..0: scfsi << 1 (MPEG-1) | scalefac_compress >> 4 (LSF) */
+                if (lsf) {
+                    /* 63-bit LSF unit (13818-3 2.4.1.7): part2_3 12, big_values 9,
+                     * global_gain 8, scalefac_compress 9, window switching 1 +
+                     * 22, scalefac_scale 1, count1table 1 -> the MPEG-1 layout
+                     * with scalefac_compress bits 0..3 in its 4-bit slot, the
+                     * intensity-right-channel flag in the preflag slot, bits
+                     * 4..8 in the side word's low 5 bits */
+                    const uint64_t v63 = win_bits64(w, ub) >> 1;
+                    const uint32_t sfc9 = (uint32_t)(v63 >> 25) & 511u;
+                    const uint64_t low25 = v63 & 0x1FFFFFFull;
+                    const bool is_right = (h3 >> 6) == 1 && ((h3 >> 4) & 1) && qch == 1;
+                    v59 = ((v63 >> 34) << 30) | ((uint64_t)(sfc9 & 15u) << 26) | ((low25 >> 2) << 3) |
+                          ((uint64_t)is_right << 2) | (low25 & 3u);
+                    low5 = sfc9 >> 4;
+                } else {
+                    v59 = win_bits64(w, ub) >> 5;
+                    low5 = (uint32_t)(win_bits64(w, sbit + 9 + (nch == 1 ? 5 : 3) + 4 * qch) >> 60) << 1;
+                }
                 const uint32_t myp23 = unit_ok ? (uint32_t)(v59 >> 47) : 0u;
                 const bool mybad = unit_ok && ((v59 >> 38) & 0x1FFu) > 288u; /* SURVEY A.9 (5) */
-                sw = unit_ok ? (v59 << 5) | ((uint64_t)scfsi << 1) : 0ull;
+                sw = unit_ok ? (v59 << 5) | low5 : 0ull;
                 int p23[2][2];
                 p23[0][0] = __builtin_amdgcn_readlane((int)myp23, 0);
                 p23[0][1] = __builtin_amdgcn_readlane((int)myp23, 1);
@@ -244,7 +283,7 @@ __global__ void __launch_bounds__(64) k_demux(const uint8_t *__restrict__ in, co
                         mdbit = (P - (uint32_t)mdb) * 8u;
                     } else {
                         uint32_t bits = (uint32_t)avail * 8u;
-                        while (gr0 < 2 && (int)(bits >> 3) < mdb) {
+                        while (gr0 < ngr && (int)(bits >> 3) < mdb) {
                             for (int ch = 0; ch < nch; ch++) bits += (uint32_t)p23[gr0][ch];
                             gr0++;
                         }
@@ -258,7 +297,7 @@ __global__ void __launch_bounds__(64) k_demux(const uint8_t *__restrict__ in, co
                     P += (uint32_t)plen;
                     const int64_t after = (int64_t)P - (int64_t)((end + 7u) >> 3);
                     avail = after < 0 ? 0 : (int)after;
-                    inf.samples = 1152;
+                    inf.samples = lsf ? 576 : 1152;
                     decoded++;
                 }
                 const uint32_t body = (r.first_gr & REC_DROP) ? 4u : need;
@@ -285,9 +324,11 @@ __global__ void __launch_bounds__(64) k_demux(const uint8_t *__restrict__ in, co
             const uint32_t h = min((4u - (Pm & 3u)) & 3u, L);     /* head bytes up to an aligned word */
             const uint32_t wb = (Pm + h) >> 2, we = (Pm + L) >> 2; /* whole words [wb, we)           */
             if ((uint32_t)lane < h) dst[Pm + lane] = src[lane];
+            /* tail bytes [t0, L) after the last whole word -- or after the head
+             * when there is none (an LSF payload can be < 8 bytes) */
+            const uint32_t t0 = 4u * we > Pm + h ? 4u * we - Pm : h; /* h <= t0 <= L */
+            if ((uint32_t)lane < L - t0) dst[Pm + t0 + lane] = src[t0 + lane];
             if (wb < we) {
-                const uint32_t t0 = 4u * we - Pm; /* tail bytes [t0, L) */
-                if ((uint32_t)lane < L - t0) dst[Pm + t0 + lane] = src[t0 + lane];
                 const uint64_t sa0 = (uint64_t)(src + (4u * wb - Pm));
                 const uint32_t sh = (uint32_t)(sa0 & 3u) * 8u;
                 const uint32_t *swd = (const uint32_t *)(sa0 & ~(uint64_t)3);
@@ -306,6 +347,7 @@ __global__ void __launch_bounds__(64) k_demux(const uint8_t *__restrict__ in, co
     if (lane == 0) {
         S.res_len = c;
         S.frames += decoded;
+        S.kind = kind;
     }
 }
 
@@ -413,6 +455,56 @@ __device__ __forceinline__ uint32_t read_sf(const uint32_t *bits, uint32_t pos, 
     return pos;
 }
 
+/* LSF scalefactors (ISO 13818-3 2.4.3.2; FFmpeg mp_decode_layer3): slen[4]
+ * from the 9-bit scalefac_compress (intensity right channel: its half and
+ * other ranges), group sizes from MP3D_LSF_NSF, read in coding order and
+ * stored byte by byte into the canonical UnitMeta.sf layout (mixed blocks:
+ * short bands from sf[8]).  LSF units only -- off the MPEG-1 path, so the
+ * plain per-byte global stores are fine.  *preflag = scalefac_compress >= 500. */
+typedef const __attribute__((address_space(3))) uint32_t *lds_cu32;
+__device__ __attribute__((noinline)) uint32_t read_sf_lsf(lds_cu32 bits, uint32_t pos, uint64_t side, uint8_t *sf,
+                                                          int *preflag) {
+    const int ws = (int)(side >> 30) & 1, bt = ws ? (int)(side >> 28) & 3 : 0;
+    const int tindex = bt == 2 ? (((side >> 27) & 1) ? 2 : 1) : 0;
+    const bool is_right = (side >> 7) & 1;
+    int sfc = (int)((side >> 31) & 15) | (int)((side & 31) << 4);
+    int n1, n2, n3, t2;
+    *preflag = 0;
+    if (is_right) {
+        sfc >>= 1;
+        if (sfc < 180) { n1 = 6; n2 = 6; n3 = 0; t2 = 3; }
+        else if (sfc < 244) { sfc -= 180; n1 = 4; n2 = 4; n3 = 0; t2 = 4; }
+        else { sfc -= 244; n1 = 3; n2 = 0; n3 = 0; t2 = 5; }
+    } else {
+        if (sfc < 400) { n1 = 5; n2 = 4; n3 = 4; t2 = 0; }
+        else if (sfc < 500) { sfc -= 400; n1 = 5; n2 = 4; n3 = 0; t2 = 1; }
+        else { sfc -= 500; n1 = 3; n2 = 0; n3 = 0; t2 = 2; *preflag = 1; }
+    }
+    int slen[4];
+    if (n3) { slen[3] = sfc % n3; sfc /= n3; } else slen[3] = 0;
+    if (n2) { slen[2] = sfc % n2; sfc /= n2; } else slen[2] = 0;
+    slen[1] = sfc % n1;
+    slen[0] = sfc / n1;
+    *(uint4 *)sf = make_uint4(0u, 0u, 0u, 0u);
+    *(uint4 *)(sf + 16) = make_uint4(0u, 0u, 0u, 0u);
+    *(uint2 *)(sf + 32) = make_uint2(0u, 0u);
+    int j = 0;
+    for (int k = 0; k < 4; k++) {
+        const int sl = slen[k], n = MP3D_LSF_NSF[t2][tindex][k];
+        for (int i = 0; i < n; i++, j++) {
+            uint32_t v = 0u;
+            if (sl) { /* ds_read (the staged words are LDS; no flat access) */
+                const uint32_t w = pos >> 5;
+                const uint64_t pr = ((uint64_t)bits[w] << 32) | bits[w + 1];
+                v = (uint32_t)(pr >> (64u - (pos & 31u) - (uint32_t)sl)) & ((1u << sl) - 1u);
+            }
+            pos += (uint32_t)sl;
+            sf[tindex == 2 && j >= 6 ? j + 2 : j] = (uint8_t)v;
+        }
+    }
+    return pos;
+}
+
 /* is[] row writer: words (2 x int16) are shifted through 4 registers and
  * stored 16 B at a time (one dwordx4 per 8 lines instead of 4 dword stores) */
 struct RowWriter {
@@ -447,14 +539,14 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
     __shared__ uint16_t s_lut[MP3D_LUT_MAX];
     __shared__ __attribute__((aligned(16))) uint32_t s_bits[HUFF_WAVES][HUFF_CAPW + 4];
     __shared__ uint32_t s_tsel[32]; /* table_select -> LUT base | bits1 << 16 | linbits << 24 */
-    __shared__ uint16_t s_lbnd[3][24]; /* long sfb start line per sample rate (23 bounds)       */
+    __shared__ uint16_t s_lbnd[9][24]; /* long sfb start line per sample-rate index (23 bounds) */
     __shared__ uint8_t s_slen[32];     /* MPEG-1 slen1 | slen2 per scalefac_compress          */
     const int lut_n = tab->lut_hdr.base[MP3D_LUT_TABLES - 1] + (1 << tab->lut_hdr.bits1[MP3D_LUT_TABLES - 1]);
     const int zbase = (lut_n + 1) & ~1; /* 2-entry all-zero table for table_select 0, 4, 14 */
     for (int i = threadIdx.x; i < (lut_n + 1) / 2; i += blockDim.x)
         ((uint32_t *)s_lut)[i] = ((const uint32_t *)tab->lut)[i];
     if (threadIdx.x == 0) ((uint32_t *)s_lut)[zbase / 2] = 0u;
-    if (threadIdx.x < 3) {
+    if (threadIdx.x < 9) {
         int acc = 0;
         for (int i = 0; i < 22; i++) {
             s_lbnd[threadIdx.x][i] = (uint16_t)acc;
@@ -529,7 +621,7 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
             uint64_t sq[4] = {0, 0, 0, 0};
             if (valid) {
                 r = rec[fr];
-                valid = r.frame_bytes && !(r.first_gr & (REC_TAG | REC_DROP)) && ch < r.nch;
+                valid = r.frame_bytes && !(r.first_gr & (REC_TAG | REC_DROP)) && ch < r.nch && (gr == 0 || !r.lsf);
                 const ulonglong2 a = *(const ulonglong2 *)&sideu[u & ~3];
                 const ulonglong2 b = *(const ulonglong2 *)&sideu[(u & ~3) + 2];
                 sq[0] = a.x; sq[1] = a.y; sq[2] = b.x; sq[3] = b.y;
@@ -591,18 +683,23 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                 }
                 wave_sync();
                 if (inb) {
-                    uint32_t sfw[10];
-#pragma unroll
-                    for (int i = 0; i < 10; i++) sfw[i] = 0u;
                     const uint32_t seg = 32u * (off - base) - 32u * w0; /* md bit -> staged bit */
                     uint32_t pos = start + seg;
-                    if (need_g0) {
-                        /* scfsi reuse: granule 0's scalefactors of this channel
-                         * first, then granule 1's read over them in place */
-                        read_sf(bits, g0_start + seg, sq[ch], 0, sfw, s_slen);
-                    }
-                    pos = read_sf(bits, pos, side, scfsi, sfw, s_slen);
-                    {
+                    int lsf_pre = 0;
+                    if (r.lsf) {
+                        /* off the MPEG-1 path: a call keeps its registers out of
+                         * the kernel's allocation; bits passed as an LDS pointer */
+                        pos = read_sf_lsf((lds_cu32)bits, pos, side, (uint8_t *)&meta[u], &lsf_pre);
+                    } else {
+                        uint32_t sfw[10];
+#pragma unroll
+                        for (int i = 0; i < 10; i++) sfw[i] = 0u;
+                        if (need_g0) {
+                            /* scfsi reuse: granule 0's scalefactors of this channel
+                             * first, then granule 1's read over them in place */
+                            read_sf(bits, g0_start + seg, sq[ch], 0, sfw, s_slen);
+                        }
+                        pos = read_sf(bits, pos, side, scfsi, sfw, s_slen);
                         uint8_t *mrec = (uint8_t *)&meta[u];
                         *(uint4 *)mrec = make_uint4(sfw[0], sfw[1], sfw[2], sfw[3]);
                         *(uint4 *)(mrec + 16) = make_uint4(sfw[4], sfw[5], sfw[6], sfw[7]);
@@ -614,7 +711,10 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                     int r1, r2;
                     uint32_t ts0, ts1, ts2;
                     if (ws) {
-                        r1 = 36;
+                        /* region0: 36 lines; FFmpeg LSF: 54 for long-type units
+                         * (108 at 8 kHz), 72 for short units at 8 kHz */
+                        const bool sh = ((side >> 28) & 3) == 2;
+                        r1 = r.sr_idx < 3 ? 36 : sh ? (r.sr_idx == 8 ? 72 : 36) : (r.sr_idx == 8 ? 108 : 54);
                         r2 = 576;
                         ts0 = s_tsel[(side >> 22) & 31];
                         ts1 = s_tsel[(side >> 17) & 31];
@@ -704,14 +804,14 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                     m.block_type = (uint8_t)(ws ? (side >> 28) & 3 : 0);
                     m.mixed = (uint8_t)(ws && ((side >> 28) & 3) == 2 ? (side >> 27) & 1 : 0);
                     m.scalefac_scale = (uint8_t)((side >> 6) & 1);
-                    m.preflag = (uint8_t)((side >> 7) & 1);
+                    m.preflag = (uint8_t)(r.lsf ? lsf_pre : (int)((side >> 7) & 1));
                     m.sbg[0] = (uint8_t)(ws ? (side >> 14) & 7 : 0);
                     m.sbg[1] = (uint8_t)(ws ? (side >> 11) & 7 : 0);
                     m.sbg[2] = (uint8_t)(ws ? (side >> 8) & 7 : 0);
                     m.nz_end = (uint16_t)nz_end;
                     m.part2_3_length = (uint16_t)p23;
                     m.used_bits = (uint16_t)(pos - start - seg);
-                    m.pad_ = 0;
+                    m.flags = (uint16_t)(r.lsf ? ((side >> 31) & 1) << 1 : 0); /* LSF intensity_scale */
                     /* everything after sf[40]: one 16-B store */
                     *(uint4 *)((uint8_t *)&meta[u] + 40) = *(const uint4 *)((const uint8_t *)&m + 40);
                 }
@@ -729,14 +829,14 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                 m.block_type = (uint8_t)(ws ? (side >> 28) & 3 : 0);
                 m.mixed = (uint8_t)(ws && ((side >> 28) & 3) == 2 ? (side >> 27) & 1 : 0);
                 m.scalefac_scale = (uint8_t)((side >> 6) & 1);
-                m.preflag = (uint8_t)((side >> 7) & 1);
+                m.preflag = (uint8_t)(r.lsf ? 0 : (int)((side >> 7) & 1));
                 m.sbg[0] = (uint8_t)(ws ? (side >> 14) & 7 : 0);
                 m.sbg[1] = (uint8_t)(ws ? (side >> 11) & 7 : 0);
                 m.sbg[2] = (uint8_t)(ws ? (side >> 8) & 7 : 0);
                 m.nz_end = 0;
                 m.part2_3_length = 0;
                 m.used_bits = 0;
-                m.pad_ = 1;
+                m.flags = (uint16_t)(1 | (r.lsf ? ((side >> 31) & 1) << 1 : 0));
                 meta[u] = m;
             }
         }
@@ -858,13 +958,16 @@ __device__ __forceinline__ float pow43_big(int a) {
     return x * y;
 }
 
-struct SynShared {                   /* read-only, one copy per workgroup          */
-    uint32_t lvar[3][3][288];        /* tab->lvar (u16 pairs) [rate][variant]      */
+template <bool LSF> struct SynShared { /* read-only, one copy per workgroup        */
+    /* tab->lvar (u16 pairs) [rate][variant] of the variant's family: MPEG-1
+     * rates 0..2, or the six LSF rates 3..8                                */
+    uint32_t lvar[LSF ? 6 : 3][3][288];
     float ce[16][16], co[16][16];    /* matrixing A: C[2m][i], C[2m+1][i], i < 16  */
     float dw[32][16];                /* window taps per output j                   */
     float p43[256];                  /* |is|^(4/3) for |is| < 256                  */
     float w36[4][36];                /* long-block windows (x IMDCT output scale)  */
-    float isr[7][2];                 /* MPEG-1 intensity ratios                    */
+    float isr[LSF ? 32 : 7][2];      /* intensity ratios: MPEG-1 [is_pos], LSF      */
+                                     /* [intensity_scale * 16 + is_pos]            */
 };
 struct SynWave {                     /* one per wave (stream)                      */
     float buf[SYN_BUF];              /* xr -> S -> X hand-offs                     */
@@ -877,18 +980,32 @@ struct SynWave {                     /* one per wave (stream)                   
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-template <bool SRC_XR, bool F32>
+template <bool SRC_XR, bool F32, bool LSF>
 __global__ void __launch_bounds__(64 * SYN_WAVES) __attribute__((amdgpu_waves_per_eu(3, 8)))
 k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, const UnitMeta *__restrict__ meta,
         const float *__restrict__ xr_in, const uint8_t *__restrict__ xr_bt, const uint8_t *__restrict__ xr_mixed,
         const DevTables *__restrict__ tab, StreamState *__restrict__ st, void *__restrict__ pcm, int n_streams,
         int F, int xr_nch, int xr_sr) {
-    __shared__ __attribute__((aligned(16))) SynShared T;
+    __shared__ __attribute__((aligned(16))) SynShared<LSF> T;
     __shared__ __attribute__((aligned(16))) SynWave Wv[SYN_WAVES];
+    constexpr int NRATE = LSF ? 6 : 3;
+    if (!SRC_XR) {
+        /* one variant per MPEG family (StreamState.kind, fixed by k_demux):
+         * MPEG-1 takes kinds 0 / 1, LSF kind 2.  A workgroup holding no
+         * stream of its variant leaves before staging any table (the same
+         * decision in every lane: no barrier is skipped by part of it). */
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < SYN_WAVES; k++) {
+            const int sk = blockIdx.x * SYN_WAVES + k;
+            if (sk < n_streams) any |= (st[sk].kind == 2) == LSF;
+        }
+        if (!any) return;
+    }
     {
         const int tid = threadIdx.x;
-        for (int i = tid; i < 3 * 3 * 288; i += 64 * SYN_WAVES)
-            (&T.lvar[0][0][0])[i] = ((const uint32_t *)&tab->lvar[0][0][0])[i];
+        for (int i = tid; i < NRATE * 3 * 288; i += 64 * SYN_WAVES)
+            (&T.lvar[0][0][0])[i] = ((const uint32_t *)&tab->lvar[LSF ? 3 : 0][0][0])[i];
         for (int i = tid; i < 256; i += 64 * SYN_WAVES) {
             const int r = i >> 4, c = i & 15;
             T.ce[r][c] = tab->dct_c[2 * r][c];
@@ -897,12 +1014,15 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
         }
         for (int i = tid; i < 32 * 16; i += 64 * SYN_WAVES) (&T.dw[0][0])[i] = (&tab->dwin[0][0])[i];
         for (int i = tid; i < 4 * 36; i += 64 * SYN_WAVES) (&T.w36[0][0])[i] = (&c_win36[0][0])[i];
-        if (tid < 14) (&T.isr[0][0])[tid] = (&c_is_ratio[0][0])[tid];
+        if (LSF) {
+            if (tid < 64) (&T.isr[0][0])[tid] = (&c_is_lsf[0][0][0])[tid];
+        } else if (tid < 14) (&T.isr[0][0])[tid] = (&c_is_ratio[0][0])[tid];
         __syncthreads();
     }
     const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); /* wave-uniform (SGPR) */
     const int s = blockIdx.x * SYN_WAVES + wid;
     if (s >= n_streams) return; /* after the only workgroup barrier */
+    if (!SRC_XR && (st[s].kind == 2) != LSF) return; /* the other variant's stream */
     SynWave &Wd = Wv[wid];
     float *const sBuf = Wd.buf;
     const int lane = threadIdx.x & 63;
@@ -985,13 +1105,13 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                 continue;
             }
             nch = (int)(r5 >> 24);
-            sr = (int)((r6 >> 16) & 3u);
+            sr = (int)((r6 >> 16) & 15u) - (LSF ? 3 : 0); /* FrameRec.sr_idx in the family */
             mode = (int)(r5 >> 22) & 3;
             mext = (int)(r5 >> 20) & 3;
         }
         const bool active = ch < nch;
         const uint32_t(*lvar)[288] = T.lvar[sr];
-        for (int gr = 0; gr < 2; gr++) {
+        for (int gr = 0; gr < (LSF ? 1 : 2); gr++) { /* LSF: one granule per frame */
             /* lane-derived indices are re-derived from an opaque copy each
              * granule so they are not hoisted and held live across the loop */
             const int lane = opaque((int)(threadIdx.x & 63));
@@ -1115,6 +1235,8 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                      * its highest nonzero band (per window) decide the IS bands
                      * (FFmpeg compute_stereo; oracle/mp3_oracle.c orc_stereo).
                      * nzR bit = right-channel band idx holding a nonzero line. */
+                    /* no intensity for is_pos >= 7 (MPEG-1), >= 16 (LSF, FFmpeg) */
+                    constexpr int IS_ILLEGAL = LSF ? 16 : 7;
                     uint64_t nzR = 0;
 #pragma unroll
                     for (int i = 0; i < 5; i++) {
@@ -1128,10 +1250,11 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                     const UnitMeta &R = Wd.m[1];
                     int ip = 0xFF;
                     if (lane < 22) {
-                        if (bt1 != 2 || (mx1 && lane < 8)) {
+                        /* long bands of a mixed block: 8 (MPEG-1), 6 (LSF) */
+                        if (bt1 != 2 || (mx1 && lane < (LSF ? 6 : 8))) {
                             const int p = R.sf[lane == 21 ? 20 : lane];
                             const bool short_nz = (nzR >> 22) != 0ull;
-                            if (!short_nz && ((uint32_t)(nzR & 0x3FFFFFull) >> lane) == 0u && p < 7) ip = p;
+                            if (!short_nz && ((uint32_t)(nzR & 0x3FFFFFull) >> lane) == 0u && p < IS_ILLEGAL) ip = p;
                         }
                     } else if (lane < 61 && bt1 == 2) {
                         const int b = (lane - 22) / 3, w = lane - 22 - 3 * b;
@@ -1141,9 +1264,11 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                             /* no nonzero line in window w at bands >= b */
                             uint64_t above = 0;
                             for (int bb = b; bb < 13; bb++) above |= 1ull << (22 + 3 * bb + w);
-                            if ((nzR & above) == 0ull && p < 7) ip = p;
+                            if ((nzR & above) == 0ull && p < IS_ILLEGAL) ip = p;
                         }
                     }
+                    /* LSF: ratio row by intensity_scale (UnitMeta.flags bit 1) */
+                    if (LSF && ip != 0xFF) ip += (int)(R.flags & 2u) << 3;
                     Wd.is[lane] = (uint8_t)ip;
                     wave_sync();
 #pragma unroll
@@ -1174,7 +1299,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                 }
                 /* the next granule's loads fly during phases I, M, W (issued
                  * after cis is consumed: fewer live registers in phase Q) */
-                if (gr == 0 || f + 1 < F) prefetch(2 * f + gr + 1);
+                if (LSF ? f + 1 < F : (gr == 0 || f + 1 < F)) prefetch(LSF ? 2 * f + 2 : 2 * f + gr + 1);
                 /* scatter in (short-block reordered) position */
 #pragma unroll
                 for (int i = 0; i < 5; i++) {
@@ -1422,8 +1547,8 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
 /* k_gather_frames: segmented long-stream decode (mp3d_batch_decode_long).  */
 /* Output frame j of the long stream is frame (j - a[k]) of virtual stream  */
 /* k - k0 (k = j / L) in the batch output; copies its PCM row (16-B words)   */
-/* and frame info (zero-filled: rows without audio, the unused half of a   */
-/* mono row).  One workgroup per output frame.                              */
+/* and frame info (zero-filled: rows without audio, the unused part of a   */
+/* mono / LSF row).  One workgroup per output frame.                        */
 /* ------------------------------------------------------------------------ */
 __global__ void __launch_bounds__(256) k_gather_frames(const uint4 *__restrict__ src, uint4 *__restrict__ dst,
                                                        const DevInfo *__restrict__ isrc, DevInfo *__restrict__ idst,
@@ -1433,7 +1558,9 @@ __global__ void __launch_bounds__(256) k_gather_frames(const uint4 *__restrict__
     const int j = (k0 + k) * L + jl % L; /* global output frame                         */
     const size_t sf = (size_t)k * F + (j - a[k]);
     const DevInfo inf = isrc[sf];
-    const int lim = inf.samples == 0 ? 0 : inf.channels == 1 ? row16 / 2 : row16; /* mono: 1152 samples */
+    /* words holding audio: samples x channels of the 2304-sample row (mono
+     * 1152, LSF 576 per channel); the rest is zero-filled */
+    const int lim = inf.samples * inf.channels * row16 / 2304;
     for (int i = threadIdx.x; i < row16; i += blockDim.x)
         dst[(size_t)jl * row16 + i] = i < lim ? src[sf * row16 + i] : make_uint4(0u, 0u, 0u, 0u);
     if (idst && threadIdx.x == 0) idst[jl] = isrc[sf];
@@ -1443,7 +1570,8 @@ __global__ void __launch_bounds__(256) k_gather_frames(const uint4 *__restrict__
 /* Host-side launchers                                                       */
 /* ------------------------------------------------------------------------ */
 hipError_t upload_constants(const float *imdct12, const float *win36, const float *win12,
-                            const float *alias_cs, const float *alias_ca, const float *is_ratio, const float *pow2q) {
+                            const float *alias_cs, const float *alias_ca, const float *is_ratio, const float *pow2q,
+                            const float *is_lsf) {
     hipError_t e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_imdct12), imdct12, sizeof(float) * 6 * 6))) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_win36), win36, sizeof(float) * 4 * 36))) return e;
@@ -1452,6 +1580,7 @@ hipError_t upload_constants(const float *imdct12, const float *win36, const floa
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_alias_ca), alias_ca, sizeof(float) * 8))) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_is_ratio), is_ratio, sizeof(float) * 14))) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_pow2q), pow2q, sizeof(float) * 4))) return e;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_is_lsf), is_lsf, sizeof(float) * 64))) return e;
     return hipSuccess;
 }
 
@@ -1478,17 +1607,25 @@ void launch_huffman(const uint8_t *md, const uint64_t *md_off, const FrameRec *r
 void launch_synth(const FrameRec *rec, const int16_t *is_buf, const UnitMeta *meta, const DevTables *tab,
                   StreamState *st, void *pcm, bool f32, int n_streams, int F, hipStream_t strm) {
     const dim3 grid((n_streams + SYN_WAVES - 1) / SYN_WAVES), block(64 * SYN_WAVES);
-    if (f32)
-        hipLaunchKernelGGL((k_synth<false, true>), grid, block, 0, strm, rec, is_buf, meta, (const float *)nullptr,
-                           (const uint8_t *)nullptr, (const uint8_t *)nullptr, tab, st, pcm, n_streams, F, 2, 0);
-    else
-        hipLaunchKernelGGL((k_synth<false, false>), grid, block, 0, strm, rec, is_buf, meta, (const float *)nullptr,
-                           (const uint8_t *)nullptr, (const uint8_t *)nullptr, tab, st, pcm, n_streams, F, 2, 0);
+    /* both family variants; a workgroup without a stream of its variant
+     * exits after SYN_WAVES scalar loads (the LSF launch on an all-MPEG-1
+     * batch costs only its workgroup dispatch) */
+#define MP3D_SYNTH_LAUNCH(F32_, LSF_)                                                                            \
+    hipLaunchKernelGGL((k_synth<false, F32_, LSF_>), grid, block, 0, strm, rec, is_buf, meta, (const float *)nullptr, \
+                       (const uint8_t *)nullptr, (const uint8_t *)nullptr, tab, st, pcm, n_streams, F, 2, 0)
+    if (f32) {
+        MP3D_SYNTH_LAUNCH(true, false);
+        MP3D_SYNTH_LAUNCH(true, true);
+    } else {
+        MP3D_SYNTH_LAUNCH(false, false);
+        MP3D_SYNTH_LAUNCH(false, true);
+    }
+#undef MP3D_SYNTH_LAUNCH
 }
 
 void launch_synth_xr(const float *xr, const uint8_t *bt, const uint8_t *mixed, const DevTables *tab, StreamState *st,
                      int16_t *pcm, int n_streams, int F, int nch, int sr, hipStream_t strm) {
-    hipLaunchKernelGGL((k_synth<true, false>), dim3((n_streams + SYN_WAVES - 1) / SYN_WAVES), dim3(64 * SYN_WAVES), 0,
+    hipLaunchKernelGGL((k_synth<true, false, false>), dim3((n_streams + SYN_WAVES - 1) / SYN_WAVES), dim3(64 * SYN_WAVES), 0,
                        strm, (const FrameRec *)nullptr, (const int16_t *)nullptr, (const UnitMeta *)nullptr, xr, bt,
                        mixed, tab, st, (void *)pcm, n_streams, F, nch, sr);
 }

@@ -35,7 +35,8 @@ def oracle_pcm16(data):
 @pytest.mark.parametrize("name", _golden.names())
 def test_golden_cases_batch_api(name):
     data, ref = _golden.case(name)
-    nf = max(ref.shape[1] // 1152, _golden.manifest()[name].get("our_frames") or 0)
+    spf = _golden.manifest()[name].get("spf", 1152)
+    nf = max(ref.shape[1] // spf, _golden.manifest()[name].get("our_frames") or 0)
     dec = mp3_amd.BatchDecoder(1, nf + 4)
     # whole file as one stream; ID3v2 + Info frame handled on the device
     pcm, infos = dec.decode(np.frombuffer(data, np.uint8), [0], [len(data)], nf + 4)
