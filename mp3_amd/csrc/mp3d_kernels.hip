@@ -930,6 +930,7 @@ __device__ __forceinline__ void imdct36_w(const float *X, float *w) {
 #define XROW 36      /* LDS row stride of X: 16-B rows, conflict-free b128 writes */
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 /* Opaque copy of a loop-invariant LDS index: keeps the compiler from
  * hoisting one address VGPR per unrolled access out of the frame loop
@@ -1473,20 +1474,26 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                 /* output slots in pairs (t0, t1): lanes 0-31 hold L, lanes
                  * 32-63 R; one half-wave swap leaves lane j with (L, R) of
                  * slot t0 and lane 32 + j with (L, R) of slot t1 */
-                auto out_at = [&](int t) {
-                    float o = 0.f;
+                /* two output slots (2 tp, 2 tp + 1) at once: packed FMAs
+                 * (v_pk_fma_f32, tap broadcast), half the VALU issues of the
+                 * scalar form; the same fma order per slot, so bit-identical */
+                auto out2 = [&](int tp) {
+                    f32x2 o = {0.f, 0.f};
 #pragma unroll
                     for (int i = 0; i < 8; i++) {
-                        const int sa = t - 2 * i, sbb = t - 2 * i - 1;
-                        const float va = sa >= 0 ? xa[sa] : ha[sa + 14];
-                        const float vb = sbb >= 0 ? xb[sbb] : hb[sbb + 15];
-                        o = fmaf(Dw[2 * i], va, o);
-                        o = fmaf(Dw[2 * i + 1], vb, o);
+                        const int ka = 2 * tp - 2 * i, kb = ka - 1;
+                        f32x2 va, vb;
+                        va.x = ka >= 0 ? xa[ka] : ha[ka + 14];
+                        va.y = ka + 1 >= 0 ? xa[ka + 1] : ha[ka + 15];
+                        vb.x = kb >= 0 ? xb[kb] : hb[kb + 15];
+                        vb.y = kb + 1 >= 0 ? xb[kb + 1] : hb[kb + 16];
+                        o = __builtin_elementwise_fma((f32x2){Dw[2 * i], Dw[2 * i]}, va, o);
+                        o = __builtin_elementwise_fma((f32x2){Dw[2 * i + 1], Dw[2 * i + 1]}, vb, o);
                     }
                     return o;
                 };
-                auto pcm_at = [&](int t) {
-                    const float p = rintf(out_at(t) * 32768.f);
+                auto to_pcm = [&](float v) {
+                    const float p = rintf(v * 32768.f);
                     return (int)fminf(fmaxf(p, -32768.f), 32767.f);
                 };
                 const int so = f * 2304 * PB + gr * 576 * nch * PB;
@@ -1497,24 +1504,28 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                         const int vo = opaque((sb + 32 * ch) * 8);
 #pragma unroll
                         for (int tp = 0; tp < 9; tp++) {
-                            const float o0 = out_at(2 * tp), o1 = out_at(2 * tp + 1);
-                            const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(o0), __float_as_uint(o1),
+                            const f32x2 o = out2(tp);
+                            const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(o.x), __float_as_uint(o.y),
                                                                             false, false);
                             __builtin_amdgcn_raw_buffer_store_b64((u32x2){r[0], r[1]}, r_pcm, vo + 512 * tp, so, 0);
                         }
                     } else {
                         const int vo = opaque(sb * 4);
 #pragma unroll
-                        for (int t = 0; t < 18; t++) {
-                            const float o = out_at(t);
-                            if (active) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), r_pcm, vo + 128 * t, so, 0);
+                        for (int tp = 0; tp < 9; tp++) {
+                            const f32x2 o = out2(tp);
+                            if (active) {
+                                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o.x), r_pcm, vo + 256 * tp, so, 0);
+                                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o.y), r_pcm, vo + 256 * tp + 128, so, 0);
+                            }
                         }
                     }
                 } else if (nch == 2) {
                     const int vo = opaque((sb + 32 * ch) * 4);
 #pragma unroll
                     for (int tp = 0; tp < 9; tp++) {
-                        const int p0 = pcm_at(2 * tp), p1 = pcm_at(2 * tp + 1);
+                        const f32x2 o = out2(tp);
+                        const int p0 = to_pcm(o.x), p1 = to_pcm(o.y);
                         const auto r = __builtin_amdgcn_permlane32_swap(p0, p1, false, false);
                         __builtin_amdgcn_raw_buffer_store_b32(((uint32_t)r[0] & 0xFFFFu) | ((uint32_t)r[1] << 16),
                                                               r_pcm, vo + 256 * tp, so, 0);
@@ -1522,9 +1533,12 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                 } else {
                     const int vo = opaque(sb * 2);
 #pragma unroll
-                    for (int t = 0; t < 18; t++) {
-                        const int p = pcm_at(t);
-                        if (active) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)p, r_pcm, vo + 64 * t, so, 0);
+                    for (int tp = 0; tp < 9; tp++) {
+                        const f32x2 o = out2(tp);
+                        if (active) {
+                            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)to_pcm(o.x), r_pcm, vo + 128 * tp, so, 0);
+                            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)to_pcm(o.y), r_pcm, vo + 128 * tp + 64, so, 0);
+                        }
                     }
                 }
 #pragma unroll
