@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MP3D_ABI_VERSION 2
+#define MP3D_ABI_VERSION 3
 
 #if defined(__GNUC__) || defined(__clang__)
 #define MP3D_API __attribute__((visibility("default")))
@@ -107,6 +107,18 @@ MP3D_API int mp3d_batch_decode_f32(mp3d_batch *b, const uint8_t *frames, const u
                           const uint32_t *sizes, int n_streams, int frames_per_stream, float *pcm,
                           mp3d_frame_info *infos, void *hip_stream);
 MP3D_API int mp3d_batch_sync(mp3d_batch *b);
+
+/* ---- decode options (ABI v3) --------------------------------------------- *
+ * MP3D_OPT_CRC_CHECK: verify the CRC-16 of error-protected frames (ISO
+ *   11172-3 2.4.3.1: polynomial 0x8005 over header bytes 2..3 and the side
+ *   info) and drop a frame whose CRC mismatches, like a bad frame
+ *   (info.samples = 0; the bit reservoir restarts from the frame's own
+ *   bytes).  FFmpeg behaves so with err_detect = crccheck + explode; its
+ *   default, and this library's, ignores the CRC.
+ * Options apply to later decode calls of the handle.                        */
+#define MP3D_OPT_CRC_CHECK 1
+MP3D_API int mp3d_batch_set_options(mp3d_batch *b, int flags);
+MP3D_API int mp3d_dec_set_options(mp3d_dec *dec, int flags);
 
 /* ---- staged entry points (parity taps / BASELINE config 2) ------------- *
  * huffman_only: run demux + reservoir + scalefactors + Huffman and return

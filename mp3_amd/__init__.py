@@ -47,7 +47,9 @@ EXPORTS = ["mp3d_dec_create", "mp3d_dec_create_on", "mp3d_dec_destroy", "mp3d_de
            "mp3d_batch_huffman_only", "mp3d_batch_synth_only", "mp3d_strerror", "mp3d_last_hip_error",
            "mp3d_abi_version", "mp3d_batch_set_timing", "mp3d_batch_kernel_times", "mp3d_batch_stream_info",
            "mp3d_dec_stream_info", "mp3d_batch_decode_long",
-           "mp3d_long_plan"]
+           "mp3d_long_plan", "mp3d_batch_set_options", "mp3d_dec_set_options"]
+
+OPT_CRC_CHECK = 1  # MP3D_OPT_CRC_CHECK: drop frames whose CRC-16 mismatches
 
 _lib = None
 
@@ -91,6 +93,8 @@ def lib():
                                              ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(StreamInfo)]
         L.mp3d_long_plan.argtypes = [ctypes.c_char_p, ctypes.c_size_t, i, ctypes.c_longlong, vp, vp,
                                      ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_int)]
+        L.mp3d_batch_set_options.argtypes = [vp, i]
+        L.mp3d_dec_set_options.argtypes = [vp, i]
         _lib = L
     return _lib
 
@@ -141,6 +145,10 @@ class Decoder:
 
     def reset(self):
         lib().mp3d_dec_reset(self._h)
+
+    def set_options(self, flags):
+        """MP3D_OPT_* flags (OPT_CRC_CHECK) for later decode calls."""
+        _check(lib().mp3d_dec_set_options(self._h, int(flags)))
 
     def decode_frame(self, buf, f32=False):
         """Returns (samples_per_channel, pcm [samples*channels], FrameInfo);
@@ -202,6 +210,10 @@ class BatchDecoder:
 
     def reset(self):
         _check(lib().mp3d_batch_reset(self._h))
+
+    def set_options(self, flags):
+        """MP3D_OPT_* flags (OPT_CRC_CHECK) for later decode calls."""
+        _check(lib().mp3d_batch_set_options(self._h, int(flags)))
 
     def sync(self):
         _check(lib().mp3d_batch_sync(self._h))

@@ -24,7 +24,7 @@ namespace mp3d {
 hipError_t upload_constants(const float *, const float *, const float *, const float *, const float *, const float *,
                             const float *, const float *);
 void launch_demux(const uint8_t *, const uint64_t *, const uint32_t *, uint8_t *, const uint64_t *, StreamState *,
-                  FrameRec *, uint64_t *, void *, int, int, hipStream_t);
+                  FrameRec *, uint64_t *, void *, int, int, int, hipStream_t);
 void launch_huffman(const uint8_t *, const uint64_t *, const FrameRec *, const uint64_t *, const DevTables *, int16_t *,
                     UnitMeta *, int, int, int, hipStream_t);
 void launch_synth(const FrameRec *, const int16_t *, const UnitMeta *, const DevTables *, StreamState *, void *, bool, int,
@@ -277,6 +277,7 @@ struct mp3d_batch {
     std::vector<uint32_t> last_len;
     int last_n = -1;
     bool timing = false;
+    int opts = 0; /* MP3D_OPT_* */
     hipEvent_t ev[4] = {};
     float times[4] = {0, 0, 0, 0};
 };
@@ -366,6 +367,12 @@ extern "C" int mp3d_batch_reset(mp3d_batch *b) {
     return MP3D_OK;
 }
 
+extern "C" int mp3d_batch_set_options(mp3d_batch *b, int flags) {
+    if (!b || (flags & ~MP3D_OPT_CRC_CHECK)) return MP3D_E_ARG;
+    b->opts = flags;
+    return MP3D_OK;
+}
+
 extern "C" int mp3d_batch_sync(mp3d_batch *b) {
     if (!b) return MP3D_E_ARG;
     HIPCHK(hipSetDevice(b->device));
@@ -439,7 +446,8 @@ static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offse
     DeviceCtx &dc = g_dev[b->device];
     if (b->timing) HIPCHK(hipEventRecord(b->ev[0], s));
     /* demux + main-data gather in one pass */
-    launch_demux(din, b->d_in_off, b->d_in_len, b->md, b->d_md_off, b->st, b->rec, b->sideu, b->d_infos, n, F, s);
+    launch_demux(din, b->d_in_off, b->d_in_len, b->md, b->d_md_off, b->st, b->rec, b->sideu, b->d_infos, n, F,
+                 b->opts, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[1], s));
     launch_huffman(b->md, b->d_md_off, b->rec, b->sideu, dc.tables, b->is_buf, b->meta, n, F, dc.n_cu, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[2], s));
@@ -819,6 +827,11 @@ extern "C" void mp3d_dec_reset(mp3d_dec *d) {
     (void)mp3d_batch_reset(d->b);
     d->frames = 0;
     d->kind = 0;
+}
+
+extern "C" int mp3d_dec_set_options(mp3d_dec *d, int flags) {
+    if (!d) return MP3D_E_ARG;
+    return mp3d_batch_set_options(d->b, flags);
 }
 
 extern "C" int mp3d_dec_stream_info(mp3d_dec *d, mp3d_stream_info *out) {

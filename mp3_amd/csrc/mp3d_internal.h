@@ -21,6 +21,9 @@
 #define MP3D_RES_BYTES 512       /* carried main-data history per stream   */
 #define MP3D_FIFO_SLOTS 15       /* synthesis history slots carried        */
 #define MP3D_MAX_FRAME_BYTES 1441
+#ifndef MP3D_OPT_CRC_CHECK
+#define MP3D_OPT_CRC_CHECK 1     /* = include/mp3d.h (the kernels do not include it) */
+#endif
 #define MP3D_TAG_SEEN (1u << 31)
 #define MP3D_TAG_LAME (1u << 30)
 #define MP3D_TAG_FRAMES (1u << 29)

@@ -114,6 +114,21 @@ __device__ __forceinline__ uint64_t win_bits64(const HdrWin &w, uint32_t b) {
     return sh ? (hi << sh) | ((uint64_t)x2 >> (32 - sh)) : hi;
 }
 
+/* CRC-16 of a protected frame in the header window (ISO 11172-3 2.4.3.1;
+ * FFmpeg handle_crc, AV_CRC_16_ANSI: polynomial 0x8005, MSB first, initial
+ * 0xFFFF) over header bytes 2..3 and the side info, against bytes 4..5.
+ * Wave-uniform bytes, so the loop runs on the scalar unit; opt-in only. */
+__device__ bool crc16_ok(const HdrWin &w, uint32_t side_bytes) {
+    uint32_t crc = 0xFFFFu;
+    for (uint32_t i = 2; i < 6u + side_bytes; i++) {
+        if (i == 4) i = 6; /* the stored CRC is not covered */
+        crc ^= win_byte(w, i) << 8;
+#pragma unroll
+        for (int k = 0; k < 8; k++) crc = (crc & 0x8000u) ? ((crc << 1) ^ 0x8005u) & 0xFFFFu : (crc << 1) & 0xFFFFu;
+    }
+    return crc == ((win_byte(w, 4) << 8) | win_byte(w, 5));
+}
+
 /* Xing/Info tag + LAME encoder extension of a stream's first frame, as
  * FFmpeg's demuxer reads it (libavformat/mp3dec.c mp3_parse_info_tag):
  * "Xing"/"Info", BE32 flags, optional frame count (1), byte count (2), TOC
@@ -151,7 +166,7 @@ __global__ void __launch_bounds__(64) k_demux(const uint8_t *__restrict__ in, co
                                               const uint32_t *__restrict__ in_len, uint8_t *__restrict__ md,
                                               const uint64_t *__restrict__ md_off, StreamState *__restrict__ st,
                                               FrameRec *__restrict__ rec, uint64_t *__restrict__ sideu,
-                                              DevInfo *__restrict__ infos, int F) {
+                                              DevInfo *__restrict__ infos, int F, int opts) {
     const int s = blockIdx.x;
     const int lane = threadIdx.x;
     const uint8_t *p0 = in + in_off[s];
@@ -259,7 +274,10 @@ __global__ void __launch_bounds__(64) k_demux(const uint8_t *__restrict__ in, co
                 p23[0][1] = __builtin_amdgcn_readlane((int)myp23, 1);
                 p23[1][0] = __builtin_amdgcn_readlane((int)myp23, 2);
                 p23[1][1] = __builtin_amdgcn_readlane((int)myp23, 3);
-                const bool bad = plen < 0 || __ballot(mybad) != 0ull;
+                /* MP3D_OPT_CRC_CHECK: a protected frame whose CRC-16 mismatches
+                 * is dropped like a bad one (FFmpeg handle_crc + explode) */
+                const bool crc_bad = (opts & MP3D_OPT_CRC_CHECK) && crc && !crc16_ok(w, (uint32_t)side_bytes);
+                const bool bad = plen < 0 || __ballot(mybad) != 0ull || crc_bad;
                 const uint32_t tgo = 4u + (uint32_t)crc + (uint32_t)side_bytes;
                 const bool tag = stream_start && f == 0 && plen >= 4 && have == (uint32_t)fb &&
                                  ((win_byte(w, tgo) == 'X' && win_byte(w, tgo + 1) == 'i' && win_byte(w, tgo + 2) == 'n' &&
@@ -1600,9 +1618,9 @@ hipError_t upload_constants(const float *imdct12, const float *win36, const floa
 
 void launch_demux(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len, uint8_t *md,
                   const uint64_t *md_off, StreamState *st, FrameRec *rec, uint64_t *sideu, void *infos, int n_streams,
-                  int F, hipStream_t strm) {
+                  int F, int opts, hipStream_t strm) {
     hipLaunchKernelGGL(k_demux, dim3(n_streams), dim3(64), 0, strm, in, in_off, in_len, md, md_off, st, rec, sideu,
-                       (DevInfo *)infos, F);
+                       (DevInfo *)infos, F, opts);
 }
 
 void launch_huffman(const uint8_t *md, const uint64_t *md_off, const FrameRec *rec, const uint64_t *sideu,

@@ -234,7 +234,13 @@ typedef struct {
     orc_side side;
     orc_hdr hdr;
     int frames;
+    int opts; /* ORC_OPT_* (orc_set_options) */
 } orc_dec;
+
+/* Option: verify the CRC-16 of protected frames; a mismatch drops the
+ * frame (FFmpeg with err_detect = crccheck + explode; its default -- and so
+ * the golden decoder's -- ignores the CRC). */
+#define ORC_OPT_CRC_CHECK 1
 
 typedef struct {
     int frame_bytes, channels, hz, layer, bitrate_kbps;
@@ -245,7 +251,28 @@ ORC_API orc_dec *orc_create(void) {
     return (orc_dec *)calloc(1, sizeof(orc_dec));
 }
 ORC_API void orc_destroy(orc_dec *d) { free(d); }
-ORC_API void orc_reset(orc_dec *d) { memset(d, 0, sizeof(*d)); }
+ORC_API void orc_reset(orc_dec *d) {
+    const int opts = d->opts;
+    memset(d, 0, sizeof(*d));
+    d->opts = opts;
+}
+ORC_API void orc_set_options(orc_dec *d, int opts) { d->opts = opts; }
+
+/* CRC-16 of a protected frame (ISO 11172-3 2.4.3.1; FFmpeg handle_crc with
+ * AV_CRC_16_ANSI: polynomial 0x8005, MSB first, initial 0xFFFF) over header
+ * bytes 2..3 and the side info, checked against the stored bytes 4..5. */
+static int orc_crc_ok(const uint8_t *buf, int side_bytes) {
+    unsigned crc = 0xFFFF;
+    for (int i = 2; i < 6 + side_bytes; i++) {
+        if (i == 4) i = 6; /* the stored CRC itself is not covered */
+        for (int k = 7; k >= 0; k--) {
+            const unsigned bit = ((buf[i] >> k) & 1u) ^ ((crc >> 15) & 1u);
+            crc = (crc << 1) & 0xFFFFu;
+            if (bit) crc ^= 0x8005u;
+        }
+    }
+    return crc == (((unsigned)buf[4] << 8) | buf[5]);
+}
 ORC_API int orc_state_bytes(void) { return (int)sizeof(orc_dec); }
 
 /* ------------------------------------------------------------------------ */
@@ -626,9 +653,10 @@ ORC_API int orc_decode_frame_f64(orc_dec *d, const uint8_t *buf, int bytes, doub
     const uint8_t *side = buf + 4 + h.crc_bytes;
     orc_side *s = &d->side;
     orc_parse_side(side, &h, s);
+    const int crc_bad = (d->opts & ORC_OPT_CRC_CHECK) && h.crc_bytes && !orc_crc_ok(buf, h.side_bytes);
     for (int gr = 0; gr < h.ngr; gr++)
         for (int ch = 0; ch < h.nch; ch++)
-            if (s->gr[gr][ch].big_values > 288) {
+            if (crc_bad || s->gr[gr][ch].big_values > 288) {
                 /* dropped; FFmpeg mp_decode_frame then keeps
                  * the frame's last min(BACKSTEP_SIZE = 512, bytes - 4) post-
                  * header bytes as the whole reservoir */
@@ -822,9 +850,10 @@ ORC_API int orc_parse_info_tag(const uint8_t *buf, long len, int *out) {
  * frame).  Skips an ID3v2 tag and a leading Xing/Info frame (as FFmpeg's
  * demuxer).  Returns audio frames decoded; *samples_out = samples per
  * channel written. */
-ORC_API long orc_decode_stream_n(const uint8_t *buf, long len, float *pcm, long max_frames, int *nch_out, int *hz_out,
-                                 long *samples_out) {
+ORC_API long orc_decode_stream_opts(const uint8_t *buf, long len, float *pcm, long max_frames, int *nch_out,
+                                    int *hz_out, long *samples_out, int opts) {
     orc_dec *d = orc_create();
+    d->opts = opts;
     long pos = orc_skip_id3v2(buf, len);
     long nf = 0, ns = 0;
     int first = 1;
@@ -863,6 +892,11 @@ ORC_API long orc_decode_stream_n(const uint8_t *buf, long len, float *pcm, long 
     if (samples_out) *samples_out = ns;
     orc_destroy(d);
     return nf;
+}
+
+ORC_API long orc_decode_stream_n(const uint8_t *buf, long len, float *pcm, long max_frames, int *nch_out, int *hz_out,
+                                 long *samples_out) {
+    return orc_decode_stream_opts(buf, len, pcm, max_frames, nch_out, hz_out, samples_out, 0);
 }
 
 ORC_API long orc_decode_stream(const uint8_t *buf, long len, float *pcm, long max_frames, int *nch_out, int *hz_out) {

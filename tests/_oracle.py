@@ -35,6 +35,9 @@ def lib():
                                           ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                           ctypes.POINTER(ctypes.c_long)]
         L.orc_decode_stream_n.restype = ctypes.c_long
+        L.orc_decode_stream_opts.argtypes = L.orc_decode_stream_n.argtypes + [ctypes.c_int]
+        L.orc_decode_stream_opts.restype = ctypes.c_long
+        L.orc_set_options.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.orc_is_info_frame.argtypes = [ctypes.c_char_p, ctypes.c_long]
         L.orc_synth_only.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
@@ -56,23 +59,27 @@ def info_tag(data: bytes):
     return bool(found), d
 
 
-def decode_stream(data: bytes, max_frames=100000):
+OPT_CRC_CHECK = 1  # ORC_OPT_CRC_CHECK: drop frames whose CRC-16 mismatches
+
+
+def decode_stream(data: bytes, max_frames=100000, opts=0):
     """Planar float32 [nch, samples] (ID3v2 and Xing/Info frame skipped;
     1152 samples per MPEG-1 frame, 576 per MPEG-2/2.5 frame)."""
     L = lib()
     out = np.zeros((2, max_frames * 1152), np.float32)
     nch, hz, ns = ctypes.c_int(), ctypes.c_int(), ctypes.c_long()
-    L.orc_decode_stream_n(data, len(data), out.ctypes.data, max_frames, ctypes.byref(nch), ctypes.byref(hz),
-                          ctypes.byref(ns))
+    L.orc_decode_stream_opts(data, len(data), out.ctypes.data, max_frames, ctypes.byref(nch), ctypes.byref(hz),
+                             ctypes.byref(ns), int(opts))
     return out[: nch.value, : ns.value], hz.value
 
 
 class Decoder:
     """Per-frame oracle decoder with parity taps."""
 
-    def __init__(self):
+    def __init__(self, opts=0):
         self.L = lib()
         self.d = self.L.orc_create()
+        self.L.orc_set_options(self.d, int(opts))
 
     def __del__(self):
         try:

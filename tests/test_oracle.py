@@ -92,3 +92,57 @@ def test_oracle_no_tag_no_trim():
     data, _ = _golden.case("c3_s0")
     found, tag = _oracle.info_tag(data)
     assert not found and not tag["has_lame"] and tag["skip_samples"] == 0
+
+
+def _crc16_cms(data: bytes, crc=0xFFFF):
+    """CRC-16 with polynomial 0x8005, MSB first, initial 0xFFFF, no final
+    xor (the catalogued CRC-16/CMS; FFmpeg AV_CRC_16_ANSI seeded 0xFFFF)."""
+    for byte in data:
+        crc ^= byte << 8
+        for _ in range(8):
+            crc = ((crc << 1) ^ 0x8005) & 0xFFFF if crc & 0x8000 else (crc << 1) & 0xFFFF
+    return crc
+
+
+def _corrupt_crc(data, offs, frames):
+    b = bytearray(data)
+    for f in frames:
+        b[int(offs[f]) + 5] ^= 0x5A
+    return bytes(b)
+
+
+CRC_CFG = dict(_gen.C5, crc_pct=100)
+
+
+def test_crc16_known_answer_and_generator_crcs():
+    """The CRC recipe matches the catalogue check value, and every frame the
+    generator protects carries the CRC of its header bytes 2..3 + side info
+    (ISO 11172-3 2.4.3.1) -- so the option below is pinned independently of
+    the oracle's own implementation."""
+    assert _crc16_cms(b"123456789") == 0xAEE7
+    for cfg, seed in [(CRC_CFG, 31), (dict(CRC_CFG, sr_idx=-2), 32)]:
+        data, offs = _gen.stream(cfg, seed, 10)
+        for o in offs:
+            o = int(o)
+            assert data[o + 1] & 1 == 0  # protection bit 0 = CRC present
+            lsf = (data[o + 1] >> 3) & 3 != 3
+            mono = data[o + 3] >> 6 == 3
+            side = (9 if mono else 17) if lsf else (17 if mono else 32)
+            crc = _crc16_cms(data[o + 2:o + 4] + data[o + 6:o + 6 + side])
+            assert crc == (data[o + 4] << 8 | data[o + 5])
+
+
+def test_oracle_crc_option_drops_bad_frames():
+    """ORC_OPT_CRC_CHECK: frames with a corrupted CRC are dropped (FFmpeg
+    err_detect=crccheck+explode); without the option the CRC is ignored
+    (FFmpeg's default, the golden decoder's behaviour)."""
+    data, offs = _gen.stream(CRC_CFG, 33, 12)
+    bad = _corrupt_crc(data, offs, [3, 7])
+    ref, _ = _oracle.decode_stream(data)
+    ign, _ = _oracle.decode_stream(bad)
+    assert np.array_equal(ign, ref)
+    chk, _ = _oracle.decode_stream(bad, opts=_oracle.OPT_CRC_CHECK)
+    assert chk.shape[1] == ref.shape[1] - 2 * 1152
+    assert np.array_equal(chk[:, :3 * 1152], ref[:, :3 * 1152])
+    clean, _ = _oracle.decode_stream(data, opts=_oracle.OPT_CRC_CHECK)
+    assert np.array_equal(clean, ref)
