@@ -51,7 +51,9 @@ def main():
         if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
             cs["hbm_bytes_per_launch"] = (2 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024.0
     (dst / (a.tag + "_pmc.json")).write_text(json.dumps(out, indent=1, sort_keys=True))
-    synth = out.get("k_synth<false>", {})
+    # the MPEG-1 int16 decode variant (k_synth<SRC_XR=false, F32=false, LSF=false>)
+    key = next((k for k in out if k.replace(" ", "") in ("k_synth<false,false,false>", "k_synth<false>")), None)
+    synth = out.get(key, {})
     if "hbm_bytes_per_launch" in synth:
         (dst / "pmc_traffic.json").write_text(json.dumps({
             "tag": a.tag, "streams": a.streams, "frames": a.frames,
