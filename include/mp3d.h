@@ -140,7 +140,7 @@ MP3D_API int mp3d_batch_synth_only(mp3d_batch *b, const float *xr, const uint8_t
  * (libavformat/mp3dec.c): with a LAME / Lavf / Lavc encoder extension the
  * first enc_delay + 529 decoded samples per channel are encoder/decoder
  * delay, and when the tag also carries a frame count, samples from
- * total_frames * 1152 + 529 - enc_padding on are padding.  The decoder
+ * total_frames * 1152 (576 for MPEG-2/2.5 LSF) + 529 - enc_padding on are padding.  The decoder
  * always emits every decoded frame; apply the trim when concatenating.      */
 typedef struct mp3d_stream_info {
     int has_tag;          /* a Xing/Info frame opened the stream               */
