@@ -19,10 +19,10 @@
 #include "../../include/mp3d.h"
 #include "mp3d_internal.h"
 #include "mp3d_tables.h"
+#include "mp3d_consts.h"
 
 namespace mp3d {
-hipError_t upload_constants(const float *, const float *, const float *, const float *, const float *, const float *,
-                            const float *, const float *);
+hipError_t upload_constants(const float *, const float *, const float *, const float *);
 void launch_demux(const uint8_t *, const uint64_t *, const uint32_t *, uint8_t *, const uint64_t *, StreamState *,
                   FrameRec *, uint64_t *, void *, int, int, int, hipStream_t);
 void launch_huffman(const uint8_t *, const uint64_t *, const FrameRec *, const uint64_t *, const DevTables *, int16_t *,
@@ -214,7 +214,16 @@ static int upload_symbols() {
     for (int i = 0; i < 4; i++) p2q[i] = (float)pow(2.0, i / 4.0);
     for (int i = 0; i < 22; i++)
         if (((MP3D_PRETAB_BITS >> (2 * i)) & 3u) != MP3D_PRETAB[i]) return MP3D_E_ARG; /* table drift */
-    HIPCHK(upload_constants(&imdct12[0][0], &win36[0][0], win12, cs, ca, &isr[0][0], p2q, &isl[0][0][0]));
+    /* the kernel's literal tables (mp3d_consts.h, tools/gen_consts.py) must
+     * equal this recipe bit for bit */
+    for (int k = 0; k < 6; k++)
+        for (int o = 0; o < 6; o++)
+            if (imdct12[k][o] != MP3D_K_IMDCT12[k][o]) return MP3D_E_ARG;
+    for (int i = 0; i < 12; i++)
+        if (win12[i] != MP3D_K_WIN12[i]) return MP3D_E_ARG;
+    for (int i = 0; i < 8; i++)
+        if (cs[i] != MP3D_K_ALIAS_CS[i] || ca[i] != MP3D_K_ALIAS_CA[i]) return MP3D_E_ARG;
+    HIPCHK(upload_constants(&win36[0][0], &isr[0][0], p2q, &isl[0][0][0]));
     return MP3D_OK;
 }
 

@@ -19,17 +19,14 @@
 
 #include "mp3d_internal.h"
 #include "mp3d_tables.h"
+#include "mp3d_consts.h" /* IMDCT-12 / short window / alias coefficients as literals */
 
 namespace mp3d {
 
 /* ------------------------------------------------------------------------ */
 /* Constant-memory tables (uniform access -> scalar loads)                   */
 /* ------------------------------------------------------------------------ */
-__constant__ float c_imdct12[6][6];   /* [k][o]: o<3 -> out o, o>=3 -> out 6+(o-3)   */
 __constant__ float c_win36[4][36];    /* long windows x IMDCT output scale (imdct36_w) */
-__constant__ float c_win12[12];
-__constant__ float c_alias_cs[8];
-__constant__ float c_alias_ca[8];
 __constant__ float c_is_ratio[7][2];  /* MPEG-1 intensity: k/(1+k), 1/(1+k) */
 __constant__ float c_pow2q[4];        /* 2^(i/4) */
 __constant__ float c_is_lsf[2][16][2];/* LSF intensity [intensity_scale][is_pos]: L, R */
@@ -1369,8 +1366,8 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
 #pragma unroll
                 for (int k = 0; k < 8; k++) {
                     const float lo = x[17 - k], hi = x[k];
-                    if (upper) x[k] = hi * c_alias_cs[k] + up[k] * c_alias_ca[k];
-                    if (lower) x[17 - k] = lo * c_alias_cs[k] - dn[k] * c_alias_ca[k];
+                    if (upper) x[k] = hi * MP3D_K_ALIAS_CS[k] + up[k] * MP3D_K_ALIAS_CA[k];
+                    if (lower) x[17 - k] = lo * MP3D_K_ALIAS_CS[k] - dn[k] * MP3D_K_ALIAS_CA[k];
                 }
                 const bool long_imdct = bt != 2 || (mixed && sb < 2);
                 if (long_imdct) {
@@ -1398,15 +1395,15 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                         for (int o = 0; o < 6; o++) {
                             float acc = 0.f;
 #pragma unroll
-                            for (int k = 0; k < 6; k++) acc = fmaf(x[3 * k + w], c_imdct12[k][o], acc);
+                            for (int k = 0; k < 6; k++) acc = fmaf(x[3 * k + w], MP3D_K_IMDCT12[k][o], acc);
                             h[o] = acc;
                         }
 #pragma unroll
                         for (int i = 0; i < 3; i++) {
-                            z[6 * w + i] = fmaf(h[i], c_win12[i], z[6 * w + i]);
-                            z[6 * w + 5 - i] = fmaf(-h[i], c_win12[5 - i], z[6 * w + 5 - i]);
-                            z[6 * w + 6 + i] = fmaf(h[3 + i], c_win12[6 + i], z[6 * w + 6 + i]);
-                            z[6 * w + 11 - i] = fmaf(h[3 + i], c_win12[11 - i], z[6 * w + 11 - i]);
+                            z[6 * w + i] = fmaf(h[i], MP3D_K_WIN12[i], z[6 * w + i]);
+                            z[6 * w + 5 - i] = fmaf(-h[i], MP3D_K_WIN12[5 - i], z[6 * w + 5 - i]);
+                            z[6 * w + 6 + i] = fmaf(h[3 + i], MP3D_K_WIN12[6 + i], z[6 * w + 6 + i]);
+                            z[6 * w + 11 - i] = fmaf(h[3 + i], MP3D_K_WIN12[11 - i], z[6 * w + 11 - i]);
                         }
                     }
 #pragma unroll
@@ -1601,15 +1598,9 @@ __global__ void __launch_bounds__(256) k_gather_frames(const uint4 *__restrict__
 /* ------------------------------------------------------------------------ */
 /* Host-side launchers                                                       */
 /* ------------------------------------------------------------------------ */
-hipError_t upload_constants(const float *imdct12, const float *win36, const float *win12,
-                            const float *alias_cs, const float *alias_ca, const float *is_ratio, const float *pow2q,
-                            const float *is_lsf) {
+hipError_t upload_constants(const float *win36, const float *is_ratio, const float *pow2q, const float *is_lsf) {
     hipError_t e;
-    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_imdct12), imdct12, sizeof(float) * 6 * 6))) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_win36), win36, sizeof(float) * 4 * 36))) return e;
-    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_win12), win12, sizeof(float) * 12))) return e;
-    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_alias_cs), alias_cs, sizeof(float) * 8))) return e;
-    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_alias_ca), alias_ca, sizeof(float) * 8))) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_is_ratio), is_ratio, sizeof(float) * 14))) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_pow2q), pow2q, sizeof(float) * 4))) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_is_lsf), is_lsf, sizeof(float) * 64))) return e;
