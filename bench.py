@@ -39,6 +39,9 @@ PCM_BYTES_PER_FRAME = 4608.0   # 1152 x 2 ch x int16
 # algorithmic FLOPs per stereo frame: dense 32x32 matrixing
 # + 512-tap window per slot (72 slot-channels) + IMDCT (4 units x 32 sb x 2*18*18)
 FLOP_PER_FRAME = 72 * (2 * 32 * 32 + 2 * 512) + 4 * 32 * 2 * 18 * 18
+# MFMA work of the DCT tile (phase M): 24 v_mfma_f32_16x16x4_f32 (2 048 flop
+# each) per granule, 2 granules per frame -- the butterfly-halved matrixing
+MFMA_FLOP_PER_FRAME = 2 * 24 * 2048
 # k_synth algorithmic bytes per frame: is[] int16 in (4 x 576 x 2) + PCM out
 SYNTH_BYTES_PER_FRAME = 4 * 576 * 2 + PCM_BYTES_PER_FRAME
 
@@ -163,15 +166,16 @@ def main():
     flops = FLOP_PER_FRAME * frames_per_launch
     achieved_tf = flops / synth_s / 1e12 if synth_s > 0 else 0.0
 
-    traffic = None
+    traffic = mfma_util = None
     prof = ROOT / "profiles" / "pmc_traffic.json"
     if prof.exists():
         try:
             pj = json.loads(prof.read_text())
             if pj.get("streams") == n and pj.get("frames") == F:
                 traffic = pj.get("k_synth_hbm_bytes_per_launch")
+                mfma_util = pj.get("k_synth_mfma_util")
         except Exception:
-            traffic = None
+            traffic = mfma_util = None
 
     gather = None
     if args.gather and world > 1:
@@ -212,6 +216,13 @@ def main():
                 "launch_us": kt["synth"],
                 "achieved_GBs_algorithmic": SYNTH_BYTES_PER_FRAME * frames_per_launch / synth_s / 1e9 if synth_s else 0,
                 "traffic": traffic,
+                "dct_tile": {
+                    "mfma_flop_per_frame": MFMA_FLOP_PER_FRAME,
+                    "mfma_tflops": MFMA_FLOP_PER_FRAME * frames_per_launch / synth_s / 1e12 if synth_s else 0,
+                    "mfma_util_pmc": mfma_util,
+                    "note": "matrix-core busy fraction of k_synth from rocprofv3 (SQ_VALU_MFMA_BUSY_CYCLES, "
+                            "profiles/pmc_traffic.json); peak 157.3 TFLOP/s FP32 MFMA",
+                },
             },
             "hbm": {
                 "hbm_rw_frac": value / world * (BYTES_IN_PER_FRAME + PCM_BYTES_PER_FRAME) / (HBM_PEAK_GBS * 1e9),

@@ -44,12 +44,20 @@ def main():
     dst.mkdir(exist_ok=True)
     shutil.copy(src / "stats" / "run_kernel_stats.csv", dst / (a.tag + "_kernel_stats.csv"))
     out = {}
-    for p in ("pmc_sq1", "pmc_sq2", "pmc_fetch", "pmc_write"):
+    for p in ("pmc_sq1", "pmc_sq2", "pmc_fetch", "pmc_write", "pmc_mfma"):
+        if not (src / p / "run_counter_collection.csv").exists():
+            continue
         for k, cs in counters(src / p).items():
             out.setdefault(k, {}).update(cs)
     for k, cs in out.items():
         if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
             cs["hbm_bytes_per_launch"] = (2 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024.0
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in cs and cs.get("GRBM_GUI_ACTIVE"):
+            # rocprofv3's MfmaUtil: MFMA busy cycles summed over the 1 024 SIMDs
+            # / (per-XCD GRBM_GUI_ACTIVE x SIMDs); GRBM_GUI_ACTIVE as collected
+            # here is the sum over the 8 XCDs (MI355X_MICROARCH.md, DVFS note)
+            cs["mfma_util"] = cs["SQ_VALU_MFMA_BUSY_CYCLES"] / (cs["GRBM_GUI_ACTIVE"] / 8.0 * 1024)
+            cs["mfma_f32_flop_per_launch"] = cs.get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0.0) * 512
     (dst / (a.tag + "_pmc.json")).write_text(json.dumps(out, indent=1, sort_keys=True))
     # the MPEG-1 int16 decode variant (k_synth<SRC_XR=false, F32=false, LSF=false>)
     key = next((k for k in out if k.replace(" ", "") in ("k_synth<false,false,false>", "k_synth<false>")), None)
@@ -59,6 +67,8 @@ def main():
             "tag": a.tag, "streams": a.streams, "frames": a.frames,
             "k_synth_hbm_bytes_per_launch": synth["hbm_bytes_per_launch"],
             "k_synth_fetch_kib": synth["FETCH_SIZE"], "k_synth_write_kib": synth["WRITE_SIZE"],
+            "k_synth_mfma_util": synth.get("mfma_util"),
+            "k_synth_mfma_f32_flop_per_launch": synth.get("mfma_f32_flop_per_launch"),
             "method": "2 x FETCH_SIZE + WRITE_SIZE, separate rocprofv3 --pmc passes (tools/profile.sh)"}, indent=1))
     for k, cs in sorted(out.items()):
         print(k, {c: "%.4g" % v for c, v in cs.items()})
