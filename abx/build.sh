@@ -1,0 +1,6 @@
+#!/bin/bash
+# abx/build.sh NAME [extra hipcc flags...]: build mp3_amd/csrc as abx/NAME.so (A/B experiments)
+set -e
+N=$1; shift
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -fvisibility=hidden -o abx/$N.so "$@" \
+  mp3_amd/csrc/mp3d_kernels.hip mp3_amd/csrc/mp3d_host.cpp

@@ -22,7 +22,7 @@
 #include "mp3d_consts.h"
 
 namespace mp3d {
-hipError_t upload_constants(const float *, const float *, const float *, const float *);
+hipError_t upload_constants(const float *, const float *, const float *, const float *, const uint16_t *);
 void launch_demux(const uint8_t *, const uint64_t *, const uint32_t *, uint8_t *, const uint64_t *, StreamState *,
                   FrameRec *, uint64_t *, void *, int, int, int, hipStream_t);
 void launch_huffman(const uint8_t *, const uint64_t *, const FrameRec *, const uint64_t *, const DevTables *, int16_t *,
@@ -223,7 +223,12 @@ static int upload_symbols() {
         if (win12[i] != MP3D_K_WIN12[i]) return MP3D_E_ARG;
     for (int i = 0; i < 8; i++)
         if (cs[i] != MP3D_K_ALIAS_CS[i] || ca[i] != MP3D_K_ALIAS_CA[i]) return MP3D_E_ARG;
-    HIPCHK(upload_constants(&win36[0][0], &isr[0][0], p2q, &isl[0][0][0]));
+    uint16_t fbt[9][16] = {};
+    for (int sr = 0; sr < 9; sr++)
+        for (int bi = 1; bi < 15; bi++)
+            fbt[sr][bi] = (uint16_t)((sr < 3 ? 144000 * (int)MP3D_BITRATE_L3[bi] : 72000 * (int)MP3D_BITRATE_L3_LSF[bi]) /
+                                     (int)MP3D_SAMPLE_RATE[sr]);
+    HIPCHK(upload_constants(&win36[0][0], &isr[0][0], p2q, &isl[0][0][0], &fbt[0][0]));
     return MP3D_OK;
 }
 

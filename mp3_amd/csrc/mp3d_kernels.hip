@@ -29,7 +29,12 @@ namespace mp3d {
 __constant__ float c_win36[4][36];    /* long windows x IMDCT output scale (imdct36_w) */
 __constant__ float c_is_ratio[7][2];  /* MPEG-1 intensity: k/(1+k), 1/(1+k) */
 __constant__ float c_pow2q[4];        /* 2^(i/4) */
-__constant__ float c_is_lsf[2][16][2];/* LSF intensity [intensity_scale][is_pos]: L, R */
+__constant__ float c_is_lsf[2][16][2];
+/* Layer III frame bytes without padding per (sample-rate index 0..8,
+ * bitrate index): 144000 kbps / Hz (MPEG-1), 72000 kbps / Hz (LSF); 0 for
+ * free format / bad index.  A table read instead of a scalar division in
+ * the per-frame header check. */
+__constant__ uint16_t c_frame_bytes[9][16];/* LSF intensity [intensity_scale][is_pos]: L, R */
 
 struct DevInfo { /* mirrors mp3d_frame_info (include/mp3d.h) */
     int32_t frame_bytes, channels, hz, layer, bitrate_kbps, samples;
@@ -54,11 +59,8 @@ __device__ __forceinline__ int hdr_frame_bytes(uint32_t b1, uint32_t b2, int kin
     if ((b1 & 0xE0) != 0xE0 || ((b1 >> 1) & 3) != 1 || ((b1 >> 3) & 3) == 1) return -1;
     const int bi = (int)(b2 >> 4);
     if (bi == 0 || bi == 15 || ((b2 >> 2) & 3) == 3) return -1;
-    const int k = hdr_kind(b1);
-    if (kind && k != kind) return -1;
-    const int hz = (int)MP3D_SAMPLE_RATE[hdr_sr_idx(b1, b2)];
-    return (k == 1 ? 144000 * (int)MP3D_BITRATE_L3[bi] : 72000 * (int)MP3D_BITRATE_L3_LSF[bi]) / hz +
-           (int)((b2 >> 1) & 1);
+    if (kind && hdr_kind(b1) != kind) return -1;
+    return (int)c_frame_bytes[hdr_sr_idx(b1, b2)][bi] + (int)((b2 >> 1) & 1);
 }
 
 /* bit offset of unit (gr, ch) inside the side info: MPEG-1 9-bit
@@ -1598,8 +1600,10 @@ __global__ void __launch_bounds__(256) k_gather_frames(const uint4 *__restrict__
 /* ------------------------------------------------------------------------ */
 /* Host-side launchers                                                       */
 /* ------------------------------------------------------------------------ */
-hipError_t upload_constants(const float *win36, const float *is_ratio, const float *pow2q, const float *is_lsf) {
+hipError_t upload_constants(const float *win36, const float *is_ratio, const float *pow2q, const float *is_lsf,
+                            const uint16_t *frame_bytes) {
     hipError_t e;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_frame_bytes), frame_bytes, sizeof(uint16_t) * 9 * 16))) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_win36), win36, sizeof(float) * 4 * 36))) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_is_ratio), is_ratio, sizeof(float) * 14))) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_pow2q), pow2q, sizeof(float) * 4))) return e;
