@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Build k_synth phase-ablation variants (abx/NAME.so) for A/B timing only:
+their output is wrong by construction.  Usage: python abx/variants.py"""
+import os
+import shutil
+import subprocess
+import sys
+
+SRC = open("mp3_amd/csrc/mp3d_kernels.hip").read()
+
+
+def variant(name, reps):
+    s = SRC
+    for a, b in reps:
+        assert s.count(a) >= 1, (name, a)
+        s = s.replace(a, b)
+    d = "/tmp/vars/" + name
+    os.makedirs(d, exist_ok=True)
+    for h in ["mp3d_internal.h", "mp3d_tables.h", "mp3d_consts.h"]:
+        shutil.copy("mp3_amd/csrc/" + h, d)
+    open(d + "/mp3d_kernels.hip", "w").write(s)
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
+                           "-fvisibility=hidden", "-o", "abx/%s.so" % name, d + "/mp3d_kernels.hip",
+                           "mp3_amd/csrc/mp3d_host.cpp"])
+
+
+VARS = {
+    "NI": [("""                const bool long_imdct = bt != 2 || (mixed && sb < 2);
+                if (long_imdct) {""", """                const bool long_imdct = bt != 2 || (mixed && sb < 2);
+                if (true) {
+#pragma unroll
+                    for (int i = 0; i < 18; i++) { o18[i] = x[i] + ov[i]; ov[i] = active ? x[17 - i] : ov[i]; }
+                } else if (long_imdct) {"""),
+           ("""                const bool upper = (bt != 2 && sb >= 1)""", """                const bool upper = false && (bt != 2 && sb >= 1)"""),
+           ("""                const bool lower = (bt != 2 && sb <= 30)""", """                const bool lower = false && (bt != 2 && sb <= 30)""")],
+    "NW": [("""                        o = __builtin_elementwise_fma((f32x2){Dw[2 * i], Dw[2 * i]}, va, o);
+                        o = __builtin_elementwise_fma((f32x2){Dw[2 * i + 1], Dw[2 * i + 1]}, vb, o);""",
+            """                        if (i == 0) o = va + vb;""")],
+    "NM": [("""                        ce[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ae[ks], Be[nt][ks], ce[nt], 0, 0, 0);
+                        co[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ao[ks], Bo[nt][ks], co[nt], 0, 0, 0);""",
+            """                        ce[nt][ks] = Ae[ks] * Be[nt][ks];
+                        co[nt][ks] = Ao[ks] * Bo[nt][ks];""")],
+}
+
+if __name__ == "__main__":
+    for n in (sys.argv[1:] or VARS):
+        variant(n, VARS[n])

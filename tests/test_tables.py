@@ -117,3 +117,17 @@ def test_pow43_escape_recipe():
         p = (x * y).astype(np.float32)
         ulp = np.abs(p.view(np.int32).astype(np.int64) - ref.view(np.int32))
         assert ulp.max() <= 2, (pert, int(ulp.max()))
+
+
+def test_kernel_literal_tables_match_recipe():
+    """mp3_amd/csrc/mp3d_consts.h (the k_synth IMDCT-12 / short-window /
+    alias coefficients compiled in as literals) is exactly what
+    tools/gen_consts.py renders from the ISO formulas (the library also
+    checks it against its own host recipe at init)."""
+    import importlib.util
+    import pathlib
+    root = pathlib.Path(__file__).resolve().parents[1]
+    spec = importlib.util.spec_from_file_location("gen_consts", root / "tools" / "gen_consts.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    assert (root / "mp3_amd" / "csrc" / "mp3d_consts.h").read_text() == mod.render()
