@@ -25,6 +25,11 @@ def variant(name, reps):
 
 
 VARS = {
+    "W4": [("__attribute__((amdgpu_waves_per_eu(3, 8)))", "__attribute__((amdgpu_waves_per_eu(4, 8)))")],
+    "W2": [("""    __shared__ __attribute__((aligned(16))) SynWave Wv[SYN_WAVES];""",
+            """    __shared__ __attribute__((aligned(16))) SynWave Wv[SYN_WAVES];
+    __shared__ float pad_[5000];
+    if (n_streams < 0) pad_[threadIdx.x] = 0.f;""")],
     "NI": [("""                const bool long_imdct = bt != 2 || (mixed && sb < 2);
                 if (long_imdct) {""", """                const bool long_imdct = bt != 2 || (mixed && sb < 2);
                 if (true) {
