@@ -266,7 +266,9 @@ __global__ void __launch_bounds__(64) k_demux(const uint8_t *__restrict__ in, co
                     low5 = (uint32_t)(win_bits64(w, sbit + 9 + (nch == 1 ? 5 : 3) + 4 * qch) >> 60) << 1;
                 }
                 const uint32_t myp23 = unit_ok ? (uint32_t)(v59 >> 47) : 0u;
-                const bool mybad = unit_ok && ((v59 >> 38) & 0x1FFu) > 288u; /* SURVEY A.9 (5) */
+                /* FFmpeg drops the frame: big_values > 288, or
+                 * window switching with the reserved block_type 0 */
+                const bool mybad = unit_ok && (((v59 >> 38) & 0x1FFu) > 288u || (v59 & (7ull << 23)) == (4ull << 23));
                 sw = unit_ok ? (v59 << 5) | low5 : 0ull;
                 int p23[2][2];
                 p23[0][0] = __builtin_amdgcn_readlane((int)myp23, 0);

@@ -656,8 +656,11 @@ ORC_API int orc_decode_frame_f64(orc_dec *d, const uint8_t *buf, int bytes, doub
     const int crc_bad = (d->opts & ORC_OPT_CRC_CHECK) && h.crc_bytes && !orc_crc_ok(buf, h.side_bytes);
     for (int gr = 0; gr < h.ngr; gr++)
         for (int ch = 0; ch < h.nch; ch++)
-            if (crc_bad || s->gr[gr][ch].big_values > 288) {
-                /* dropped; FFmpeg mp_decode_frame then keeps
+            if (crc_bad || s->gr[gr][ch].big_values > 288 ||
+                (s->gr[gr][ch].window_switching && s->gr[gr][ch].block_type == 0)) {
+                /* dropped (FFmpeg mp_decode_layer3 rejects
+                 * big_values > 288 and the reserved block_type 0 under window
+                 * switching, tests/golden edge_bt0_drop); mp_decode_frame then keeps
                  * the frame's last min(BACKSTEP_SIZE = 512, bytes - 4) post-
                  * header bytes as the whole reservoir */
                 int keep = fb - 4 < 512 ? fb - 4 : 512;

@@ -13,8 +13,11 @@ int16 PCM next to the stream bytes.
   edge_trunc      C3 stream whose last frame is cut short (dropped)
   edge_320k_32k   stereo 320 kbps @ 32 kHz (1441-B frames, long units:
                   exercises the multi-batch LDS staging of k_huffman)
+  edge_bt0_drop   C3-like stream (40 % short units), frame 4's first unit
+                  has window switching with the reserved block_type 0
+                  (FFmpeg: "invalid block type", frame dropped)
 
-Usage:  python tests/golden/make_edge_golden.py
+Usage:  python tests/golden/make_edge_golden.py [case ...]
 """
 import json
 import pathlib
@@ -39,6 +42,10 @@ def set_big_values(frame: bytearray, gr: int, ch: int, value: int):
         b = bit + i
         v = (value >> (8 - i)) & 1
         frame[b >> 3] = (frame[b >> 3] & ~(0x80 >> (b & 7))) | (v << (7 - (b & 7)))
+
+
+def set_bit(frame: bytearray, b: int, v: int):
+    frame[b >> 3] = (frame[b >> 3] & ~(0x80 >> (b & 7))) | (v << (7 - (b & 7)))
 
 
 def cases():
@@ -71,13 +78,24 @@ def cases():
     cfg.update(sr_idx=2, bitrate_idx=14, mode=0, mode_ext=-1, short_pct=20, mixed_pct=20, crc_pct=0)
     data, offs = _gen.stream(cfg, 6_000_005, 16)
     out["edge_320k_32k"] = (data, 32000, 2)
+
+    data, offs = _gen.stream(dict(_gen.C3, short_pct=40), 4242, 12)
+    ba = bytearray(data)
+    side = (int(offs[4]) + 4) * 8  # frame 4: MPEG-1 stereo, no CRC
+    assert ba[(side + 53) >> 3] >> (7 - ((side + 53) & 7)) & 1  # window_switching of (gr 0, ch 0)
+    set_bit(ba, side + 54, 0)  # block_type = 0 (reserved with window switching)
+    set_bit(ba, side + 55, 0)
+    out["edge_bt0_drop"] = (bytes(ba), 44100, 2)
     return out
 
 
 def main():
     man_path = HERE / "manifest.json"
     manifest = json.loads(man_path.read_text())
+    only = set(sys.argv[1:])
     for name, (data, hz, nch) in cases().items():
+        if only and name not in only:
+            continue
         ref = ffmpeg_oracle.decode(data, hz, nch)
         (HERE / (name + ".mp3")).write_bytes(data)
         np.save(HERE / (name + ".pcm16.npy"), to_int16(ref))
