@@ -756,6 +756,7 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                     rw.nw = 0;
                     rw.w0 = rw.w1 = rw.w2 = rw.w3 = 0u;
                     int k = 0;
+                    const uint32_t end_bit = start + seg + p23;
                     for (; k < bv2; k += 2) {
                         const uint32_t ts = k < r1 ? ts0 : (k < r2 ? ts1 : ts2);
                         const uint32_t tb = ts & 0xFFFFu, b1 = (ts >> 16) & 15u, lin = ts >> 24;
@@ -781,15 +782,17 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                         const uint32_t ey = ny ? rb >> (32 - ny) : 0u;
                         rb <<= ny;
                         const uint32_t sy = y != 0u, sgy = rb >> 31;
-                        pos += len_c + nx + sx + ny + sy;
+                        /* FFmpeg: no pair starts at or past the part2_3 end
+                         * (a truncated unit's remaining lines read as zeros) */
+                        const bool live = pos < end_bit;
+                        pos += live ? len_c + nx + sx + ny + sy : 0u;
                         int X = (int)(x + ex), Y = (int)(y + ey);
-                        X = (sx && sgx) ? -X : X;
-                        Y = (sy && sgy) ? -Y : Y;
+                        X = !live ? 0 : (sx && sgx) ? -X : X;
+                        Y = !live ? 0 : (sy && sgy) ? -Y : Y;
                         rw.push((uint32_t)(uint16_t)X | ((uint32_t)(uint16_t)Y << 16));
                     }
                     /* count1 quadruples until the part2_3 end; a quadruple that
                      * overreads it is discarded (FFmpeg) */
-                    const uint32_t end_bit = start + seg + p23;
                     const bool c1b = (side >> 5) & 1;
                     while (k <= 572 && pos < end_bit) {
                         const uint32_t hw = win32(bits, pos);

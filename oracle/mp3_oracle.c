@@ -367,6 +367,9 @@ static long orc_huffman(orc_bits *b, const orc_gr *g, int sr_idx, long end_bit, 
         int tab = MP3D_HTAB_OF_SELECT[sel];
         int linbits = MP3D_LINBITS[sel];
         for (; k < end; k += 2) {
+            /* FFmpeg huffman_decode: no pair starts at or past the unit's
+             * part2_3 end (the rest of the unit reads as zeros) */
+            if (b->pos >= end_bit) break;
             int x = 0, y = 0;
             if (tab >= 0) {
                 int v = orc_tree_decode(&g_trees[tab], b);

@@ -13,6 +13,10 @@ int16 PCM next to the stream bytes.
   edge_trunc      C3 stream whose last frame is cut short (dropped)
   edge_320k_32k   stereo 320 kbps @ 32 kHz (1441-B frames, long units:
                   exercises the multi-batch LDS staging of k_huffman)
+  edge_p23_short  C3 stream, frames 3 and 6: part2_3_length of the first
+                  unit cut to 60 % (its big_values run past the unit end --
+                  FFmpeg stops decoding pairs there -- and the next unit
+                  starts inside its data)
   edge_bt0_drop   C3-like stream (40 % short units), frame 4's first unit
                   has window switching with the reserved block_type 0
                   (FFmpeg: "invalid block type", frame dropped)
@@ -46,6 +50,22 @@ def set_big_values(frame: bytearray, gr: int, ch: int, value: int):
 
 def set_bit(frame: bytearray, b: int, v: int):
     frame[b >> 3] = (frame[b >> 3] & ~(0x80 >> (b & 7))) | (v << (7 - (b & 7)))
+
+
+def set_part2_3(frame: bytearray, gr: int, ch: int, value: int):
+    """Overwrite part2_3_length of unit (gr, ch) in an MPEG-1 frame's side info."""
+    crc = 0 if frame[1] & 1 else 2
+    nch = 1 if (frame[3] >> 6) == 3 else 2
+    bit = (4 + crc) * 8 + 9 + (5 if nch == 1 else 3) + 4 * nch + 59 * (gr * nch + ch)
+    for i in range(12):
+        set_bit(frame, bit + i, (value >> (11 - i)) & 1)
+
+
+def get_part2_3(frame: bytes, gr: int, ch: int):
+    crc = 0 if frame[1] & 1 else 2
+    nch = 1 if (frame[3] >> 6) == 3 else 2
+    bit = (4 + crc) * 8 + 9 + (5 if nch == 1 else 3) + 4 * nch + 59 * (gr * nch + ch)
+    return sum(((frame[(bit + i) >> 3] >> (7 - ((bit + i) & 7))) & 1) << (11 - i) for i in range(12))
 
 
 def cases():
@@ -86,6 +106,14 @@ def cases():
     set_bit(ba, side + 54, 0)  # block_type = 0 (reserved with window switching)
     set_bit(ba, side + 55, 0)
     out["edge_bt0_drop"] = (bytes(ba), 44100, 2)
+
+    data, offs = _gen.stream(_gen.C3, 6_000_006, 12)
+    ba = bytearray(data)
+    for f in (3, 6):
+        fr = bytearray(ba[offs[f]:offs[f + 1]])
+        set_part2_3(fr, 0, 0, get_part2_3(fr, 0, 0) * 6 // 10)
+        ba[offs[f]:offs[f + 1]] = fr
+    out["edge_p23_short"] = (bytes(ba), 44100, 2)
     return out
 
 
