@@ -25,6 +25,8 @@ def variant(name, reps):
 
 
 VARS = {
+    "R8": [("#define HUFF_ROUNDS 4 ", "#define HUFF_ROUNDS 8 ")],
+    "R16": [("#define HUFF_ROUNDS 4 ", "#define HUFF_ROUNDS 16")],
     "W4": [("__attribute__((amdgpu_waves_per_eu(3, 8)))", "__attribute__((amdgpu_waves_per_eu(4, 8)))")],
     "W2": [("""    __shared__ __attribute__((aligned(16))) SynWave Wv[SYN_WAVES];""",
             """    __shared__ __attribute__((aligned(16))) SynWave Wv[SYN_WAVES];

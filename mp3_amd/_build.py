@@ -49,10 +49,20 @@ def build_oracle(force=False):
     return out
 
 
+def build_examples(force=False):
+    """examples/mp3d_play: the player's decode loop in C over the C ABI."""
+    out = ROOT / "examples" / "mp3d_play"
+    deps = [ROOT / "examples" / "mp3d_play.c", ROOT / "include" / "mp3d.h", ROOT / "mp3_amd" / "libmp3d.so"]
+    if force or _stale(out, deps):
+        subprocess.check_call(["make", "-s", "-B", "-C", str(ROOT / "examples")])
+    return out
+
+
 def build_all(force=False):
     build_hip(force)
     build_gen(force)
     build_oracle(force)
+    build_examples(force)
 
 
 if __name__ == "__main__":
