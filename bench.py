@@ -97,6 +97,9 @@ def main():
     ap.add_argument("--frames", type=int, default=32, help="frames per stream per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true", help="also time an RCCL PCM gather to rank 0 (reported apart)")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse the "
+                         "multi-rank path with several ranks on one GPU)")
     args = ap.parse_args()
 
     import torch
@@ -108,10 +111,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; ranks beyond the visible GPUs (a gloo rehearsal on a
+    # one-GPU box) share them round-robin
+    gpu = local % max(1, torch.cuda.device_count())
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(args.dist_backend)
+    dev = torch.device("cuda", gpu)
     n, F = args.streams, args.frames
 
     # --- synthetic C3 shard of this rank (seed by global stream id) -------
@@ -122,7 +131,7 @@ def main():
     d_in = torch.from_numpy(buf).to(dev)
     pcm = torch.empty((n, F, 2304), dtype=torch.int16, device=dev)
     infos = torch.zeros((n, F, 6), dtype=torch.int32, device=dev)
-    dec = mp3_amd.BatchDecoder(n, F, device=local)
+    dec = mp3_amd.BatchDecoder(n, F, device=gpu)
     strm = torch.cuda.current_stream(dev).cuda_stream
 
     def step():

@@ -28,6 +28,8 @@ def max_over_ranks(seconds: float, device=None) -> float:
     """Job time = the slowest rank's time (identity when not distributed)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return seconds
+    if dist.get_backend() == "gloo":
+        device = "cpu"  # gloo reduces host tensors
     t = torch.tensor([seconds], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
@@ -39,8 +41,10 @@ def gather_to_root(t: torch.Tensor, root: int = 0):
     words there (PCM rows are 2304 int16 = 1152 words)."""
     world, rank = dist.get_world_size(), dist.get_rank()
     src = t.contiguous()
-    if dist.get_backend() == "gloo" and src.dtype in (torch.int16, torch.uint8, torch.int8):
-        src = src.view(torch.int32)
+    if dist.get_backend() == "gloo":
+        src = src.cpu()  # gloo gathers host tensors
+        if src.dtype in (torch.int16, torch.uint8, torch.int8):
+            src = src.view(torch.int32)
     out = [torch.empty_like(src) for _ in range(world)] if rank == root else None
     dist.gather(src, out, dst=root)
     if out is not None:
