@@ -24,7 +24,11 @@ def variant(name, reps):
                            "mp3_amd/csrc/mp3d_host.cpp"])
 
 
+W4H = ("__global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(",
+       "__global__ void __launch_bounds__(HUFF_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 8))) k_huffman(")
 VARS = {
+    "H8a": [("#define HUFF_WAVES 4", "#define HUFF_WAVES 8"), ("#define HUFF_CAPW 2400", "#define HUFF_CAPW 2080"), W4H],
+    "H8b": [("#define HUFF_WAVES 4", "#define HUFF_WAVES 8"), ("#define HUFF_CAPW 2400", "#define HUFF_CAPW 2000"), W4H],
     "R8": [("#define HUFF_ROUNDS 4 ", "#define HUFF_ROUNDS 8 ")],
     "R16": [("#define HUFF_ROUNDS 4 ", "#define HUFF_ROUNDS 16")],
     "W4": [("__attribute__((amdgpu_waves_per_eu(3, 8)))", "__attribute__((amdgpu_waves_per_eu(4, 8)))")],

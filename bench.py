@@ -82,10 +82,25 @@ def cpu_baseline(buf, offs, sizes, F, threads=None, budget_s=12.0):
         t.join()
     dt = time.perf_counter() - t0
     frames = sum(done)
+    # single-thread point on a short sample (single- and all-core)
+    t1, f1 = time.perf_counter(), 0
+    nch, hz = ctypes.c_int(), ctypes.c_int()
+    for s in range(n_streams - 1, -1, -1):
+        if time.perf_counter() - t1 > budget_s / 4:
+            break
+        d = bytes(buf[offs[s]:offs[s] + sizes[s]])
+        f1 += L.orc_decode_stream(d, len(d), out[0].ctypes.data, F, ctypes.byref(nch), ctypes.byref(hz))
+    dt1 = time.perf_counter() - t1
+    model = ""
+    try:
+        model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
     return {"value": frames / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+            "single_thread_value": f1 / dt1, "cpu_model": model, "host_cpus": os.cpu_count(),
             "sample": "first %d streams x %d frames (%d frames) of the same C3 input, decoded by "
-                      "oracle/liboracle.so (double-precision scalar restatement) on %d host threads in %.1f s"
-                      % (sum(streams_done), F, frames, threads, dt)}
+                      "oracle/liboracle.so (double-precision scalar restatement, gcc -O2) on %d host threads in "
+                      "%.1f s; single thread: %d frames in %.1f s" % (sum(streams_done), F, frames, threads, dt, f1, dt1)}
 
 
 def main():
