@@ -926,9 +926,10 @@ __device__ __forceinline__ void imdct36_w(const float *X, float *w) {
 /* ------------------------------------------------------------------------ */
 /* k_synth: one wave (64 lanes) per stream, frames and granules in order,   */
 /* SYN_WAVES streams per workgroup sharing the read-only tables in LDS      */
-/* (line tables of all three sample rates, |is|^(4/3), long windows, the   */
-/* matrixing A fragments and the synthesis window): after the prologue the  */
-/* granule loop issues no vector-memory load but the one-granule-ahead      */
+/* (line tables of the variant's sample rates, |is|^(4/3), long windows,  */
+/* the intensity ratios, the matrixing A fragments and the synthesis       */
+/* window): after the prologue the granule loop issues no vector-memory    */
+/* load but the one-granule-ahead                                           */
 /* prefetch of is[] / UnitMeta / FrameRec, so no s_waitcnt vmcnt drains the */
 /* PCM stores or the prefetch early.  Every phase exchanges data through   */
 /* ONE 5 KB per-wave LDS buffer; a wave keeps only the per-stream state     */
@@ -944,7 +945,10 @@ __device__ __forceinline__ void imdct36_w(const float *X, float *w) {
 /*     previous granule this lane needs live in registers -> int16 PCM,     */
 /*     L/R pairs joined across the half-waves (v_permlane32_swap) into one  */
 /*     4-B store per lane and slot pair.                                    */
-/* Template SRC_XR: config-2 entry (spectra given as f32 xr, after stereo). */
+/* Templates: SRC_XR config-2 entry (spectra given as f32 xr, after        */
+/* stereo); F32 float PCM sink; LSF MPEG-2 / 2.5 streams (one granule per  */
+/* frame, LSF rates and intensity ratios) -- each launch decodes only the  */
+/* streams of its MPEG family (StreamState.kind).                           */
 /* ------------------------------------------------------------------------ */
 #define SYN_WAVES 4
 #define SROW 36      /* LDS row stride of S (floats): 16-B rows, few conflicts */
