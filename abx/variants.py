@@ -27,6 +27,11 @@ def variant(name, reps):
 W4H = ("__global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(",
        "__global__ void __launch_bounds__(HUFF_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 8))) k_huffman(")
 VARS = {
+    "DM1": [("const bool lsf = hdr_kind(h1) == 2;", "const bool lsf = false;")],
+    "DM2": [("|| (v59 & (7ull << 23)) == (4ull << 23))", ")")],
+    "DM3": [("if (kind && hdr_kind(b1) != kind) return -1;", ""),
+            ("const bool crc_bad = (opts & MP3D_OPT_CRC_CHECK) && crc && !crc16_ok(w, (uint32_t)side_bytes);",
+             "const bool crc_bad = false;")],
     "H8a": [("#define HUFF_WAVES 4", "#define HUFF_WAVES 8"), ("#define HUFF_CAPW 2400", "#define HUFF_CAPW 2080"), W4H],
     "H8b": [("#define HUFF_WAVES 4", "#define HUFF_WAVES 8"), ("#define HUFF_CAPW 2400", "#define HUFF_CAPW 2000"), W4H],
     "R8": [("#define HUFF_ROUNDS 4 ", "#define HUFF_ROUNDS 8 ")],
