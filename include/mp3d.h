@@ -1,5 +1,6 @@
 /*
- * mp3d.h -- C ABI of the MI355X-native batched MPEG-1 Layer III decoder.
+ * mp3d.h -- C ABI of the MI355X-native batched MP3 (MPEG-1 and MPEG-2 / 2.5
+ * Layer III) decoder.
  *
  * Drop-in boundary for the decode hot path of lxm0851/mp3.  The reference
  * snapshot contains no decoder source and therefore no FFI surface to copy
@@ -17,8 +18,9 @@
  *    MP3D_E* code on failure; nothing throws or aborts across the ABI.
  *  - Caller owns every buffer passed in.  A handle owns its device memory
  *    and decoder state; *_destroy frees it.
- *  - PCM is int16, interleaved L/R, 1152 samples per channel per frame
- *    (MPEG-1 Layer III).  Mono frames fill 1152 samples.
+ *  - PCM is int16 (or float32 with the _f32 entry points), interleaved L/R,
+ *    1152 samples per channel per MPEG-1 frame, 576 per MPEG-2 / 2.5 (LSF)
+ *    frame, at the start of the frame's 2304-sample row.
  *  - The compute path is HIP on an AMD Instinct MI355X (gfx950).  There is
  *    no CPU fallback: without a usable GPU, create calls fail with
  *    MP3D_E_NO_DEVICE.
@@ -53,10 +55,10 @@ extern "C" {
 typedef struct mp3d_frame_info {
     int frame_bytes;  /* bytes consumed (0: no frame found)                */
     int channels;     /* 1 or 2                                            */
-    int hz;           /* 32000, 44100 or 48000                             */
+    int hz;           /* 32000 / 44100 / 48000 (MPEG-1), 8000 .. 24000 LSF */
     int layer;        /* 3                                                 */
-    int bitrate_kbps; /* 32..320                                           */
-    int samples;      /* PCM samples per channel produced (1152 or 0)      */
+    int bitrate_kbps; /* 32..320 (MPEG-1), 8..160 (LSF)                    */
+    int samples;      /* PCM samples per channel: 1152, 576 (LSF) or 0    */
 } mp3d_frame_info;
 
 typedef struct mp3d_dec mp3d_dec;
@@ -65,7 +67,8 @@ typedef struct mp3d_batch mp3d_batch;
 /* ---- per-frame decoder (the player's decode call) ---------------------- *
  * One decoder per audio stream and host thread.  mp3d_decode_frame finds
  * the next frame in buf (skipping an ID3v2 tag / garbage before the sync
- * word), decodes it on the GPU and returns samples per channel: 1152, or 0
+ * word), decodes it on the GPU and returns samples per channel: 1152 (576
+ * for an MPEG-2 / 2.5 LSF frame), or 0
  * when bytes were consumed without audio (Xing/Info tag frame, invalid
  * frame).  info->frame_bytes (+ any skipped prefix) tells how far to
  * advance; pcm may be NULL (decode for state only).  Reservoir underflow
@@ -130,6 +133,7 @@ MP3D_API int mp3d_dec_set_options(mp3d_dec *dec, int flags);
 MP3D_API int mp3d_batch_huffman_only(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets, const uint32_t *sizes,
                             int n_streams, int frames_per_stream, int16_t *is_out, uint8_t *sf_out,
                             void *hip_stream);
+/* synth_only takes MPEG-1 rates (32 / 44.1 / 48 kHz) */
 MP3D_API int mp3d_batch_synth_only(mp3d_batch *b, const float *xr, const uint8_t *block_type, const uint8_t *mixed,
                           int n_streams, int frames_per_stream, int nch, int sample_rate_hz, int16_t *pcm,
                           void *hip_stream);
