@@ -3,4 +3,5 @@
 set -e
 N=$1; shift
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -fvisibility=hidden -o abx/$N.so "$@" \
-  mp3_amd/csrc/mp3d_kernels.hip mp3_amd/csrc/mp3d_host.cpp
+  mp3_amd/csrc/mp3d_demux.hip mp3_amd/csrc/mp3d_huffman.hip mp3_amd/csrc/mp3d_synth.hip \
+  mp3_amd/csrc/mp3d_host.cpp

@@ -6,22 +6,23 @@ import shutil
 import subprocess
 import sys
 
-SRC = open("mp3_amd/csrc/mp3d_kernels.hip").read()
+KERNELS = ["mp3d_demux.hip", "mp3d_huffman.hip", "mp3d_synth.hip"]
 
 
 def variant(name, reps):
-    s = SRC
+    srcs = {k: open("mp3_amd/csrc/" + k).read() for k in KERNELS}
     for a, b in reps:
-        assert s.count(a) >= 1, (name, a)
-        s = s.replace(a, b)
+        assert any(a in s for s in srcs.values()), (name, a)
+        srcs = {k: s.replace(a, b) for k, s in srcs.items()}
     d = "/tmp/vars/" + name
     os.makedirs(d, exist_ok=True)
-    for h in ["mp3d_internal.h", "mp3d_tables.h", "mp3d_consts.h"]:
+    for h in ["mp3d_internal.h", "mp3d_tables.h", "mp3d_consts.h", "mp3d_device.h"]:
         shutil.copy("mp3_amd/csrc/" + h, d)
-    open(d + "/mp3d_kernels.hip", "w").write(s)
+    for k, s in srcs.items():
+        open(d + "/" + k, "w").write(s)
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
-                           "-fvisibility=hidden", "-o", "abx/%s.so" % name, d + "/mp3d_kernels.hip",
-                           "mp3_amd/csrc/mp3d_host.cpp"])
+                           "-fvisibility=hidden", "-o", "abx/%s.so" % name] + [d + "/" + k for k in KERNELS] +
+                          ["mp3_amd/csrc/mp3d_host.cpp"])
 
 
 W4H = ("__global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(",

@@ -4,7 +4,8 @@
  * 2.4.3.4 formulas), batch buffer management and kernel launches.
  *
  * No CPU decode path exists here: every frame is decoded by the HIP kernels
- * in mp3d_kernels.hip; without a device the create calls fail.
+ * in mp3d_demux.hip, mp3d_huffman.hip and mp3d_synth.hip; without a device
+ * the create calls fail.
  */
 #include <hip/hip_runtime.h>
 
@@ -22,7 +23,8 @@
 #include "mp3d_consts.h"
 
 namespace mp3d {
-hipError_t upload_constants(const float *, const float *, const float *, const float *, const uint16_t *);
+hipError_t upload_synth_constants(const float *, const float *, const float *, const float *);
+hipError_t upload_demux_constants(const uint16_t *);
 void launch_demux(const uint8_t *, const uint64_t *, const uint32_t *, uint8_t *, const uint64_t *, StreamState *,
                   FrameRec *, uint64_t *, void *, int, int, int, hipStream_t);
 void launch_huffman(const uint8_t *, const uint64_t *, const FrameRec *, const uint64_t *, const DevTables *, int16_t *,
@@ -178,7 +180,7 @@ static int upload_symbols() {
         }
     /* long windows (block types 0, 1, 3) with the fast IMDCT's output
      * scale s_n = 1 / (2 cos(pi (2n+1) / 72)) and signs folded in
-     * (mp3d_kernels.hip imdct36_w): out i<9 uses y_(9+i), i in 9..17 -y_(26-i),
+     * (mp3d_synth.hip imdct36_w): out i<9 uses y_(9+i), i in 9..17 -y_(26-i),
      * 18..26 -y_(26-i), 27..35 -y_(i-27)                                   */
     for (int bt = 0; bt < 4; bt++)
         for (int i = 0; i < 36; i++) {
@@ -228,7 +230,8 @@ static int upload_symbols() {
         for (int bi = 1; bi < 15; bi++)
             fbt[sr][bi] = (uint16_t)((sr < 3 ? 144000 * (int)MP3D_BITRATE_L3[bi] : 72000 * (int)MP3D_BITRATE_L3_LSF[bi]) /
                                      (int)MP3D_SAMPLE_RATE[sr]);
-    HIPCHK(upload_constants(&win36[0][0], &isr[0][0], p2q, &isl[0][0][0], &fbt[0][0]));
+    HIPCHK(upload_synth_constants(&win36[0][0], &isr[0][0], p2q, &isl[0][0][0]));
+    HIPCHK(upload_demux_constants(&fbt[0][0]));
     return MP3D_OK;
 }
 

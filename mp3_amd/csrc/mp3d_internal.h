@@ -1,6 +1,6 @@
 /*
  * mp3d_internal.h -- device data layout shared by the HIP kernels
- * (mp3d_kernels.hip) and the host library (mp3d_host.cpp).
+ * (mp3d_demux.hip, mp3d_huffman.hip, mp3d_synth.hip) and the host library (mp3d_host.cpp).
  *
  * HBM layout of one batch (SoA, one process per GPU):
  *   input   : caller's frame bytes, stream s at in_off[s] (u64), in_len[s]

@@ -1,0 +1,806 @@
+/*
+ * mp3d_synth.hip -- k_synth (ISO 11172-3
+ * 2.4.3.4 + Annex A, 13818-3 2.4.3.2): requantise, stereo, alias reduction,
+ * IMDCT + overlap, polyphase synthesis (matrixing on the matrix cores) ->
+ * int16 / float PCM; and k_gather_frames for the frame-parallel long-stream
+ * decode (§8(f) row 2).  Pipeline overview: mp3d_device.h.
+ */
+#include "mp3d_device.h"
+#include "mp3d_consts.h" /* IMDCT-12 / short window / alias coefficients as literals */
+
+namespace mp3d {
+
+/* ------------------------------------------------------------------------ */
+/* Constant-memory tables (uniform access -> scalar loads)                   */
+/* ------------------------------------------------------------------------ */
+__constant__ float c_win36[4][36];     /* long windows x IMDCT output scale (imdct36_w)  */
+__constant__ float c_is_ratio[7][2];   /* MPEG-1 intensity: k/(1+k), 1/(1+k)             */
+__constant__ float c_pow2q[4];         /* 2^(i/4)                                        */
+__constant__ float c_is_lsf[2][16][2]; /* LSF intensity [intensity_scale][is_pos]: L, R */
+
+/* 9-point DCT-III: v[n] = sum_m a[m] cos(pi m (2n+1) / 18), n = 0..8, via the
+ * symmetry v[8-n] = sum_m (-1)^m a[m] cos(...): even / odd m partial sums */
+__device__ __forceinline__ void dct3_9(const float *a, float *v) {
+    const float C10 = 9.848077530e-01f; /* cos(10 deg) */
+    const float C20 = 9.396926208e-01f; /* cos(20 deg) */
+    const float C30 = 8.660254038e-01f; /* cos(30 deg) */
+    const float C40 = 7.660444431e-01f; /* cos(40 deg) */
+    const float C50 = 6.427876097e-01f; /* cos(50 deg) */
+    const float C70 = 3.420201433e-01f; /* cos(70 deg) */
+    const float C80 = 1.736481777e-01f; /* cos(80 deg) */
+    const float ev0 = fmaf(a[8], C80, fmaf(a[6], 0.5f, fmaf(a[4], C40, fmaf(a[2], C20, a[0]))));
+    const float od0 = fmaf(a[7], C70, fmaf(a[5], C50, fmaf(a[3], C30, a[1] * C10)));
+    v[0] = ev0 + od0;
+    v[8] = ev0 - od0;
+    const float ev1 = fmaf(a[8], -0.5f, (fmaf(a[4], -0.5f, fmaf(a[2], 0.5f, a[0])) - a[6]));
+    const float od1 = fmaf(a[7], -C30, fmaf(a[5], -C30, a[1] * C30));
+    v[1] = ev1 + od1;
+    v[7] = ev1 - od1;
+    const float ev2 = fmaf(a[8], C40, fmaf(a[6], 0.5f, fmaf(a[4], -C20, fmaf(a[2], -C80, a[0]))));
+    const float od2 = fmaf(a[7], C10, fmaf(a[5], -C70, fmaf(a[3], -C30, a[1] * C50)));
+    v[2] = ev2 + od2;
+    v[6] = ev2 - od2;
+    const float ev3 = fmaf(a[8], -C20, fmaf(a[6], 0.5f, fmaf(a[4], C80, fmaf(a[2], -C40, a[0]))));
+    const float od3 = fmaf(a[7], -C50, fmaf(a[5], C10, fmaf(a[3], -C30, a[1] * C70)));
+    v[3] = ev3 + od3;
+    v[5] = ev3 - od3;
+    v[4] = a[0] - a[2] + a[4] - a[6] + a[8];
+}
+
+
+/* 36-point IMDCT of one subband's 18 lines (ISO 2.4.3.4) without the 18x36
+ * matrix: x_i = y_(i+9) / -y_(26-i) / -y_(i-27) with y the 18-point DCT-IV
+ * of X; y_n = w_n / (2 cos(pi (2n+1) / 72)) (scale folded into c_win36), w
+ * the 18-point DCT-III of Z_k = X_k + X_(k-1), split into the 9-point
+ * DCT-III of Z_2m (even) and of Z_(2m+1) + Z_(2m-1) (odd, scaled by
+ * 1 / (2 cos(pi (2n+1) / 36))).  ~150 flops instead of 324 FMAs.        */
+__device__ __forceinline__ void imdct36_w(const float *X, float *w) {
+    float e[9], p[9], E[9], P[9];
+    float zprev = 0.f;
+#pragma unroll
+    for (int m = 0; m < 9; m++) {
+        e[m] = m ? X[2 * m] + X[2 * m - 1] : X[0];
+        const float zo = X[2 * m + 1] + X[2 * m];
+        p[m] = zo + zprev;
+        zprev = zo;
+    }
+    dct3_9(e, E);
+    dct3_9(p, P);
+    const float K[9] = {5.019099188e-01f, 5.176380902e-01f, 5.516889595e-01f, 6.103872944e-01f, 7.071067812e-01f,
+                        8.717233978e-01f, 1.183100792e+00f, 1.931851653e+00f, 5.736856623e+00f};
+#pragma unroll
+    for (int n = 0; n < 9; n++) {
+        const float o = P[n] * K[n];
+        w[n] = E[n] + o;
+        w[17 - n] = E[n] - o;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* k_synth: one wave (64 lanes) per stream, frames and granules in order,   */
+/* SYN_WAVES streams per workgroup sharing the read-only tables in LDS      */
+/* (line tables of the variant's sample rates, |is|^(4/3), long windows,  */
+/* the intensity ratios, the matrixing A fragments and the synthesis       */
+/* window): after the prologue the granule loop issues no vector-memory    */
+/* load but the one-granule-ahead                                           */
+/* prefetch of is[] / UnitMeta / FrameRec, so no s_waitcnt vmcnt drains the */
+/* PCM stores or the prefetch early.  Every phase exchanges data through   */
+/* ONE 5 KB per-wave LDS buffer; a wave keeps only the per-stream state     */
+/* (IMDCT overlap, synthesis history) in VGPRs.                             */
+/*  Q  lane = line pair: requantise both channels (ISO 2.4.3.4, per-band   */
+/*     2^(q/4) precomputed by lane = band), joint stereo paired by          */
+/*     bitstream line, scatter into LDS in short-block reordered position.  */
+/*  I  lane = (ch, sb): alias reduction (neighbours read from LDS), IMDCT   */
+/*     36 / 3x12 + window + overlap + frequency inversion -> S[ch,t][sb].   */
+/*  M  32-point matrixing X = C.S on the matrix cores (v_mfma_f32_16x16x4): */
+/*     rows m, cols (ch, t), K = sb; A = C fragments, B = S rows (LDS).     */
+/*  W  lane = (ch, j): 512-tap window over 16 slots; the 29 X values of the */
+/*     previous granule this lane needs live in registers -> int16 PCM,     */
+/*     L/R pairs joined across the half-waves (v_permlane32_swap) into one  */
+/*     4-B store per lane and slot pair.                                    */
+/* Templates: SRC_XR config-2 entry (spectra given as f32 xr, after        */
+/* stereo); F32 float PCM sink; LSF MPEG-2 / 2.5 streams (one granule per  */
+/* frame, LSF rates and intensity ratios) -- each launch decodes only the  */
+/* streams of its MPEG family (StreamState.kind).                           */
+/* ------------------------------------------------------------------------ */
+#define SYN_WAVES 4
+#define SROW 36      /* LDS row stride of S (floats): 16-B rows, few conflicts */
+#define SYN_BUF 1296 /* floats: max(xr 2x576, S 36x36, X 36x36)              */
+#define XROW 36      /* LDS row stride of X: 16-B rows, conflict-free b128 writes */
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+/* Opaque copy of a loop-invariant LDS index: keeps the compiler from
+ * hoisting one address VGPR per unrolled access out of the frame loop
+ * (it would rather hold ~60 of them live than fold immediate offsets). */
+__device__ __forceinline__ int opaque(int v) {
+    __asm__ volatile("" : "+v"(v));
+    return v;
+}
+
+__device__ __forceinline__ float pow2_quarter(int q) { /* 2^(q/4), exact table */
+    const int r = q & 3;
+    const float f = r == 0 ? 1.0f : r == 1 ? 1.18920711500272106672f : r == 2 ? 1.41421356237309504880f
+                                                                              : 1.68179283050742908606f;
+    return ldexpf(f, q >> 2);
+}
+
+/* |is|^(4/3) for 256 <= |is| <= 8206 without the 33 KB table: cube root
+ * from v_log_f32 / v_exp_f32, one Newton step, times |is|; within 2 ulp of
+ * the correctly rounded value for every such |is| (checked exhaustively in
+ * tests/test_tables.py against the same float32 recipe). */
+__device__ __forceinline__ float pow43_big(int a) {
+    const float x = (float)a;
+    float y = __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(x) * (1.0f / 3.0f));
+    const float y2 = y * y;
+    y = y - fmaf(y2, y, -x) * __builtin_amdgcn_rcpf(3.0f * y2);
+    return x * y;
+}
+
+template <bool LSF> struct SynShared { /* read-only, one copy per workgroup        */
+    /* tab->lvar (u16 pairs) [rate][variant] of the variant's family: MPEG-1
+     * rates 0..2, or the six LSF rates 3..8                                */
+    uint32_t lvar[LSF ? 6 : 3][3][288];
+    float ce[16][16], co[16][16];    /* matrixing A: C[2m][i], C[2m+1][i], i < 16  */
+    float dw[32][16];                /* window taps per output j                   */
+    float p43[256];                  /* |is|^(4/3) for |is| < 256                  */
+    float w36[4][36];                /* long-block windows (x IMDCT output scale)  */
+    float isr[LSF ? 32 : 7][2];      /* intensity ratios: MPEG-1 [is_pos], LSF      */
+                                     /* [intensity_scale * 16 + is_pos]            */
+};
+struct SynWave {                     /* one per wave (stream)                      */
+    float buf[SYN_BUF];              /* xr -> S -> X hand-offs                     */
+    float scale[2][64];              /* 2^(q/4) per (ch, band idx): long b | 22 + 3 b + w */
+    UnitMeta m[2];
+    uint8_t is[64];                  /* intensity position per right band idx, 0xFF none */
+};
+
+#define WAIT_VMCNT0() __builtin_amdgcn_s_waitcnt(0x0F70) /* vmcnt(0), other counters free */
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+template <bool SRC_XR, bool F32, bool LSF>
+__global__ void __launch_bounds__(64 * SYN_WAVES) __attribute__((amdgpu_waves_per_eu(3, 8)))
+k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, const UnitMeta *__restrict__ meta,
+        const float *__restrict__ xr_in, const uint8_t *__restrict__ xr_bt, const uint8_t *__restrict__ xr_mixed,
+        const DevTables *__restrict__ tab, StreamState *__restrict__ st, void *__restrict__ pcm, int n_streams,
+        int F, int xr_nch, int xr_sr) {
+    __shared__ __attribute__((aligned(16))) SynShared<LSF> T;
+    __shared__ __attribute__((aligned(16))) SynWave Wv[SYN_WAVES];
+    constexpr int NRATE = LSF ? 6 : 3;
+    if (!SRC_XR) {
+        /* one variant per MPEG family (StreamState.kind, fixed by k_demux):
+         * MPEG-1 takes kinds 0 / 1, LSF kind 2.  A workgroup holding no
+         * stream of its variant leaves before staging any table (the same
+         * decision in every lane: no barrier is skipped by part of it). */
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < SYN_WAVES; k++) {
+            const int sk = blockIdx.x * SYN_WAVES + k;
+            if (sk < n_streams) any |= (st[sk].kind == 2) == LSF;
+        }
+        if (!any) return;
+    }
+    {
+        const int tid = threadIdx.x;
+        for (int i = tid; i < NRATE * 3 * 288; i += 64 * SYN_WAVES)
+            (&T.lvar[0][0][0])[i] = ((const uint32_t *)&tab->lvar[LSF ? 3 : 0][0][0])[i];
+        for (int i = tid; i < 256; i += 64 * SYN_WAVES) {
+            const int r = i >> 4, c = i & 15;
+            T.ce[r][c] = tab->dct_c[2 * r][c];
+            T.co[r][c] = tab->dct_c[2 * r + 1][c];
+            T.p43[i] = tab->pow43[i];
+        }
+        for (int i = tid; i < 32 * 16; i += 64 * SYN_WAVES) (&T.dw[0][0])[i] = (&tab->dwin[0][0])[i];
+        for (int i = tid; i < 4 * 36; i += 64 * SYN_WAVES) (&T.w36[0][0])[i] = (&c_win36[0][0])[i];
+        if (LSF) {
+            if (tid < 64) (&T.isr[0][0])[tid] = (&c_is_lsf[0][0][0])[tid];
+        } else if (tid < 14) (&T.isr[0][0])[tid] = (&c_is_ratio[0][0])[tid];
+        __syncthreads();
+    }
+    const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); /* wave-uniform (SGPR) */
+    const int s = blockIdx.x * SYN_WAVES + wid;
+    if (s >= n_streams) return; /* after the only workgroup barrier */
+    if (!SRC_XR && (st[s].kind == 2) != LSF) return; /* the other variant's stream */
+    SynWave &Wd = Wv[wid];
+    float *const sBuf = Wd.buf;
+    const int lane = threadIdx.x & 63;
+    const int ch = lane >> 5;
+    const int sb = lane & 31; /* phase I: subband; phase W: output j */
+    constexpr int MW = (int)(sizeof(UnitMeta) / 4); /* 14 words per unit */
+
+    StreamState &S = st[s];
+    const int wa = tab->win_a[sb], wb = tab->win_b[sb];
+    float ov[18];
+#pragma unroll
+    for (int i = 0; i < 18; i++) ov[i] = S.overlap[ch][sb][i];
+    /* synthesis history: ha[k] = X_{k-14}[wa], hb[k] = X_{k-15}[wb] (slot
+     * index relative to the granule's first slot; fifo[t] = slot t - 15)  */
+    float ha[14], hb[15];
+#pragma unroll
+    for (int k = 0; k < 14; k++) ha[k] = S.fifo[ch][k + 1][wa];
+#pragma unroll
+    for (int k = 0; k < 15; k++) hb[k] = S.fifo[ch][k][wb];
+
+    /* Per-stream buffer resources: every granule access below is a buffer
+     * instruction with a uniform byte offset in an SGPR and the lane offset
+     * in one VGPR, instead of a 64-bit address pair per lane and load. */
+    const int gb = 2 * 576 * 2;                   /* is[] bytes per granule (2 ch) */
+    const __amdgpu_buffer_rsrc_t r_is = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(is_buf + (size_t)s * F * 4 * 576), 0, F * 2 * gb, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r_meta = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(meta + (size_t)s * F * 4), 0, F * 4 * (int)sizeof(UnitMeta), 0x00020000);
+    const __amdgpu_buffer_rsrc_t r_rec = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(rec + (size_t)s * F), 0, F * (int)sizeof(FrameRec), 0x00020000);
+    constexpr int PB = F32 ? 4 : 2; /* bytes per output sample: f32 or int16 */
+    const __amdgpu_buffer_rsrc_t r_pcm = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)((uint8_t *)pcm + (size_t)s * F * 2304 * PB), 0, F * 2304 * PB, 0x00020000);
+
+    /* granule prefetch, one granule ahead of use: is[] words (lane owns
+     * lines 2 lane + 128 i, +1), UnitMeta words of both channels (lanes
+     * 0 .. 27) and the granule's FrameRec words (lanes 32 .. 39) */
+    uint32_t nis[2][5], nmeta = 0;
+    auto prefetch = [&](int g) { /* g = granule index inside the stream */
+        const int lo = opaque(lane * 4);
+#pragma unroll
+        for (int c = 0; c < 2; c++)
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                nis[c][i] = __builtin_amdgcn_raw_buffer_load_b32(r_is, lo + c * 1152 + 256 * i, g * gb, 0);
+        nis[0][4] = nis[1][4] = 0u;
+        if (lane < 32) {
+            nis[0][4] = __builtin_amdgcn_raw_buffer_load_b32(r_is, lo + 1024, g * gb, 0);
+            nis[1][4] = __builtin_amdgcn_raw_buffer_load_b32(r_is, lo + 1152 + 1024, g * gb, 0);
+        }
+        nmeta = 0u;
+        if (lane < 2 * MW) nmeta = __builtin_amdgcn_raw_buffer_load_b32(r_meta, lo, g * 2 * (int)sizeof(UnitMeta), 0);
+        else if (lane >= 32 && lane < 40)
+            nmeta = __builtin_amdgcn_raw_buffer_load_b32(r_rec, lo - 128, (g >> 1) * (int)sizeof(FrameRec), 0);
+    };
+    if (!SRC_XR) {
+        prefetch(0);
+        /* explicit drain on the entry path, so the compiler's wait before
+         * each prefetch use is set by the loop path (stores after it) */
+        WAIT_VMCNT0();
+    }
+
+    for (int f = 0; f < F; f++) {
+        int nch, sr, mode = 0, mext = 0;
+        const size_t fr = (size_t)s * F + f;
+        if (SRC_XR) {
+            nch = xr_nch;
+            sr = xr_sr;
+        } else {
+            /* FrameRec words 4 .. 6 from the prefetch (lanes 36 .. 38) */
+            const uint32_t r4 = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, 36);
+            const uint32_t r5 = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, 37);
+            const uint32_t r6 = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, 38);
+            const uint32_t first_gr = (r6 >> 8) & 0xFFu;
+            if (!(r4 & 0xFFFFu) || (first_gr & (REC_TAG | REC_DROP))) {
+                /* no audio in this frame: fetch the next frame's granule 0
+                 * now and wait for it here, off the common path */
+                if (f + 1 < F) prefetch(2 * (f + 1));
+                WAIT_VMCNT0();
+                continue;
+            }
+            nch = (int)(r5 >> 24);
+            sr = (int)((r6 >> 16) & 15u) - (LSF ? 3 : 0); /* FrameRec.sr_idx in the family */
+            mode = (int)(r5 >> 22) & 3;
+            mext = (int)(r5 >> 20) & 3;
+        }
+        const bool active = ch < nch;
+        const uint32_t(*lvar)[288] = T.lvar[sr];
+        for (int gr = 0; gr < (LSF ? 1 : 2); gr++) { /* LSF: one granule per frame */
+            /* lane-derived indices are re-derived from an opaque copy each
+             * granule so they are not hoisted and held live across the loop */
+            const int lane = opaque((int)(threadIdx.x & 63));
+            const int ch = lane >> 5, sb = lane & 31;
+            /* block structure of both channels (uniform) */
+            int bt0, mx0, bt1 = 0, mx1 = 0;
+            /* ---------------- phase Q: requantise + stereo -> LDS ---------- */
+            if (SRC_XR) {
+                const size_t ux = (fr * 2 + gr) * (size_t)nch;
+                bt0 = xr_bt[ux];
+                mx0 = bt0 == 2 ? xr_mixed[ux] : 0;
+                if (nch == 2) {
+                    bt1 = xr_bt[ux + 1];
+                    mx1 = bt1 == 2 ? xr_mixed[ux + 1] : 0;
+                }
+                const uint16_t *lv0 = (const uint16_t *)lvar[bt0 == 2 ? (mx0 ? 2 : 1) : 0];
+                const uint16_t *lv1 = (const uint16_t *)lvar[bt1 == 2 ? (mx1 ? 2 : 1) : 0];
+#pragma unroll
+                for (int i = 0; i < 9; i++) {
+                    const int l = lane + 64 * i;
+                    sBuf[lv0[l] >> 6] = xr_in[ux * 576 + l];
+                    if (nch == 2) sBuf[576 + (lv1[l] >> 6)] = xr_in[(ux + 1) * 576 + l];
+                }
+            } else {
+                uint32_t cis[2][5];
+#pragma unroll
+                for (int c = 0; c < 2; c++)
+#pragma unroll
+                    for (int i = 0; i < 5; i++) cis[c][i] = nis[c][i];
+                /* UnitMeta into LDS for the (rare) intensity path; the common
+                 * path reads the prefetched words straight from registers */
+                if (lane < 2 * MW && lane / MW < nch) ((uint32_t *)&Wd.m[0])[lane] = nmeta;
+                /* words 10..12: gain, block type, mixed, scalefac_scale |
+                 * preflag, sbg[3] | nz_end (UnitMeta layout) */
+                const uint32_t m10a = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, 10);
+                const uint32_t m11a = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, 11);
+                const uint32_t m12a = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, 12);
+                const uint32_t m10b = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, MW + 10);
+                const uint32_t m11b = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, MW + 11);
+                const uint32_t m12b = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, MW + 12);
+                bt0 = (int)(m10a >> 8) & 0xFF;
+                mx0 = (int)(m10a >> 16) & 0xFF;
+                if (nch == 2) {
+                    bt1 = (int)(m10b >> 8) & 0xFF;
+                    mx1 = (int)(m10b >> 16) & 0xFF;
+                }
+                const int var[2] = {bt0 == 2 ? (mx0 ? 2 : 1) : 0, bt1 == 2 ? (mx1 ? 2 : 1) : 0};
+                const bool is_on = mode == 1 && nch == 2 && (mext & 1);
+                const bool ms_fold = mode == 1 && nch == 2 && mext == 2; /* M/S only: 1/sqrt2 in the scale */
+                const float isq = 0.70710678118654752f;
+                /* per-band scale 2^(q/4), lane = band idx (long b | 22 + 3 b + w);
+                 * the lane's scalefactor byte comes from the prefetched meta
+                 * words by one cross-lane read per channel */
+                {
+                    const bool lng = lane < 22;
+                    const int b = (lane - 22) / 3, w = lane - 22 - 3 * b;
+                    auto band_scale = [&](uint32_t g10, uint32_t g11, int cbase) {
+                        const int gain = (int)(g10 & 0xFFu) - 210, shift = (int)(g10 >> 24) + 1;
+                        const bool mixed = ((g10 >> 16) & 0xFFu) != 0u, preflag = (g11 & 0xFFu) != 0u;
+                        int j = mixed ? 8 + 3 * (b - 3) + w : 3 * b + w;
+                        j = lng ? lane : (j < 0 ? 0 : (j > 39 ? 39 : j));
+                        const uint32_t wd = (uint32_t)__shfl((int)nmeta, cbase + (j >> 2));
+                        const int sf = (int)(wd >> (8 * (j & 3))) & 0xFF;
+                        const int pre = preflag ? (int)(MP3D_PRETAB_BITS >> (2 * (lane & 31))) & 3 : 0;
+                        const int sbg = (int)(g11 >> (8 * (1 + (w < 3 ? w : 0)))) & 0xFF;
+                        const int q = lng ? gain - ((sf + pre) << shift) : gain - 8 * sbg - (sf << shift);
+                        return ms_fold ? pow2_quarter(q) * isq : pow2_quarter(q);
+                    };
+                    Wd.scale[0][lane] = band_scale(m10a, m11a, 0);
+                    if (nch == 2) Wd.scale[1][lane] = band_scale(m10b, m11b, MW);
+                }
+                wave_sync();
+                const int nz[2] = {(int)(m12a & 0xFFFFu), nch == 2 ? (int)(m12b & 0xFFFFu) : 0};
+                float xv[2][10];
+                bool big = false; /* some |is| >= 256 (escape) in this lane */
+#pragma unroll
+                for (int i = 0; i < 5; i++) {
+                    const int l0 = 2 * lane + 128 * i;
+                    const bool ok = i < 4 || lane < 32;
+#pragma unroll
+                    for (int c = 0; c < 2; c++) {
+                        const uint32_t tv2 = ok ? lvar[var[c]][l0 >> 1] : 0u;
+#pragma unroll
+                        for (int e = 0; e < 2; e++) {
+                            const int l = l0 + e;
+                            int v = (int)(int16_t)(e ? (cis[c][i] >> 16) : (cis[c][i] & 0xFFFFu));
+                            v = l < nz[c] ? v : 0; /* rzero lines are not stored by k_huffman */
+                            const int a = v < 0 ? -v : v;
+                            big |= a >= 256;
+                            const float mag = T.p43[a & 255] * Wd.scale[c][(e ? tv2 >> 16 : tv2) & 63u];
+                            xv[c][2 * i + e] = v < 0 ? -mag : mag;
+                        }
+                    }
+                }
+                if (__ballot(big)) {
+                    /* rare path (escapes |is| >= 256): patch those lines with
+                     * the in-register |is|^(4/3); one block, so the loop above
+                     * stays branch-free and its LDS reads batch */
+#pragma unroll
+                    for (int i = 0; i < 5; i++) {
+                        const int l0 = 2 * lane + 128 * i;
+#pragma unroll
+                        for (int c = 0; c < 2; c++) {
+#pragma unroll
+                            for (int e = 0; e < 2; e++) {
+                                int v = (int)(int16_t)(e ? (cis[c][i] >> 16) : (cis[c][i] & 0xFFFFu));
+                                v = l0 + e < nz[c] ? v : 0;
+                                const int a = v < 0 ? -v : v;
+                                if (a >= 256) {
+                                    const uint32_t tv2 = lvar[var[c]][l0 >> 1];
+                                    const float mag = pow43_big(a) * Wd.scale[c][(e ? tv2 >> 16 : tv2) & 63u];
+                                    xv[c][2 * i + e] = v < 0 ? -mag : mag;
+                                }
+                            }
+                        }
+                    }
+                }
+                if (is_on) {
+                    /* joint stereo with MPEG-1 intensity (ISO 2.4.3.4), paired by
+                     * bitstream line; the right channel's block structure and
+                     * its highest nonzero band (per window) decide the IS bands
+                     * (FFmpeg compute_stereo; oracle/mp3_oracle.c orc_stereo).
+                     * nzR bit = right-channel band idx holding a nonzero line. */
+                    /* no intensity for is_pos >= 7 (MPEG-1), >= 16 (LSF, FFmpeg) */
+                    constexpr int IS_ILLEGAL = LSF ? 16 : 7;
+                    uint64_t nzR = 0;
+#pragma unroll
+                    for (int i = 0; i < 5; i++) {
+                        const int l0 = 2 * lane + 128 * i;
+                        const uint32_t tv2 = (i < 4 || lane < 32) ? lvar[var[1]][l0 >> 1] : 0u;
+                        if (xv[1][2 * i] != 0.f) nzR |= 1ull << (tv2 & 63u);
+                        if (xv[1][2 * i + 1] != 0.f) nzR |= 1ull << ((tv2 >> 16) & 63u);
+                    }
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) nzR |= __shfl_xor(nzR, o);
+                    const UnitMeta &R = Wd.m[1];
+                    int ip = 0xFF;
+                    if (lane < 22) {
+                        /* long bands of a mixed block: 8 (MPEG-1), 6 (LSF) */
+                        if (bt1 != 2 || (mx1 && lane < (LSF ? 6 : 8))) {
+                            const int p = R.sf[lane == 21 ? 20 : lane];
+                            const bool short_nz = (nzR >> 22) != 0ull;
+                            if (!short_nz && ((uint32_t)(nzR & 0x3FFFFFull) >> lane) == 0u && p < IS_ILLEGAL) ip = p;
+                        }
+                    } else if (lane < 61 && bt1 == 2) {
+                        const int b = (lane - 22) / 3, w = lane - 22 - 3 * b;
+                        if (!mx1 || b >= 3) {
+                            const int kb = b == 12 ? 11 : b;
+                            const int p = R.sf[mx1 ? 8 + 3 * (kb - 3) + w : 3 * kb + w];
+                            /* no nonzero line in window w at bands >= b */
+                            uint64_t above = 0;
+                            for (int bb = b; bb < 13; bb++) above |= 1ull << (22 + 3 * bb + w);
+                            if ((nzR & above) == 0ull && p < IS_ILLEGAL) ip = p;
+                        }
+                    }
+                    /* LSF: ratio row by intensity_scale (UnitMeta.flags bit 1) */
+                    if (LSF && ip != 0xFF) ip += (int)(R.flags & 2u) << 3;
+                    Wd.is[lane] = (uint8_t)ip;
+                    wave_sync();
+#pragma unroll
+                    for (int i = 0; i < 5; i++) {
+                        const int l0 = 2 * lane + 128 * i;
+                        const uint32_t tv2 = (i < 4 || lane < 32) ? lvar[var[1]][l0 >> 1] : 0u;
+#pragma unroll
+                        for (int e = 0; e < 2; e++) {
+                            const int k = 2 * i + e;
+                            const float lv = xv[0][k], rv = xv[1][k];
+                            const int ipl = Wd.is[(e ? tv2 >> 16 : tv2) & 63u];
+                            if (ipl != 0xFF) {
+                                xv[0][k] = lv * T.isr[ipl][0];
+                                xv[1][k] = lv * T.isr[ipl][1];
+                            } else if (mext & 2) {
+                                xv[0][k] = (lv + rv) * isq;
+                                xv[1][k] = (lv - rv) * isq;
+                            }
+                        }
+                    }
+                } else if (ms_fold) {
+#pragma unroll
+                    for (int k = 0; k < 10; k++) {
+                        const float lv = xv[0][k], rv = xv[1][k];
+                        xv[0][k] = lv + rv;
+                        xv[1][k] = lv - rv;
+                    }
+                }
+                /* the next granule's loads fly during phases I, M, W (issued
+                 * after cis is consumed: fewer live registers in phase Q) */
+                if (LSF ? f + 1 < F : (gr == 0 || f + 1 < F)) prefetch(LSF ? 2 * f + 2 : 2 * f + gr + 1);
+                /* scatter in (short-block reordered) position */
+#pragma unroll
+                for (int i = 0; i < 5; i++) {
+                    if (i < 4 || lane < 32) {
+                        const int l0 = 2 * lane + 128 * i;
+#pragma unroll
+                        for (int c = 0; c < 2; c++) {
+                            if (c < nch) {
+                                if (var[c] == 0) { /* long block: in place, one 8-B store */
+                                    *(float2 *)&sBuf[576 * c + l0] = make_float2(xv[c][2 * i], xv[c][2 * i + 1]);
+                                } else {
+                                    const uint32_t tv2 = lvar[var[c]][l0 >> 1];
+                                    sBuf[576 * c + (tv2 >> 6 & 1023u)] = xv[c][2 * i];
+                                    sBuf[576 * c + (tv2 >> 22)] = xv[c][2 * i + 1];
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+            wave_sync();
+            /* ---------------- phase I: alias + IMDCT + overlap ------------ */
+            const int bt = ch ? bt1 : bt0, mixed = ch ? mx1 : mx0;
+            float o18[18];
+            {
+                const int base = ch * 576 + 18 * sb;
+                float x[18], up[8], dn[8];
+#pragma unroll
+                for (int i = 0; i < 9; i++) {
+                    const float2 v = *(const float2 *)&sBuf[base + 2 * i];
+                    x[2 * i] = v.x;
+                    x[2 * i + 1] = v.y;
+                }
+                const int pb = sb ? base - 8 : base, nb = sb < 31 ? base + 18 : base;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const float2 p = *(const float2 *)&sBuf[pb + 2 * i];
+                    const float2 n = *(const float2 *)&sBuf[nb + 2 * i];
+                    up[7 - 2 * i] = p.x; /* up[k] = x_{sb-1}[17 - k] */
+                    up[6 - 2 * i] = p.y;
+                    dn[2 * i] = n.x;     /* dn[k] = x_{sb+1}[k]      */
+                    dn[2 * i + 1] = n.y;
+                }
+                /* alias reduction (ISO 2.4.3.4): all 31 boundaries (long),
+                 * the first one (mixed), none (short) */
+                const bool upper = (bt != 2 && sb >= 1) || (bt == 2 && mixed && sb == 1);
+                const bool lower = (bt != 2 && sb <= 30) || (bt == 2 && mixed && sb == 0);
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const float lo = x[17 - k], hi = x[k];
+                    if (upper) x[k] = hi * MP3D_K_ALIAS_CS[k] + up[k] * MP3D_K_ALIAS_CA[k];
+                    if (lower) x[17 - k] = lo * MP3D_K_ALIAS_CS[k] - dn[k] * MP3D_K_ALIAS_CA[k];
+                }
+                const bool long_imdct = bt != 2 || (mixed && sb < 2);
+                if (long_imdct) {
+                    const float *wv = T.w36[bt == 2 ? 0 : bt];
+                    float w[18];
+                    imdct36_w(x, w);
+#pragma unroll
+                    for (int i = 0; i < 9; i++) {
+                        o18[i] = fmaf(w[9 + i], wv[i], ov[i]);
+                        o18[17 - i] = fmaf(w[9 + i], wv[17 - i], ov[17 - i]);
+                        const float n0 = w[8 - i] * wv[18 + i];
+                        const float n1 = w[8 - i] * wv[35 - i];
+                        ov[i] = active ? n0 : ov[i];
+                        ov[17 - i] = active ? n1 : ov[17 - i];
+                    }
+                } else {
+                    /* z[6w+6+i] += y_w[i] * win12[i], w = 0..2, i = 0..11 */
+                    float z[24]; /* z[6..29] */
+#pragma unroll
+                    for (int i = 0; i < 24; i++) z[i] = 0.f;
+#pragma unroll
+                    for (int w = 0; w < 3; w++) {
+                        float h[6];
+#pragma unroll
+                        for (int o = 0; o < 6; o++) {
+                            float acc = 0.f;
+#pragma unroll
+                            for (int k = 0; k < 6; k++) acc = fmaf(x[3 * k + w], MP3D_K_IMDCT12[k][o], acc);
+                            h[o] = acc;
+                        }
+#pragma unroll
+                        for (int i = 0; i < 3; i++) {
+                            z[6 * w + i] = fmaf(h[i], MP3D_K_WIN12[i], z[6 * w + i]);
+                            z[6 * w + 5 - i] = fmaf(-h[i], MP3D_K_WIN12[5 - i], z[6 * w + 5 - i]);
+                            z[6 * w + 6 + i] = fmaf(h[3 + i], MP3D_K_WIN12[6 + i], z[6 * w + 6 + i]);
+                            z[6 * w + 11 - i] = fmaf(h[3 + i], MP3D_K_WIN12[11 - i], z[6 * w + 11 - i]);
+                        }
+                    }
+#pragma unroll
+                    for (int i = 0; i < 18; i++) o18[i] = (i < 6 ? 0.f : z[i - 6]) + ov[i];
+#pragma unroll
+                    for (int i = 0; i < 18; i++) {
+                        const float n = i < 12 ? z[12 + i] : 0.f;
+                        ov[i] = active ? n : ov[i];
+                    }
+                }
+            }
+            wave_sync(); /* every lane has read its xr before S overwrites it */
+            {
+                const int sw = opaque(18 * ch * SROW + sb);
+#pragma unroll
+                for (int t = 0; t < 18; t++) sBuf[sw + t * SROW] = ((sb & 1) && (t & 1)) ? -o18[t] : o18[t];
+            }
+            wave_sync();
+            /* ---------------- phase M: matrixing on the matrix cores ------- */
+            /* one butterfly level of the 32-point DCT-II (ISO Annex A matrixing):
+             *   X[2m]   = sum_i C[2m][i]   (S_i + S_31-i)
+             *   X[2m+1] = sum_i C[2m+1][i] (S_i - S_31-i),  i, m < 16
+             * = two 16x16 products: half the MFMAs of the dense 32x32.
+             * v_mfma_f32_16x16x4_f32, rows m, cols n = (ch, t), K order
+             * i = 4 q + ks (q = lane >> 4): a lane's 4 B values and their
+             * mirrors are two 16-B runs of an S row. */
+            {
+                const int q = lane >> 4, r16 = lane & 15;
+                const float4 ae = *(const float4 *)&T.ce[r16][4 * q];
+                const float4 ao = *(const float4 *)&T.co[r16][4 * q];
+                const float Ae[4] = {ae.x, ae.y, ae.z, ae.w}, Ao[4] = {ao.x, ao.y, ao.z, ao.w};
+                float Be[3][4], Bo[3][4];
+#pragma unroll
+                for (int nt = 0; nt < 3; nt++) {
+                    int n = 16 * nt + r16;
+                    n = n < 36 ? n : 35;
+                    const float4 a4 = *(const float4 *)&sBuf[n * SROW + 4 * q];
+                    const float4 b4 = *(const float4 *)&sBuf[n * SROW + 28 - 4 * q]; /* S[31-i] = b4[3-ks] */
+                    const float av[4] = {a4.x, a4.y, a4.z, a4.w}, bv[4] = {b4.w, b4.z, b4.y, b4.x};
+#pragma unroll
+                    for (int ks = 0; ks < 4; ks++) {
+                        Be[nt][ks] = av[ks] + bv[ks];
+                        Bo[nt][ks] = av[ks] - bv[ks];
+                    }
+                }
+                f32x4 ce[3], co[3];
+#pragma unroll
+                for (int nt = 0; nt < 3; nt++) ce[nt] = co[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < 4; ks++)
+#pragma unroll
+                    for (int nt = 0; nt < 3; nt++) {
+                        ce[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ae[ks], Be[nt][ks], ce[nt], 0, 0, 0);
+                        co[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ao[ks], Bo[nt][ks], co[nt], 0, 0, 0);
+                    }
+                wave_sync(); /* all S reads retired before X overwrites them */
+                /* D[row m = 4 q + r][col n] -> X[n][2m] (even), X[n][2m+1] (odd) */
+#pragma unroll
+                for (int nt = 0; nt < 3; nt++) {
+                    const int n = 16 * nt + r16;
+                    if (n < 36) {
+                        *(f32x4 *)&sBuf[n * XROW + 8 * q] = (f32x4){ce[nt][0], co[nt][0], ce[nt][1], co[nt][1]};
+                        *(f32x4 *)&sBuf[n * XROW + 8 * q + 4] = (f32x4){ce[nt][2], co[nt][2], ce[nt][3], co[nt][3]};
+                    }
+                }
+            }
+            wave_sync();
+            /* ---------------- phase W: 512-tap window -> PCM --------------- */
+            {
+                float Dw[16];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const float4 d = *(const float4 *)&T.dw[sb][4 * i];
+                    Dw[4 * i] = d.x; Dw[4 * i + 1] = d.y; Dw[4 * i + 2] = d.z; Dw[4 * i + 3] = d.w;
+                }
+                float xa[18], xb[18];
+                const int pa = opaque(18 * ch * XROW + wa), pb = opaque(18 * ch * XROW + wb);
+#pragma unroll
+                for (int t = 0; t < 18; t++) {
+                    xa[t] = sBuf[pa + t * XROW];
+                    xb[t] = sBuf[pb + t * XROW];
+                }
+                /* output slots in pairs (t0, t1): lanes 0-31 hold L, lanes
+                 * 32-63 R; one half-wave swap leaves lane j with (L, R) of
+                 * slot t0 and lane 32 + j with (L, R) of slot t1 */
+                /* two output slots (2 tp, 2 tp + 1) at once: packed FMAs
+                 * (v_pk_fma_f32, tap broadcast), half the VALU issues of the
+                 * scalar form; the same fma order per slot, so bit-identical */
+                auto out2 = [&](int tp) {
+                    f32x2 o = {0.f, 0.f};
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        const int ka = 2 * tp - 2 * i, kb = ka - 1;
+                        f32x2 va, vb;
+                        va.x = ka >= 0 ? xa[ka] : ha[ka + 14];
+                        va.y = ka + 1 >= 0 ? xa[ka + 1] : ha[ka + 15];
+                        vb.x = kb >= 0 ? xb[kb] : hb[kb + 15];
+                        vb.y = kb + 1 >= 0 ? xb[kb + 1] : hb[kb + 16];
+                        o = __builtin_elementwise_fma((f32x2){Dw[2 * i], Dw[2 * i]}, va, o);
+                        o = __builtin_elementwise_fma((f32x2){Dw[2 * i + 1], Dw[2 * i + 1]}, vb, o);
+                    }
+                    return o;
+                };
+                auto to_pcm = [&](float v) {
+                    const float p = rintf(v * 32768.f);
+                    return (int)fminf(fmaxf(p, -32768.f), 32767.f);
+                };
+                const int so = f * 2304 * PB + gr * 576 * nch * PB;
+                if (F32) {
+                    /* float sink: the same sums, unscaled and unclipped (FFmpeg's
+                     * float decoder convention); (L, R) = 8 B per lane and slot */
+                    if (nch == 2) {
+                        const int vo = opaque((sb + 32 * ch) * 8);
+#pragma unroll
+                        for (int tp = 0; tp < 9; tp++) {
+                            const f32x2 o = out2(tp);
+                            const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(o.x), __float_as_uint(o.y),
+                                                                            false, false);
+                            __builtin_amdgcn_raw_buffer_store_b64((u32x2){r[0], r[1]}, r_pcm, vo + 512 * tp, so, 0);
+                        }
+                    } else {
+                        const int vo = opaque(sb * 4);
+#pragma unroll
+                        for (int tp = 0; tp < 9; tp++) {
+                            const f32x2 o = out2(tp);
+                            if (active) {
+                                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o.x), r_pcm, vo + 256 * tp, so, 0);
+                                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o.y), r_pcm, vo + 256 * tp + 128, so, 0);
+                            }
+                        }
+                    }
+                } else if (nch == 2) {
+                    const int vo = opaque((sb + 32 * ch) * 4);
+#pragma unroll
+                    for (int tp = 0; tp < 9; tp++) {
+                        const f32x2 o = out2(tp);
+                        const int p0 = to_pcm(o.x), p1 = to_pcm(o.y);
+                        const auto r = __builtin_amdgcn_permlane32_swap(p0, p1, false, false);
+                        __builtin_amdgcn_raw_buffer_store_b32(((uint32_t)r[0] & 0xFFFFu) | ((uint32_t)r[1] << 16),
+                                                              r_pcm, vo + 256 * tp, so, 0);
+                    }
+                } else {
+                    const int vo = opaque(sb * 2);
+#pragma unroll
+                    for (int tp = 0; tp < 9; tp++) {
+                        const f32x2 o = out2(tp);
+                        if (active) {
+                            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)to_pcm(o.x), r_pcm, vo + 128 * tp, so, 0);
+                            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)to_pcm(o.y), r_pcm, vo + 128 * tp + 64, so, 0);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 14; k++) ha[k] = active ? xa[k + 4] : ha[k];
+#pragma unroll
+                for (int k = 0; k < 15; k++) hb[k] = active ? xb[k + 3] : hb[k];
+            }
+            wave_sync(); /* X reads done before the next granule's xr */
+        }
+    }
+    /* state out */
+#pragma unroll
+    for (int i = 0; i < 18; i++) S.overlap[ch][sb][i] = ov[i];
+#pragma unroll
+    for (int k = 0; k < 14; k++) S.fifo[ch][k + 1][wa] = ha[k];
+#pragma unroll
+    for (int k = 0; k < 15; k++) S.fifo[ch][k][wb] = hb[k];
+}
+/* ------------------------------------------------------------------------ */
+/* k_gather_frames: segmented long-stream decode (mp3d_batch_decode_long).  */
+/* Output frame j of the long stream is frame (j - a[k]) of virtual stream  */
+/* k - k0 (k = j / L) in the batch output; copies its PCM row (16-B words)   */
+/* and frame info (zero-filled: rows without audio, the unused part of a   */
+/* mono / LSF row).  One workgroup per output frame.                        */
+/* ------------------------------------------------------------------------ */
+__global__ void __launch_bounds__(256) k_gather_frames(const uint4 *__restrict__ src, uint4 *__restrict__ dst,
+                                                       const DevInfo *__restrict__ isrc, DevInfo *__restrict__ idst,
+                                                       const int *__restrict__ a, int L, int F, int k0, int row16) {
+    const int jl = blockIdx.x;           /* output frame relative to segment k0's first */
+    const int k = jl / L;                /* segment relative to k0                      */
+    const int j = (k0 + k) * L + jl % L; /* global output frame                         */
+    const size_t sf = (size_t)k * F + (j - a[k]);
+    const DevInfo inf = isrc[sf];
+    /* words holding audio: samples x channels of the 2304-sample row (mono
+     * 1152, LSF 576 per channel); the rest is zero-filled */
+    const int lim = inf.samples * inf.channels * row16 / 2304;
+    for (int i = threadIdx.x; i < row16; i += blockDim.x)
+        dst[(size_t)jl * row16 + i] = i < lim ? src[sf * row16 + i] : make_uint4(0u, 0u, 0u, 0u);
+    if (idst && threadIdx.x == 0) idst[jl] = isrc[sf];
+}
+
+
+/* ------------------------------------------------------------------------ */
+/* Host-side launchers                                                       */
+/* ------------------------------------------------------------------------ */
+hipError_t upload_synth_constants(const float *win36, const float *is_ratio, const float *pow2q, const float *is_lsf) {
+    hipError_t e;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_win36), win36, sizeof(float) * 4 * 36))) return e;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_is_ratio), is_ratio, sizeof(float) * 14))) return e;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_pow2q), pow2q, sizeof(float) * 4))) return e;
+    return hipMemcpyToSymbol(HIP_SYMBOL(c_is_lsf), is_lsf, sizeof(float) * 64);
+}
+
+void launch_synth(const FrameRec *rec, const int16_t *is_buf, const UnitMeta *meta, const DevTables *tab,
+                  StreamState *st, void *pcm, bool f32, int n_streams, int F, hipStream_t strm) {
+    const dim3 grid((n_streams + SYN_WAVES - 1) / SYN_WAVES), block(64 * SYN_WAVES);
+    /* both family variants; a workgroup without a stream of its variant
+     * exits after SYN_WAVES scalar loads (the LSF launch on an all-MPEG-1
+     * batch costs only its workgroup dispatch) */
+#define MP3D_SYNTH_LAUNCH(F32_, LSF_)                                                                            \
+    hipLaunchKernelGGL((k_synth<false, F32_, LSF_>), grid, block, 0, strm, rec, is_buf, meta, (const float *)nullptr, \
+                       (const uint8_t *)nullptr, (const uint8_t *)nullptr, tab, st, pcm, n_streams, F, 2, 0)
+    if (f32) {
+        MP3D_SYNTH_LAUNCH(true, false);
+        MP3D_SYNTH_LAUNCH(true, true);
+    } else {
+        MP3D_SYNTH_LAUNCH(false, false);
+        MP3D_SYNTH_LAUNCH(false, true);
+    }
+#undef MP3D_SYNTH_LAUNCH
+}
+
+void launch_synth_xr(const float *xr, const uint8_t *bt, const uint8_t *mixed, const DevTables *tab, StreamState *st,
+                     int16_t *pcm, int n_streams, int F, int nch, int sr, hipStream_t strm) {
+    hipLaunchKernelGGL((k_synth<true, false, false>), dim3((n_streams + SYN_WAVES - 1) / SYN_WAVES), dim3(64 * SYN_WAVES), 0,
+                       strm, (const FrameRec *)nullptr, (const int16_t *)nullptr, (const UnitMeta *)nullptr, xr, bt,
+                       mixed, tab, st, (void *)pcm, n_streams, F, nch, sr);
+}
+
+void launch_gather_frames(const void *src, void *dst, const void *isrc, void *idst, const int *a, int L, int F, int k0,
+                          int n_out, int bytes_per_row, hipStream_t strm) {
+    hipLaunchKernelGGL(k_gather_frames, dim3(n_out), dim3(256), 0, strm, (const uint4 *)src, (uint4 *)dst,
+                       (const DevInfo *)isrc, (DevInfo *)idst, a, L, F, k0, bytes_per_row / 16);
+}
+
+} // namespace mp3d

@@ -100,7 +100,7 @@ def test_tables_present_in_ffmpeg_copy():
 def test_pow43_escape_recipe():
     """k_synth computes |is|^(4/3) for 256 <= |is| <= 8206 (escape values) without
     a table: y = exp2(log2(x) / 3), one Newton step on y^3 = x, times x
-    (pow43_big in mp3d_kernels.hip).  Emulated in float32 with the log/exp
+    (pow43_big in mp3d_synth.hip).  Emulated in float32 with the log/exp
     results perturbed by up to 3 ulp (the hardware v_log_f32 / v_exp_f32 are
     approximate), it stays within 2 ulp of the correctly rounded value."""
     a = np.arange(256, 8207)
