@@ -28,6 +28,8 @@ def variant(name, reps):
 W4H = ("__global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(",
        "__global__ void __launch_bounds__(HUFF_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 8))) k_huffman(")
 VARS = {
+    "CAP2300": [("#define HUFF_CAPW 2400", "#define HUFF_CAPW 2300")],
+    "LUT2400": [("#define HUFF_CAPW 2300", "#define HUFF_CAPW 2400")],
     "DM1": [("const bool lsf = hdr_kind(h1) == 2;", "const bool lsf = false;")],
     "DM2": [("|| (v59 & (7ull << 23)) == (4ull << 23))", ")")],
     "DM3": [("if (kind && hdr_kind(b1) != kind) return -1;", ""),
