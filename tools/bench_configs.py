@@ -10,6 +10,8 @@ timed with synchronize on both sides of --steps calls after --warmup calls:
        M/S / IS, 32 / 44.1 / 48 kHz, short + mixed blocks, CRC on some
        streams (per-stream divergence); frames/s and GB/s on actual bytes
   lsf  MPEG-2/2.5 LSF corpus (16-24 kHz and 8-12 kHz, VBR, all modes)
+  c3_f32  C3 decoded to the float32 PCM sink (9 216 B/frame out)
+  c3_crc  C3 streams with CRC protection, MP3D_OPT_CRC_CHECK on
 
 Usage: python tools/bench_configs.py [--only c2,c5,lsf]"""
 import argparse
@@ -70,36 +72,39 @@ def c2(args):
                     "is the limit (C3's 65 536 streams fill the chip)"}
 
 
-def decode_corpus(args, name, cfg, n, F):
+def decode_corpus(args, name, cfg, n, F, f32=False, opts=0):
     import torch
     import _gen
     import mp3_amd
     buf, offs, sizes = _gen.batch(cfg, 5_000_011, n, F, threads=min(16, os.cpu_count() or 1))
     d_in = torch.from_numpy(buf).cuda()
-    pcm = torch.empty((n, F, 2304), dtype=torch.int16, device="cuda")
+    pcm = torch.empty((n, F, 2304), dtype=torch.float32 if f32 else torch.int16, device="cuda")
     infos = torch.zeros((n, F, 6), dtype=torch.int32, device="cuda")
     dec = mp3_amd.BatchDecoder(n, F)
+    dec.set_options(opts)
     strm = torch.cuda.current_stream().cuda_stream
-    t = timed(lambda: dec.decode(d_in, offs, sizes, F, pcm=pcm, infos=infos, stream=strm), args.steps, args.warmup)
+    t = timed(lambda: dec.decode(d_in, offs, sizes, F, pcm=pcm, infos=infos, stream=strm, f32=f32), args.steps,
+              args.warmup)
     inf = infos.cpu().numpy()
     frames = int((inf[..., 5] > 0).sum())
     samples = int((inf[..., 5] * inf[..., 1]).sum())
     nbytes = int(sizes.astype(np.int64).sum())
     return {"workload": "%s: %d streams x %d frames" % (name, n, F), "frames_per_s": frames / t,
             "ms_per_step": t * 1e3, "frames_with_audio": frames, "in_GBs": nbytes / t / 1e9,
-            "rw_GBs": (nbytes + 2 * samples) / t / 1e9, "mean_frame_bytes": round(nbytes / (n * F), 1),
+            "rw_GBs": (nbytes + (4 if f32 else 2) * samples) / t / 1e9, "mean_frame_bytes": round(nbytes / (n * F), 1),
             "hz_mix": {str(int(h)): int((inf[..., 2] == h).sum()) for h in np.unique(inf[..., 2]) if h}}
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="c2,c5,lsf")
+    ap.add_argument("--only", default="c2,c5,lsf,c3_f32,c3_crc")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--streams", type=int, default=65536)
     ap.add_argument("--frames", type=int, default=32)
     args = ap.parse_args()
     import _gen
+    import mp3_amd
     for w in args.only.split(","):
         if w == "c2":
             r = c2(args)
@@ -109,6 +114,11 @@ def main():
         elif w == "lsf":
             r = decode_corpus(args, "MPEG-2/2.5 LSF corpus (8-24 kHz, VBR, all modes)",
                               dict(_gen.C5, sr_idx=-2, short_pct=15, mixed_pct=25), args.streams, args.frames)
+        elif w == "c3_f32":
+            r = decode_corpus(args, "C3 with the float32 PCM sink", _gen.C3, args.streams, args.frames, f32=True)
+        elif w == "c3_crc":
+            r = decode_corpus(args, "C3 with CRC-protected frames and MP3D_OPT_CRC_CHECK on",
+                              dict(_gen.C3, crc_pct=100), args.streams, args.frames, opts=mp3_amd.OPT_CRC_CHECK)
         else:
             raise SystemExit("unknown workload " + w)
         print(json.dumps(r), flush=True)
