@@ -30,7 +30,7 @@ void launch_demux(const uint8_t *, const uint64_t *, const uint32_t *, uint8_t *
 void launch_huffman(const uint8_t *, const uint64_t *, const FrameRec *, const uint64_t *, const DevTables *, int16_t *,
                     UnitMeta *, int, int, int, hipStream_t);
 void launch_synth(const FrameRec *, const int16_t *, const UnitMeta *, const DevTables *, StreamState *, void *, bool, int,
-                  int, hipStream_t);
+                  int, int, hipStream_t);
 void launch_synth_xr(const float *, const uint8_t *, const uint8_t *, const DevTables *, StreamState *, int16_t *, int,
                      int, int, int, hipStream_t);
 void launch_gather_frames(const void *, void *, const void *, void *, const int *, int, int, int, int, int,
@@ -473,8 +473,11 @@ static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offse
 }
 
 /* decode into int16 (f32 = false) or float32 PCM, both [n][F][2304] */
+/* kinds: k_synth family variants to launch (bit 0 MPEG-1, bit 1 LSF); 3 for
+ * a batch, one bit for the per-frame decoder, which knows its frame's family */
 static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets, const uint32_t *sizes, int n,
-                        int F, void *pcm, bool f32, mp3d_frame_info *infos, void *hip_stream) {
+                        int F, void *pcm, bool f32, mp3d_frame_info *infos, void *hip_stream, bool overwrite,
+                        int kinds = 3) {
     if (!b || !pcm) return MP3D_E_ARG;
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : b->own;
     bool sync_needed = false;
@@ -487,11 +490,12 @@ static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *of
         r = grow((void **)&b->d_pcm, &b->pcm_cap, pcm_bytes);
         if (r) return r;
         dpcm = b->d_pcm;
-        /* frames without audio leave the caller's PCM untouched */
-        HIPCHK(hipMemcpyAsync(dpcm, pcm, pcm_bytes, hipMemcpyHostToDevice, s));
+        /* frames without audio leave the caller's PCM untouched (internal
+         * callers that read only the audio rows skip the copy) */
+        if (!overwrite) HIPCHK(hipMemcpyAsync(dpcm, pcm, pcm_bytes, hipMemcpyHostToDevice, s));
     }
     DeviceCtx &dc = g_dev[b->device];
-    launch_synth(b->rec, b->is_buf, b->meta, dc.tables, b->st, dpcm, f32, n, F, s);
+    launch_synth(b->rec, b->is_buf, b->meta, dc.tables, b->st, dpcm, f32, n, F, kinds, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[3], s));
     HIPCHK(hipGetLastError());
     if (pcm_host) {
@@ -513,13 +517,13 @@ static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *of
 
 extern "C" int mp3d_batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets, const uint32_t *sizes,
                                  int n, int F, int16_t *pcm, mp3d_frame_info *infos, void *hip_stream) {
-    return batch_decode(b, frames, offsets, sizes, n, F, pcm, false, infos, hip_stream);
+    return batch_decode(b, frames, offsets, sizes, n, F, pcm, false, infos, hip_stream, false);
 }
 
 extern "C" int mp3d_batch_decode_f32(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets,
                                      const uint32_t *sizes, int n, int F, float *pcm, mp3d_frame_info *infos,
                                      void *hip_stream) {
-    return batch_decode(b, frames, offsets, sizes, n, F, pcm, true, infos, hip_stream);
+    return batch_decode(b, frames, offsets, sizes, n, F, pcm, true, infos, hip_stream, false);
 }
 
 extern "C" int mp3d_batch_huffman_only(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets,
@@ -705,7 +709,8 @@ extern "C" int mp3d_long_plan(const uint8_t *data, size_t bytes, int L, long lon
 }
 
 static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets, const uint32_t *sizes, int n,
-                        int F, void *pcm, bool f32, mp3d_frame_info *infos, void *hip_stream);
+                        int F, void *pcm, bool f32, mp3d_frame_info *infos, void *hip_stream, bool overwrite,
+                        int kinds);
 
 extern "C" int mp3d_batch_decode_long(mp3d_batch *b, const uint8_t *data, size_t bytes, int L, void *pcm, int f32,
                                       long long max_frames, mp3d_frame_info *infos, long long *n_frames,
@@ -781,7 +786,7 @@ extern "C" int mp3d_batch_decode_long(mp3d_batch *b, const uint8_t *data, size_t
         }
         /* fresh decoder state for every virtual stream */
         LCHK(hipMemsetAsync(b->st, 0, sizeof(StreamState) * ns, s));
-        rc = batch_decode(b, din, so.data(), ss.data(), ns, F, seg_pcm, f32 != 0, nullptr, s);
+        rc = batch_decode(b, din, so.data(), ss.data(), ns, F, seg_pcm, f32 != 0, nullptr, s, false);
         if (rc) goto done;
         if (k0 == 0 && sinfo) rc = mp3d_batch_stream_info(b, 1, sinfo);
         if (rc) goto done;
@@ -807,11 +812,27 @@ done:
 /* ------------------------------------------------------------------------ */
 /* Per-frame decoder                                                         */
 /* ------------------------------------------------------------------------ */
+/* Per-frame decoder: a one-stream batch plus pinned staging, so a call is
+ * one small DMA each way and one stream sync.  The frame is staged
+ * zero-padded to a fixed MP3D_PF_BYTES, which keeps the batch geometry
+ * constant (uploaded once) across calls. */
+#define MP3D_PF_BYTES 4096
 struct mp3d_dec {
     mp3d_batch *b = nullptr;
     long frames = 0;
     int kind = 0; /* MPEG family of the stream's first frame (StreamState.kind) */
+    uint8_t *h_in = nullptr;            /* pinned: the frame, zero-padded      */
+    float *h_out = nullptr;             /* pinned: one frame of PCM            */
+    mp3d_frame_info *h_info = nullptr;  /* pinned: its frame info              */
 };
+
+static void dec_free(mp3d_dec *d) {
+    if (d->b) mp3d_batch_destroy(d->b);
+    if (d->h_in) (void)hipHostFree(d->h_in);
+    if (d->h_out) (void)hipHostFree(d->h_out);
+    if (d->h_info) (void)hipHostFree(d->h_info);
+    delete d;
+}
 
 extern "C" int mp3d_dec_create_on(int device, mp3d_dec **out) {
     if (!out) return MP3D_E_ARG;
@@ -820,8 +841,14 @@ extern "C" int mp3d_dec_create_on(int device, mp3d_dec **out) {
     if (!d) return MP3D_E_NOMEM;
     int r = mp3d_batch_create(device, 1, 1, &d->b);
     if (r) {
-        delete d;
+        dec_free(d);
         return r;
+    }
+    if (hipHostMalloc((void **)&d->h_in, MP3D_PF_BYTES) != hipSuccess ||
+        hipHostMalloc((void **)&d->h_out, sizeof(float) * 2304) != hipSuccess ||
+        hipHostMalloc((void **)&d->h_info, sizeof(mp3d_frame_info)) != hipSuccess) {
+        dec_free(d);
+        return MP3D_E_NOMEM;
     }
     *out = d;
     return MP3D_OK;
@@ -835,8 +862,7 @@ extern "C" int mp3d_dec_create(mp3d_dec **out) {
 
 extern "C" void mp3d_dec_destroy(mp3d_dec *d) {
     if (!d) return;
-    mp3d_batch_destroy(d->b);
-    delete d;
+    dec_free(d);
 }
 
 extern "C" void mp3d_dec_reset(mp3d_dec *d) {
@@ -898,11 +924,15 @@ static int decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, void *pcm
         return info->frame_bytes ? 0 : MP3D_E_NEED_MORE;
     }
     uint64_t off = 0;
-    uint32_t sz = (uint32_t)fb;
-    float out[2304]; /* large enough for either sample type */
-    mp3d_frame_info fi;
-    int r = batch_decode(d->b, buf + pos, &off, &sz, 1, 1, out, f32, &fi, nullptr);
+    uint32_t sz = MP3D_PF_BYTES;
+    memcpy(d->h_in, buf + pos, (size_t)fb); /* fb <= MP3D_MAX_FRAME_BYTES */
+    memset(d->h_in + fb, 0, MP3D_PF_BYTES - (size_t)fb);
+    /* PCM straight into pinned memory: only the audio rows are read back */
+    int r = batch_decode(d->b, d->h_in, &off, &sz, 1, 1, d->h_out, f32, d->h_info, nullptr, true,
+                         host_frame_kind(buf + pos)); /* 1 MPEG-1, 2 LSF */
     if (r) return r;
+    const mp3d_frame_info fi = *d->h_info;
+    const float *out = d->h_out;
     d->frames++;
     if (fi.frame_bytes) d->kind = host_frame_kind(buf + pos);
     *info = fi;

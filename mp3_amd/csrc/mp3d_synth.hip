@@ -772,20 +772,21 @@ hipError_t upload_synth_constants(const float *win36, const float *is_ratio, con
 }
 
 void launch_synth(const FrameRec *rec, const int16_t *is_buf, const UnitMeta *meta, const DevTables *tab,
-                  StreamState *st, void *pcm, bool f32, int n_streams, int F, hipStream_t strm) {
+                  StreamState *st, void *pcm, bool f32, int n_streams, int F, int kinds, hipStream_t strm) {
     const dim3 grid((n_streams + SYN_WAVES - 1) / SYN_WAVES), block(64 * SYN_WAVES);
-    /* both family variants; a workgroup without a stream of its variant
-     * exits after SYN_WAVES scalar loads (the LSF launch on an all-MPEG-1
-     * batch costs only its workgroup dispatch) */
+    /* the family variants in `kinds` (bit 0 MPEG-1, bit 1 LSF; a batch
+     * launches both); a workgroup without a stream of its variant exits
+     * after SYN_WAVES scalar loads (the LSF launch on an all-MPEG-1 batch
+     * costs only its workgroup dispatch) */
 #define MP3D_SYNTH_LAUNCH(F32_, LSF_)                                                                            \
     hipLaunchKernelGGL((k_synth<false, F32_, LSF_>), grid, block, 0, strm, rec, is_buf, meta, (const float *)nullptr, \
                        (const uint8_t *)nullptr, (const uint8_t *)nullptr, tab, st, pcm, n_streams, F, 2, 0)
     if (f32) {
-        MP3D_SYNTH_LAUNCH(true, false);
-        MP3D_SYNTH_LAUNCH(true, true);
+        if (kinds & 1) MP3D_SYNTH_LAUNCH(true, false);
+        if (kinds & 2) MP3D_SYNTH_LAUNCH(true, true);
     } else {
-        MP3D_SYNTH_LAUNCH(false, false);
-        MP3D_SYNTH_LAUNCH(false, true);
+        if (kinds & 1) MP3D_SYNTH_LAUNCH(false, false);
+        if (kinds & 2) MP3D_SYNTH_LAUNCH(false, true);
     }
 #undef MP3D_SYNTH_LAUNCH
 }
