@@ -237,29 +237,52 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
     const __amdgpu_buffer_rsrc_t r_pcm = __builtin_amdgcn_make_buffer_rsrc(
         (void *)((uint8_t *)pcm + (size_t)s * F * 2304 * PB), 0, F * 2304 * PB, 0x00020000);
 
-    /* granule prefetch, one granule ahead of use: is[] words (lane owns
-     * lines 2 lane + 128 i, +1), UnitMeta words of both channels (lanes
-     * 0 .. 27) and the granule's FrameRec words (lanes 32 .. 39) */
-    uint32_t nis[2][5], nmeta = 0;
-    auto prefetch = [&](int g) { /* g = granule index inside the stream */
+    /* granule prefetch: is[] words one granule ahead of use (lane owns
+     * lines 2 lane + 128 i, +1), the UnitMeta words of both channels (lanes
+     * 0 .. 27) and the FrameRec words (lanes 32 .. 39) TWO granules ahead,
+     * so each is[] load is masked by its unit's nz_end: the rzero tail that
+     * k_huffman never wrote is not fetched (HBM read traffic ~ nonzero
+     * prefix, not 2 x 576 lines).  nmeta = words of the current granule,
+     * nmeta2 = words of the next one. */
+    uint32_t nis[2][5], nmeta = 0, nmeta2 = 0;
+    constexpr int GSTEP = LSF ? 2 : 1; /* is[] granule slots per decoded granule */
+    auto load_words = [&](int g) { /* buffer loads past F return 0 */
+        const int lo = opaque(lane * 4);
+        uint32_t v = 0u;
+        if (lane < 2 * MW) v = __builtin_amdgcn_raw_buffer_load_b32(r_meta, lo, g * 2 * (int)sizeof(UnitMeta), 0);
+        else if (lane >= 32 && lane < 40)
+            v = __builtin_amdgcn_raw_buffer_load_b32(r_rec, lo - 128, (g >> 1) * (int)sizeof(FrameRec), 0);
+        return v;
+    };
+    auto load_is = [&](int g, int nz0, int nz1) {
         const int lo = opaque(lane * 4);
 #pragma unroll
-        for (int c = 0; c < 2; c++)
+        for (int c = 0; c < 2; c++) {
+            const int nz = c ? nz1 : nz0;
 #pragma unroll
-            for (int i = 0; i < 4; i++)
-                nis[c][i] = __builtin_amdgcn_raw_buffer_load_b32(r_is, lo + c * 1152 + 256 * i, g * gb, 0);
-        nis[0][4] = nis[1][4] = 0u;
-        if (lane < 32) {
-            nis[0][4] = __builtin_amdgcn_raw_buffer_load_b32(r_is, lo + 1024, g * gb, 0);
-            nis[1][4] = __builtin_amdgcn_raw_buffer_load_b32(r_is, lo + 1152 + 1024, g * gb, 0);
+            for (int i = 0; i < 5; i++) {
+                nis[c][i] = 0u;
+                if ((i < 4 || lane < 32) && 2 * lane + 128 * i < nz)
+                    nis[c][i] = __builtin_amdgcn_raw_buffer_load_b32(r_is, lo + c * 1152 + 256 * i, g * gb, 0);
+            }
         }
-        nmeta = 0u;
-        if (lane < 2 * MW) nmeta = __builtin_amdgcn_raw_buffer_load_b32(r_meta, lo, g * 2 * (int)sizeof(UnitMeta), 0);
-        else if (lane >= 32 && lane < 40)
-            nmeta = __builtin_amdgcn_raw_buffer_load_b32(r_rec, lo - 128, (g >> 1) * (int)sizeof(FrameRec), 0);
+    };
+    /* steady state: is[g] masked by nmeta2's nz_end (granule g), then shift */
+    auto prefetch = [&](int g) {
+        const int nz0 = __builtin_amdgcn_readlane((int)nmeta2, 12) & 0xFFFF;
+        const int nz1 = __builtin_amdgcn_readlane((int)nmeta2, MW + 12) & 0xFFFF;
+        load_is(g, nz0, nz1);
+        nmeta = nmeta2;
+        nmeta2 = load_words(g + GSTEP);
+    };
+    /* entry and after a frame without audio: unmasked, then drained */
+    auto prefetch_full = [&](int g) {
+        load_is(g, 576, 576);
+        nmeta = load_words(g);
+        nmeta2 = load_words(g + GSTEP);
     };
     if (!SRC_XR) {
-        prefetch(0);
+        prefetch_full(0);
         /* explicit drain on the entry path, so the compiler's wait before
          * each prefetch use is set by the loop path (stores after it) */
         WAIT_VMCNT0();
@@ -280,7 +303,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
             if (!(r4 & 0xFFFFu) || (first_gr & (REC_TAG | REC_DROP))) {
                 /* no audio in this frame: fetch the next frame's granule 0
                  * now and wait for it here, off the common path */
-                if (f + 1 < F) prefetch(2 * (f + 1));
+                if (f + 1 < F) prefetch_full(2 * (f + 1));
                 WAIT_VMCNT0();
                 continue;
             }
@@ -636,6 +659,13 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
             }
             wave_sync();
             /* ---------------- phase W: 512-tap window -> PCM --------------- */
+            /* Drain vmcnt HERE, before this granule's PCM stores: the next
+             * granule's prefetch (issued in phase Q, then I and M ran) and the
+             * previous granule's stores are long done, and with no load left
+             * pending the compiler needs no wait after the stores.  (Its
+             * waitcnt pass treats loads and stores pending together as out of
+             * order and would otherwise emit vmcnt(0) right after them.) */
+            if (!SRC_XR) WAIT_VMCNT0();
             {
                 float Dw[16];
 #pragma unroll
