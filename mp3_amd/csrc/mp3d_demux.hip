@@ -204,7 +204,7 @@ __global__ void __launch_bounds__(64) k_demux(const uint8_t *__restrict__ in, co
         DevInfo inf = {0, 0, 0, 0, 0, 0};
         uint64_t sw = 0; /* lane q < 4: side word of unit q = gr * 2 + ch */
         bool copy = false;
-        uint32_t src_off = 0;
+        uint32_t src_off = 0, frame_at = 0; /* payload and header positions in the stream */
         if (fb > 0) {
             if (w.pos != cur) w = load_win(p0, len, cur, lane);
             const uint32_t h1 = win_byte(w, 1), h2 = win_byte(w, 2), h3 = win_byte(w, 3);
@@ -315,6 +315,7 @@ __global__ void __launch_bounds__(64) k_demux(const uint8_t *__restrict__ in, co
                 r.payload_avail = (uint16_t)(av < r.payload_len ? av : r.payload_len);
                 copy = !(r.first_gr & REC_TAG);
                 src_off = cur + body;
+                frame_at = cur;
                 cur = have == (uint32_t)fb ? cur + (uint32_t)fb : len;
             } else {
                 cur = len;
@@ -333,20 +334,54 @@ __global__ void __launch_bounds__(64) k_demux(const uint8_t *__restrict__ in, co
             for (uint32_t i = L + lane; i < r.payload_len; i += 64) dst[Pm + i] = 0; /* cut-short final frame */
             const uint32_t h = min((4u - (Pm & 3u)) & 3u, L);     /* head bytes up to an aligned word */
             const uint32_t wb = (Pm + h) >> 2, we = (Pm + L) >> 2; /* whole words [wb, we)           */
-            if ((uint32_t)lane < h) dst[Pm + lane] = src[lane];
             /* tail bytes [t0, L) after the last whole word -- or after the head
              * when there is none (an LSF payload can be < 8 bytes) */
             const uint32_t t0 = 4u * we > Pm + h ? 4u * we - Pm : h; /* h <= t0 <= L */
-            if ((uint32_t)lane < L - t0) dst[Pm + t0 + lane] = src[t0 + lane];
+            /* edge-byte loads first, stored after the words' loads: every
+             * load of the payload is in flight before the first store waits */
+            /* (unconditional: lanes without an edge byte re-read the frame's
+             * first header byte, which is always in the stream) */
+            const uint8_t *hb0 = p0 + frame_at;
+            const uint8_t hbv = *((uint32_t)lane < h ? src + lane : hb0);
+            const uint8_t tbv = *((uint32_t)lane < L - t0 ? src + t0 + lane : hb0);
             if (wb < we) {
-                const uint64_t sa0 = (uint64_t)(src + (4u * wb - Pm));
-                const uint32_t sh = (uint32_t)(sa0 & 3u) * 8u;
-                const uint32_t *swd = (const uint32_t *)(sa0 & ~(uint64_t)3);
-                for (uint32_t k = lane; k < we - wb; k += 64) {
-                    const uint32_t lo = swd[k];
-                    ((uint32_t *)dst)[wb + k] = sh ? __builtin_amdgcn_alignbit(swd[k + 1], lo, sh) : lo;
+                /* pointer arithmetic, not an integer round trip: the loads
+                 * stay global_load (a flat load waits on lgkmcnt too) */
+                const uint8_t *sb = src + (4u * wb - Pm);
+                const uint32_t mis = (uint32_t)((uintptr_t)sb & 3u);
+                const uint32_t sh = mis * 8u;
+                const uint32_t *swd = (const uint32_t *)(sb - mis);
+                /* all words in flight before the first store (straight-line,
+                 * so no loop-header wait drains them early): one load latency
+                 * per frame instead of one per 64-word round; the next header
+                 * window (issued above) lands with them.  A payload is at most
+                 * 1437 B (1441-B frame) = 360 words < 6 x 64. */
+                /* Loads are unconditional (lanes past the payload re-read word
+                 * 0) and the shift is branch-free (alignbit by 0 = lo): with a
+                 * load under a branch the compiler's waitcnt pass loses track
+                 * at the join and drains vmcnt before every store.  The high
+                 * word is read only for a misaligned source (index select, not
+                 * a branch): it then still holds payload bytes. */
+                const uint32_t nwd = we - wb;
+                uint32_t v[6];
+#pragma unroll
+                for (int j = 0; j < 6; j++) {
+                    const uint32_t k = 64u * j + (uint32_t)lane;
+                    const uint32_t kk = k < nwd ? k : 0u;
+                    v[j] = __builtin_amdgcn_alignbit(swd[sh ? kk + 1 : kk], swd[kk], sh);
+                }
+#pragma unroll
+                for (int j = 0; j < 6; j++) {
+                    const uint32_t k = 64u * j + (uint32_t)lane;
+                    if (k < nwd) ((uint32_t *)dst)[wb + k] = v[j];
+                }
+                for (uint32_t k = 384u + (uint32_t)lane; k < nwd; k += 64) { /* not reached (see above) */
+                    const uint32_t l = swd[k];
+                    ((uint32_t *)dst)[wb + k] = sh ? __builtin_amdgcn_alignbit(swd[k + 1], l, sh) : l;
                 }
             }
+            if ((uint32_t)lane < h) dst[Pm + lane] = hbv;
+            if ((uint32_t)lane < L - t0) dst[Pm + t0 + lane] = tbv;
         }
     }
     /* carry: the last min(avail, 512) md bytes become the next call's carry-in */
