@@ -152,7 +152,7 @@ __device__ uint32_t parse_info_tag(const uint8_t *t, uint32_t n, uint32_t &frame
     return info;
 }
 
-__global__ void __launch_bounds__(64) k_demux(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) k_demux(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
                                               const uint32_t *__restrict__ in_len, uint8_t *__restrict__ md,
                                               const uint64_t *__restrict__ md_off, StreamState *__restrict__ st,
                                               FrameRec *__restrict__ rec, uint64_t *__restrict__ sideu,
