@@ -1,27 +1,46 @@
 #!/usr/bin/env python3
 """Benchmark: stereo MP3 frames/s (128 kbps, 44.1 kHz) on MI355X.
 
-Workload (BASELINE.json configs[2]): 65,536 synthetic CBR
-128 kbps 44.1 kHz joint-stereo streams x 32 frames per step, per GPU.  A step
-is one mp3d_batch_decode call over every stream's next 32 frames (the full
-hot path: demux + reservoir + Huffman + requantise/stereo + IMDCT +
-polyphase synthesis -> int16 PCM), inputs resident in HBM, PCM written to
-HBM.  Per-stream decoder state stays resident across steps.
+Workloads (BASELINE.json configs); --config picks one:
+  3 (default)  65,536 synthetic CBR 128 kbps 44.1 kHz joint-stereo streams x 32
+               frames per GPU per step: one mp3d_batch_decode call over every
+               stream's next 32 frames (the full hot path: demux + reservoir +
+               Huffman + requantise/stereo + IMDCT + polyphase synthesis ->
+               int16 PCM), inputs resident in HBM, PCM written to HBM,
+               per-stream decoder state resident across steps.  At --gpus 8
+               this is configs[3] (C4: 524,288 streams over 8 GPUs).
+  2            1,024 streams x 64 frames, IMDCT + polyphase synthesis only from
+               synthetic spectra (mp3d_batch_synth_only), per GPU.
+  5            mixed corpus (VBR 32-320 kbps, mono / stereo / M/S / IS,
+               32 / 44.1 / 48 kHz, short + mixed blocks, CRC), 65,536 x 32 per GPU.
+  1            one 128 kbps stream (tests/golden/keypress_128k_js.mp3) through
+               the per-frame drop-in call (mp3d_decode_frame), host buffers.
 
-Multi-GPU: one process per GPU (torchrun), streams sharded by global stream
-id (seed 3_000_003 + id), no collective on the data path -> weak scaling.
+Multi-GPU: one process per GPU.  `bench.py --gpus N` without WORLD_SIZE in
+the environment starts the N rank processes itself (fresh children, before
+anything touches a GPU; the parent never does) and relays rank 0's JSON line;
+under torchrun (WORLD_SIZE set) it is one rank.  Streams are sharded by global
+stream id (seed base + id), no collective on the data path -> weak scaling.
 Timing: barrier + synchronize on both sides of exactly K steps, max over
-ranks.  The dominant kernel's duration comes from HIP events recorded on
-the stream the kernels run on (mp3d_batch_kernel_times).
+ranks.  --gather adds a second timed loop in which an RCCL PCM gather of step
+k to rank 0 runs on the process group's stream while step k+1 decodes; it is
+reported apart and never enters `value`.  The dominant kernel's duration
+comes from HIP events on the stream the kernels run on
+(mp3d_batch_kernel_times).
 
-The CPU baseline is the oracle restatement (oracle/liboracle.so, "port")
-on a bounded sample of the same workload, rank 0 only.
+The CPU baseline (rank 0, N = 1 only) is the oracle restatement built in
+single precision at -O3 with AVX-512 (oracle/liboracle_f32.so, "port": the
+reference has no decoder to build), timed on a bounded sample of the same
+input on the host threads this process may use, plus single-thread points
+for it and for the double-precision checker build.
 """
 import argparse
 import ctypes
 import json
 import os
 import pathlib
+import socket
+import subprocess
 import sys
 import threading
 import time
@@ -32,6 +51,7 @@ ROOT = pathlib.Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "tests"))
 
+METRIC = "stereo MP3 frames/s (128 kbps 44.1 kHz) at 1/2/4/8 GPU; % HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md)
 FP32_PEAK_TFLOPS = 157.3       # FP32 vector == FP32 MFMA (MI355X_MICROARCH.md)
 BYTES_IN_PER_FRAME = 417.96    # 128 kbps @ 44.1 kHz
@@ -39,68 +59,283 @@ PCM_BYTES_PER_FRAME = 4608.0   # 1152 x 2 ch x int16
 # algorithmic FLOPs per stereo frame: dense 32x32 matrixing
 # + 512-tap window per slot (72 slot-channels) + IMDCT (4 units x 32 sb x 2*18*18)
 FLOP_PER_FRAME = 72 * (2 * 32 * 32 + 2 * 512) + 4 * 32 * 2 * 18 * 18
+# FLOPs k_synth actually issues per stereo frame: fast 36-point
+# IMDCT ~250 per (unit, subband) incl. window + overlap (4 x 32 x 250), the
+# butterfly-halved matrixing on 48 MFMA columns (2 gr x 24 x 2 048) + its
+# butterfly adds (2 x 36 x 32), the window (72 x 1 024), requantise (4 x 576 x 2)
+EXEC_FLOP_PER_FRAME = 4 * 32 * 250 + 2 * 24 * 2048 + 2 * 36 * 32 + 72 * 1024 + 4 * 576 * 2
 # MFMA work of the DCT tile (phase M): 24 v_mfma_f32_16x16x4_f32 (2 048 flop
 # each) per granule, 2 granules per frame -- the butterfly-halved matrixing
 MFMA_FLOP_PER_FRAME = 2 * 24 * 2048
-# k_synth algorithmic bytes per frame: is[] int16 in (4 x 576 x 2) + PCM out
-SYNTH_BYTES_PER_FRAME = 4 * 576 * 2 + PCM_BYTES_PER_FRAME
+# C2 algorithmic bytes per frame: xr f32 in (2 gr x 2 ch x 576 x 4) + PCM out
+C2_BYTES_PER_FRAME = 2 * 2 * 576 * 4 + PCM_BYTES_PER_FRAME
+C2_FLOP_PER_FRAME = FLOP_PER_FRAME  # IMDCT + matrixing + window (requantise is outside C2)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(buf, offs, sizes, F, threads=None, budget_s=12.0):
-    """Oracle (scalar C restatement, oracle/liboracle.so) decoding the first
-    streams of the SAME C3 input the GPU decodes, one stream per task on all
-    host threads, stopping after ~budget_s seconds (bounded sample)."""
+def host_threads():
+    """Host threads this process may use: the box's CPU share (OMP_NUM_THREADS
+    is set to it on the GPU box) within the affinity mask."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
+
+
+def cpu_model():
+    try:
+        return next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except (OSError, StopIteration):
+        return ""
+
+
+# ----------------------------------------------------------------------------
+# CPU baseline (oracle restatement; test infrastructure, timed, never shipped)
+# ----------------------------------------------------------------------------
+def _oracle_libs():
     import _oracle
-    threads = threads or min(16, os.cpu_count() or 1)
-    L = _oracle.lib()
-    n_streams = len(offs)
-    out = [np.zeros((2, F * 1152), np.float32) for _ in range(threads)]
-    _oracle.decode_stream(bytes(buf[offs[0]:offs[0] + sizes[0]]), F)  # init tables before threads
+    L64 = _oracle.lib()
+    p32 = ROOT / "oracle" / "liboracle_f32.so"
+    if not p32.exists():
+        subprocess.check_call(["make", "-s", "-C", str(ROOT / "oracle")])
+    L32 = ctypes.CDLL(str(p32))
+    for L in (L32,):
+        L.orc_decode_stream.argtypes = L64.orc_decode_stream.argtypes
+        L.orc_decode_stream.restype = ctypes.c_long
+        L.orc_create.restype = ctypes.c_void_p
+        L.orc_destroy.argtypes = [ctypes.c_void_p]
+        L.orc_synth_only.argtypes = L64.orc_synth_only.argtypes
+    return L32, L64
+
+
+def _timed_pool(task, n_tasks, threads, budget_s):
+    """Run task(i, tid) -> frames for i = 0.. on `threads` threads until the
+    budget is spent (ctypes drops the GIL inside the C call)."""
     done = [0] * threads
-    streams_done = [0] * threads
-    t_end = [0.0]
+    tasks = [0] * threads
+    t_end = time.perf_counter() + budget_s
 
     def work(tid):
-        nch, hz = ctypes.c_int(), ctypes.c_int()
-        for s in range(tid, n_streams, threads):
-            if time.perf_counter() > t_end[0]:
+        for i in range(tid, n_tasks, threads):
+            if time.perf_counter() > t_end:
                 break
-            d = bytes(buf[offs[s]:offs[s] + sizes[s]])
-            done[tid] += L.orc_decode_stream(d, len(d), out[tid].ctypes.data, F, ctypes.byref(nch), ctypes.byref(hz))
-            streams_done[tid] += 1
+            done[tid] += task(i, tid)
+            tasks[tid] += 1
 
     t0 = time.perf_counter()
-    t_end[0] = t0 + budget_s
     ts = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
     for t in ts:
         t.start()
     for t in ts:
         t.join()
-    dt = time.perf_counter() - t0
-    frames = sum(done)
-    # single-thread point on a short sample (SURVEY §8(d): single- and all-core)
-    t1, f1 = time.perf_counter(), 0
-    nch, hz = ctypes.c_int(), ctypes.c_int()
-    for s in range(n_streams - 1, -1, -1):
-        if time.perf_counter() - t1 > budget_s / 4:
-            break
-        d = bytes(buf[offs[s]:offs[s] + sizes[s]])
-        f1 += L.orc_decode_stream(d, len(d), out[0].ctypes.data, F, ctypes.byref(nch), ctypes.byref(hz))
-    dt1 = time.perf_counter() - t1
-    model = ""
-    try:
-        model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
-    except (OSError, StopIteration):
-        pass
+    return sum(done), sum(tasks), time.perf_counter() - t0
+
+
+def cpu_baseline_decode(buf, offs, sizes, F, budget_s=12.0):
+    """Oracle decoding the SAME input the GPU decodes, one stream per task."""
+    L32, L64 = _oracle_libs()
+    threads = host_threads()
+    outs = [np.zeros((2, F * 1152), np.float32) for _ in range(threads)]
+    n = len(offs)
+
+    def task_for(L):
+        def task(s, tid):
+            nch, hz = ctypes.c_int(), ctypes.c_int()
+            d = bytes(buf[offs[s]:offs[s] + sizes[s]])
+            return L.orc_decode_stream(d, len(d), outs[tid].ctypes.data, F, ctypes.byref(nch), ctypes.byref(hz))
+        return task
+
+    task_for(L32)(0, 0)  # tables initialised before the threads start
+    task_for(L64)(0, 0)
+    frames, streams, dt = _timed_pool(task_for(L32), n, threads, budget_s)
+    f1, _, dt1 = _timed_pool(task_for(L32), n, 1, budget_s / 6)
+    g1, _, gt1 = _timed_pool(task_for(L64), n, 1, budget_s / 6)
     return {"value": frames / dt, "unit": "frames/s", "cores": threads, "kind": "port",
-            "single_thread_value": f1 / dt1, "cpu_model": model, "host_cpus": os.cpu_count(),
-            "sample": "first %d streams x %d frames (%d frames) of the same C3 input, decoded by "
-                      "oracle/liboracle.so (double-precision scalar restatement, gcc -O2) on %d host threads in "
-                      "%.1f s; single thread: %d frames in %.1f s" % (sum(streams_done), F, frames, threads, dt, f1, dt1)}
+            "single_thread_value": f1 / dt1, "f64_single_thread_value": g1 / gt1,
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+            "sample": "first %d streams x %d frames (%d frames) of the same input, decoded by oracle/liboracle_f32.so "
+                      "(the oracle restatement in float32, gcc -O3 -march=x86-64-v4) on %d host threads (the "
+                      "process's CPU share) in %.1f s; single thread %d frames in %.1f s; the double-precision "
+                      "checker build (-O2) %d frames in %.1f s on one thread"
+                      % (streams, F, frames, threads, dt, f1, dt1, g1, gt1)}
+
+
+def cpu_baseline_synth(xr, bt, mx, nch, budget_s=10.0):
+    """Oracle stages a8..a11 (orc_synth_only) on the same C2 spectra."""
+    L32, _ = _oracle_libs()
+    threads = host_threads()
+    n, F = xr.shape[0], xr.shape[1]
+    pcms = [np.zeros((F, 1152, nch), np.int16) for _ in range(threads)]
+
+    def task(s, tid):
+        d = L32.orc_create()
+        L32.orc_synth_only(d, xr[s].ctypes.data, bt[s].ctypes.data, mx[s].ctypes.data, F, nch, 0,
+                           pcms[tid].ctypes.data, None)
+        L32.orc_destroy(d)
+        return F
+
+    task(0, 0)
+    frames, streams, dt = _timed_pool(task, n, threads, budget_s)
+    f1, _, dt1 = _timed_pool(task, n, 1, budget_s / 4)
+    return {"value": frames / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+            "single_thread_value": f1 / dt1, "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+            "sample": "first %d streams x %d frames of the same C2 spectra through orc_synth_only "
+                      "(oracle/liboracle_f32.so, float32 -O3 -march=x86-64-v4) on %d threads in %.1f s"
+                      % (streams, F, threads, dt)}
+
+
+# ----------------------------------------------------------------------------
+# Rank launcher (--gpus N without torchrun)
+# ----------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n):
+    """Start n rank processes of this script (one per GPU) and relay rank
+    0's stdout.  The parent touches no GPU: the children are fresh processes,
+    not forks or execs of a process that has initialised HIP.  Exits with the
+    first non-zero child status (the other ranks are then terminated)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", str(pathlib.Path(__file__).resolve())] + sys.argv[1:],
+                                      env=env, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out = []
+    relay = threading.Thread(target=lambda: out.extend(procs[0].stdout), daemon=True)
+    relay.start()
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            break
+        if all(c == 0 for c in codes):
+            break
+        time.sleep(0.2)
+    relay.join(timeout=10)
+    for line in out:
+        sys.stdout.write(line.decode())
+    sys.stdout.flush()
+    if rc:
+        log("bench.py: a rank exited with status %d" % rc)
+    return rc
+
+
+# ----------------------------------------------------------------------------
+# Workloads
+# ----------------------------------------------------------------------------
+class Ctx:
+    pass
+
+
+def setup_decode(c, cfg_name):
+    import torch
+    import _gen
+    import mp3_amd
+    from mp3_amd import shard
+    cfg = _gen.C3 if cfg_name == "c3" else _gen.C5
+    base = shard.BASE_SEED_C3 if cfg_name == "c3" else 5_000_011
+    t0 = time.time()
+    buf, offs, sizes = _gen.batch(cfg, shard.shard_seed_base(c.rank, c.n, base), c.n, c.F,
+                                  threads=min(16, host_threads()))
+    log("rank %d: generated %d streams x %d frames (%.1f MB) in %.1fs" % (c.rank, c.n, c.F, buf.size / 1e6,
+                                                                        time.time() - t0))
+    c.buf, c.offs, c.sizes = buf, offs, sizes
+    c.d_in = torch.from_numpy(buf).to(c.dev)
+    c.pcm = [torch.empty((c.n, c.F, 2304), dtype=torch.int16, device=c.dev) for _ in range(2 if c.gather else 1)]
+    c.infos = torch.zeros((c.n, c.F, 6), dtype=torch.int32, device=c.dev)
+    c.dec = mp3_amd.BatchDecoder(c.n, c.F, device=c.gpu)
+
+    def step(k=0):
+        c.dec.decode(c.d_in, offs, sizes, c.F, pcm=c.pcm[k % len(c.pcm)], infos=c.infos, stream=c.strm)
+    c.step = step
+    c.in_bytes = int(sizes.astype(np.int64).sum())
+
+
+def setup_synth(c):
+    import torch
+    import _gen
+    import mp3_amd
+    from mp3_amd import shard
+    xr, bt, mx = _gen.c2_spectra(c.n, c.F, 2, seed=shard.shard_seed_base(c.rank, c.n, 1_000_003 * 2))
+    c.xr, c.bt, c.mx = xr, bt, mx
+    c.d_xr, c.d_bt, c.d_mx = (torch.from_numpy(a).to(c.dev) for a in (xr, bt, mx))
+    c.pcm = [torch.empty((c.n, c.F, 2304), dtype=torch.int16, device=c.dev) for _ in range(2 if c.gather else 1)]
+    c.dec = mp3_amd.BatchDecoder(c.n, c.F, device=c.gpu)
+
+    def step(k=0):
+        c.dec.synth_only(c.d_xr, c.d_bt, c.d_mx, 2, 44100, pcm=c.pcm[k % len(c.pcm)], stream=c.strm)
+    c.step = step
+
+
+def run_per_frame(args):
+    """configs[0]: one stream through the per-frame drop-in call."""
+    import _golden
+    import mp3_amd
+    data, _ = _golden.case("keypress_128k_js")
+    L = mp3_amd.lib()
+    d = mp3_amd.Decoder(device=0)
+    pcm = np.zeros(2304, np.int16)
+    info = mp3_amd.FrameInfo()
+
+    def one_pass():
+        d.reset()
+        pos, nf, lat = 0, 0, []
+        while pos < len(data):
+            t = time.perf_counter()
+            n = L.mp3d_decode_frame(d._h, data[pos:], len(data) - pos, pcm.ctypes.data, ctypes.byref(info))
+            lat.append(time.perf_counter() - t)
+            if n < 0 or info.frame_bytes <= 0:
+                break
+            pos += info.frame_bytes
+            nf += n > 0
+        return nf, lat
+
+    for _ in range(args.warmup):
+        one_pass()
+    t0 = time.perf_counter()
+    frames, lats = 0, []
+    for _ in range(args.steps):
+        nf, lat = one_pass()
+        frames += nf
+        lats += lat
+    dt = time.perf_counter() - t0
+    lat_us = np.array(lats) * 1e6
+    L32, _ = _oracle_libs()
+    out = np.zeros((2, 64 * 1152), np.float32)
+    nch, hz = ctypes.c_int(), ctypes.c_int()
+    t1, f1 = time.perf_counter(), 0
+    while time.perf_counter() - t1 < 2.0:
+        f1 += L32.orc_decode_stream(data, len(data), out.ctypes.data, 64, ctypes.byref(nch), ctypes.byref(hz))
+    cpu = {"value": f1 / (time.perf_counter() - t1), "unit": "frames/s", "cores": 1, "kind": "port",
+           "sample": "the same file decoded repeatedly for 2 s by oracle/liboracle_f32.so on one thread",
+           "cpu_model": cpu_model()}
+    return {"metric": METRIC, "value": frames / dt, "unit": "frames/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "tests/golden/keypress_128k_js.mp3",
+            "config": {"workload": "C1: one 128 kbps 44.1 kHz joint-stereo stream (21 audio frames + Info frame) "
+                                   "through mp3d_decode_frame, host buffers, one call per frame",
+                       "streams_per_gpu": 1, "parallelism": "none (per-frame player call)"},
+            "latency_us": {"median": float(np.median(lat_us)), "p99": float(np.percentile(lat_us, 99))},
+            "roofline": None, "cpu_baseline": cpu}
 
 
 def main():
@@ -108,160 +343,289 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--streams", type=int, default=65536, help="streams per GPU")
-    ap.add_argument("--frames", type=int, default=32, help="frames per stream per step")
+    ap.add_argument("--config", type=int, default=3, choices=(1, 2, 3, 4, 5),
+                    help="BASELINE.json configs[k-1]; 4 = 3 at --gpus 8 (65,536 streams per GPU)")
+    ap.add_argument("--streams", type=int, default=None, help="streams per GPU (default: the config's)")
+    ap.add_argument("--frames", type=int, default=None, help="frames per stream per step (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--gather", action="store_true", help="also time an RCCL PCM gather to rank 0 (reported apart)")
+    ap.add_argument("--gather", action="store_true",
+                    help="also time an RCCL PCM gather to rank 0 overlapped with the next step (reported apart)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse the "
-                         "multi-rank path with several ranks on one GPU)")
+                         "multi-rank path, e.g. several ranks on one GPU)")
+    ap.add_argument("--plumbing", action="store_true",
+                    help="no GPU: exercise the launcher, rendezvous, sharding, barriers, max-over-ranks timing and "
+                         "the gather on CPU tensors (gloo); value is null (tests/test_bench_launch.py)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    if args.config == 1:
+        if args.gpus != 1:
+            raise SystemExit("config 1 is a single-stream, single-GPU workload")
+        print(json.dumps(run_per_frame(args)), flush=True)
+        return
 
     import torch
     import torch.distributed as dist
-    import _gen
-    import mp3_amd
     from mp3_amd import shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one process per GPU; ranks beyond the visible GPUs (a gloo rehearsal on a
-    # one-GPU box) share them round-robin
-    gpu = local % max(1, torch.cuda.device_count())
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    c = Ctx()
+    c.rank, c.world, c.gather = rank, world, args.gather
+    backend = "gloo" if args.plumbing else args.dist_backend
+    if args.plumbing:
+        c.dev = torch.device("cpu")
+        c.gpu = None
+    else:
+        # one process per GPU; ranks beyond the visible GPUs (a gloo rehearsal
+        # on a one-GPU box) share them round-robin
+        c.gpu = local % max(1, torch.cuda.device_count())
+        c.dev = torch.device("cuda", c.gpu)
     if world > 1:
-        torch.cuda.set_device(gpu)
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        if backend == "nccl":
+            torch.cuda.set_device(c.gpu)
+            dist.init_process_group("nccl", device_id=c.dev)
         else:
-            dist.init_process_group(args.dist_backend)
-    dev = torch.device("cuda", gpu)
-    n, F = args.streams, args.frames
+            if c.gpu is not None:
+                torch.cuda.set_device(c.gpu)
+            dist.init_process_group(backend)
+    cfg = {2: "c2", 3: "c3", 4: "c3", 5: "c5"}[args.config]
+    c.n = args.streams or (1024 if cfg == "c2" else 65536)
+    c.F = args.frames or (64 if cfg == "c2" else 32)
+    if args.plumbing:
+        import _gen
+        c.n, c.F = min(c.n, 8), min(c.F, 4)
+        buf, offs, sizes = _gen.batch(_gen.C3, shard.shard_seed_base(rank, c.n), c.n, c.F, threads=1)
+        c.pcm = [torch.full((c.n, c.F, 2304), rank, dtype=torch.int16) for _ in range(2 if c.gather else 1)]
+        c.step = lambda k=0: None
+        sync = lambda: None  # noqa: E731
+    else:
+        c.strm = torch.cuda.current_stream(c.dev).cuda_stream
+        if cfg == "c2":
+            setup_synth(c)
+        else:
+            setup_decode(c, cfg)
+        sync = lambda: torch.cuda.synchronize(c.dev)  # noqa: E731
 
-    # --- synthetic C3 shard of this rank (seed by global stream id) -------
-    t0 = time.time()
-    gen_threads = min(16, os.cpu_count() or 1)
-    buf, offs, sizes = _gen.batch(_gen.C3, shard.shard_seed_base(rank, n), n, F, threads=gen_threads)
-    log("rank %d: generated %d streams x %d frames (%.1f MB) in %.1fs" % (rank, n, F, buf.size / 1e6, time.time() - t0))
-    d_in = torch.from_numpy(buf).to(dev)
-    pcm = torch.empty((n, F, 2304), dtype=torch.int16, device=dev)
-    infos = torch.zeros((n, F, 6), dtype=torch.int32, device=dev)
-    dec = mp3_amd.BatchDecoder(n, F, device=gpu)
-    strm = torch.cuda.current_stream(dev).cuda_stream
-
-    def step():
-        dec.decode(d_in, offs, sizes, F, pcm=pcm, infos=infos, stream=strm)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    ok = int((infos[..., 5] == 1152).sum().item())
-    if ok != n * F:
-        raise SystemExit("decode produced %d/%d frames" % (ok, n * F))
+    for k in range(args.warmup):
+        c.step(k)
+    sync()
+    frames_per_step = c.n * c.F
+    if cfg != "c2" and not args.plumbing:
+        inf = c.infos.cpu().numpy()
+        frames_per_step = int((inf[..., 5] > 0).sum())
+        if cfg == "c3" and frames_per_step != c.n * c.F:
+            raise SystemExit("decode produced %d/%d frames" % (frames_per_step, c.n * c.F))
 
     # --- timed region -------------------------------------------------------
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
+    for k in range(args.steps):
+        c.step(k)
+    sync()
     if world > 1:
         dist.barrier()
-    dt = shard.max_over_ranks(time.perf_counter() - t0, dev)
-    frames_total = n * F * world * args.steps
+    dt_rank = time.perf_counter() - t0
+    dt = shard.max_over_ranks(dt_rank, c.dev)
+    per_rank_dt = shard.all_ranks(dt_rank, c.dev)
+    per_rank_frames = shard.all_ranks(float(frames_per_step), c.dev)
+    frames_total = sum(per_rank_frames) * args.steps
     value = frames_total / dt
     ms_per_step = dt / args.steps * 1e3
 
     # --- per-kernel device time (HIP events on the decode stream) ---------
-    dec.set_timing(True)
     kt = {"demux": 0.0, "huffman": 0.0, "synth": 0.0}
-    reps = max(1, min(3, args.steps))
-    for _ in range(reps):
-        step()
-        for k, v in dec.kernel_times_us().items():
-            kt[k] += v / reps
-    dec.set_timing(False)
-    torch.cuda.synchronize(dev)
-    dom = max(kt, key=kt.get)
-    frames_per_launch = n * F
-    synth_s = kt["synth"] * 1e-6
-    flops = FLOP_PER_FRAME * frames_per_launch
-    achieved_tf = flops / synth_s / 1e12 if synth_s > 0 else 0.0
+    if not args.plumbing:
+        c.dec.set_timing(True)
+        reps = max(1, min(3, args.steps))
+        for k in range(reps):
+            c.step(k)
+            for key, v in c.dec.kernel_times_us().items():
+                kt[key] += v / reps
+        c.dec.set_timing(False)
+        sync()
 
-    traffic = mfma_util = None
-    prof = ROOT / "profiles" / "pmc_traffic.json"
-    if prof.exists():
-        try:
-            pj = json.loads(prof.read_text())
-            if pj.get("streams") == n and pj.get("frames") == F:
-                traffic = pj.get("k_synth_hbm_bytes_per_launch")
-                mfma_util = pj.get("k_synth_mfma_util")
-        except Exception:
-            traffic = mfma_util = None
-
+    # --- optional RCCL PCM gather, overlapped with the next step ----------
     gather = None
     if args.gather and world > 1:
-        # optional xGMI PCM gather to rank 0 (RCCL), timed apart from decode
-        dist.barrier()
-        torch.cuda.synchronize(dev)
-        tg = time.perf_counter()
-        shard.gather_to_root(pcm)
-        torch.cuda.synchronize(dev)
-        gather = {"ms": (time.perf_counter() - tg) * 1e3, "bytes": pcm.numel() * 2 * world}
+        gather = time_gather(c, args, dist, shard, torch, sync)
 
-    if rank == 0:
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(buf, offs, sizes, F)
-        step_s = dt / args.steps
-        res = {
-            "metric": "stereo MP3 frames/s (128 kbps 44.1 kHz) at 1/2/4/8 GPU; % HBM roofline",
-            "value": value,
-            "unit": "frames/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (seeded generator: valid CBR 128 kbps 44.1 kHz joint-stereo MP3 frames)",
-            "config": {"workload": "C3: full Layer III decode (Huffman->PCM), %d streams x %d frames per GPU per step"
-                                   % (n, F),
-                       "streams_per_gpu": n, "frames_per_stream": F, "bitrate_kbps": 128, "hz": 44100,
-                       "parallelism": "streams sharded, 1 process per GPU, no data-path collective"},
-            "roofline": {
-                "kernel": "k_synth", "bound": "mfma", "unit": "TFLOP/s",
-                "achieved": achieved_tf, "peak": FP32_PEAK_TFLOPS, "frac": achieved_tf / FP32_PEAK_TFLOPS,
-                "flop_per_frame": FLOP_PER_FRAME, "frames_per_launch": frames_per_launch,
-                "launch_us": kt["synth"],
-                "achieved_GBs_algorithmic": SYNTH_BYTES_PER_FRAME * frames_per_launch / synth_s / 1e9 if synth_s else 0,
-                "traffic": traffic,
-                "dct_tile": {
-                    "mfma_flop_per_frame": MFMA_FLOP_PER_FRAME,
-                    "mfma_tflops": MFMA_FLOP_PER_FRAME * frames_per_launch / synth_s / 1e12 if synth_s else 0,
-                    "mfma_util_pmc": mfma_util,
-                    "note": "matrix-core busy fraction of k_synth from rocprofv3 (SQ_VALU_MFMA_BUSY_CYCLES, "
-                            "profiles/pmc_traffic.json); peak 157.3 TFLOP/s FP32 MFMA",
-                },
-            },
-            "hbm": {
-                "hbm_rw_frac": value / world * (BYTES_IN_PER_FRAME + PCM_BYTES_PER_FRAME) / (HBM_PEAK_GBS * 1e9),
-                "hbm_read_frac": value / world * BYTES_IN_PER_FRAME / (HBM_PEAK_GBS * 1e9),
-                "bytes_per_frame_rw": BYTES_IN_PER_FRAME + PCM_BYTES_PER_FRAME,
-            },
-            "kernel_us": kt,
-            "dominant_kernel": "k_" + dom,
-            "cpu_baseline": cpu,
-        }
-        if gather:
-            res["gather"] = gather
-        print(json.dumps(res), flush=True)
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    res = {"metric": METRIC, "value": None if args.plumbing else value, "unit": "frames/s", "n_gpus": world,
+           "ranks": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+           "per_rank_frames_per_s": [f * args.steps / t for f, t in zip(per_rank_frames, per_rank_dt)],
+           "dist_backend": backend if world > 1 else None}
+    if args.plumbing:
+        res.update(plumbing_only=True, data="synthetic C3 shard per rank (generated, not decoded)",
+                   config={"workload": "plumbing rehearsal: %d ranks x %d streams x %d frames" % (world, c.n, c.F),
+                           "streams_per_gpu": c.n, "frames_per_stream": c.F,
+                           "first_stream_seed_per_rank": [shard.shard_seed_base(r, c.n) for r in range(world)]})
+    elif cfg == "c2":
+        res.update(report_c2(c, args, value, kt))
+    else:
+        res.update(report_decode(c, args, cfg, value, kt, frames_per_step))
+    if gather:
+        res["gather"] = gather
+    print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def time_gather(c, args, dist, shard, torch, sync):
+    """Second timed loop: step k's PCM gathered to rank 0 while step k+1
+    decodes (RCCL runs the gather on the process group's stream; the decode
+    of step k+2 waits for the gather that read its PCM buffer).  gloo gathers
+    host tensors synchronously, so that rehearsal shows no overlap."""
+    nbytes = c.pcm[0].numel() * c.pcm[0].element_size()
+    recv = None
+    if c.rank == 0 and dist.get_backend() != "gloo":
+        recv = [torch.empty_like(c.pcm[0]) for _ in range(c.world)]
+    # gather alone (no decode beside it)
+    dist.barrier()
+    sync()
+    tg = time.perf_counter()
+    shard.gather_to_root(c.pcm[0], out=recv)
+    sync()
+    alone = shard.max_over_ranks(time.perf_counter() - tg, c.dev)
+    pending = [None, None]
+    dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        b = k % 2
+        if pending[b] is not None:
+            pending[b].wait()  # decode k overwrites the buffer gather k-2 reads
+            pending[b] = None
+        c.step(k)
+        if dist.get_backend() == "gloo":
+            sync()
+            shard.gather_to_root(c.pcm[b])
+        else:
+            _, pending[b] = shard.gather_to_root(c.pcm[b], async_op=True, out=recv)
+    for w in pending:
+        if w is not None:
+            w.wait()
+    sync()
+    dist.barrier()
+    dt = shard.max_over_ranks(time.perf_counter() - t0, c.dev)
+    return {"ms_alone": alone * 1e3, "bytes_per_step": nbytes * c.world,
+            "ms_per_step_decode_plus_gather": dt / args.steps * 1e3,
+            "frames_per_s_with_gather": c.n * c.F * c.world * args.steps / dt,
+            "overlapped": dist.get_backend() != "gloo",
+            "note": "PCM of step k gathered to rank 0 over RCCL (xGMI) on the process group's stream while step "
+                    "k+1 decodes; reported apart from `value`"}
+
+
+def load_pmc(key, n, F):
+    prof = ROOT / "profiles" / "pmc_traffic.json"
+    if not prof.exists():
+        return {}
+    try:
+        pj = json.loads(prof.read_text())
+    except ValueError:
+        return {}
+    ent = pj.get(key, pj if key == "c3" else {})
+    if ent.get("streams") == n and ent.get("frames") == F:
+        return ent
+    return {}
+
+
+def report_decode(c, args, cfg, value, kt, frames_per_step):
+    n, F, world = c.n, c.F, c.world
+    synth_s = kt["synth"] * 1e-6
+    frames_per_launch = n * F
+    achieved_tf = FLOP_PER_FRAME * frames_per_launch / synth_s / 1e12 if synth_s > 0 else 0.0
+    pmc = load_pmc(cfg, n, F)
+    in_per_frame = c.in_bytes / max(1, frames_per_step)
+    if cfg == "c3":
+        if world == 8 and n == 65536:
+            wl = "C4: 524,288 concurrent streams sharded across 8 GPUs (65,536 x 32 frames per GPU per step)"
+        else:
+            wl = "C3: full Layer III decode (Huffman->PCM), %d streams x %d frames per GPU per step" % (n, F)
+        data = "synthetic (seeded generator: valid CBR 128 kbps 44.1 kHz joint-stereo MP3 frames)"
+    else:
+        wl = "C5: mixed corpus (VBR 32-320 kbps, mono/stereo/MS/IS, 32/44.1/48 kHz, short+mixed blocks, CRC), " \
+             "%d streams x %d frames per GPU per step" % (n, F)
+        data = "synthetic (seeded generator: mixed-corpus MP3 streams)"
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline_decode(c.buf, c.offs, c.sizes, F)
+    dom = max(kt, key=kt.get)
+    return {
+        "data": data,
+        "config": {"workload": wl, "streams_per_gpu": n, "frames_per_stream": F, "bitrate_kbps": 128 if cfg == "c3"
+                   else "32-320 VBR", "hz": 44100 if cfg == "c3" else "32000/44100/48000",
+                   "parallelism": "streams sharded, 1 process per GPU, no data-path collective"},
+        "roofline": {
+            "kernel": "k_synth", "bound": "mfma", "unit": "TFLOP/s",
+            "achieved": achieved_tf, "peak": FP32_PEAK_TFLOPS, "frac": achieved_tf / FP32_PEAK_TFLOPS,
+            "traffic": pmc.get("k_synth_hbm_bytes_per_launch"),
+            "limiter": "FP32 compute roofline (vector rate = matrix rate, 157.3 TF); the PMC counters "
+                       "(profiles/) show k_synth limited by VALU issue and dependent-chain latency, not by the "
+                       "matrix cores (see mfma_util_pmc)",
+            "flop_per_frame": FLOP_PER_FRAME, "frames_per_launch": frames_per_launch, "launch_us": kt["synth"],
+            "executed_flop_per_frame": EXEC_FLOP_PER_FRAME,
+            "executed_frac": EXEC_FLOP_PER_FRAME * frames_per_launch / synth_s / 1e12 / FP32_PEAK_TFLOPS
+            if synth_s else 0,
+            "dct_tile": {
+                "mfma_flop_per_frame": MFMA_FLOP_PER_FRAME,
+                "mfma_tflops": MFMA_FLOP_PER_FRAME * frames_per_launch / synth_s / 1e12 if synth_s else 0,
+                "mfma_util_pmc": pmc.get("k_synth_mfma_util"),
+                "note": "matrix-core busy fraction of k_synth from rocprofv3 (SQ_VALU_MFMA_BUSY_CYCLES, "
+                        "profiles/pmc_traffic.json); peak 157.3 TFLOP/s FP32 MFMA"},
+        },
+        "hbm": {
+            "hbm_rw_frac": value / world * (in_per_frame + PCM_BYTES_PER_FRAME) / (HBM_PEAK_GBS * 1e9),
+            "hbm_read_frac": value / world * in_per_frame / (HBM_PEAK_GBS * 1e9),
+            "bytes_per_frame_rw": in_per_frame + PCM_BYTES_PER_FRAME,
+            "step_traffic_pmc": pmc.get("step_hbm_bytes"),
+        },
+        "kernel_us": kt,
+        "dominant_kernel": "k_" + dom,
+        "cpu_baseline": cpu,
+    }
+
+
+def report_c2(c, args, value, kt):
+    n, F, world = c.n, c.F, c.world
+    synth_s = kt["synth"] * 1e-6
+    fpl = n * F
+    achieved_tf = C2_FLOP_PER_FRAME * fpl / synth_s / 1e12 if synth_s > 0 else 0.0
+    gbs = C2_BYTES_PER_FRAME * fpl / synth_s / 1e9 if synth_s > 0 else 0.0
+    pmc = load_pmc("c2", n, F)
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline_synth(c.xr, c.bt, c.mx, 2)
+    return {
+        "data": "synthetic spectra (SURVEY.md §8(d) C2: N(0, sigma_k^2) with spectral tilt, start/short/stop runs, "
+                "mixed blocks)",
+        "config": {"workload": "C2: IMDCT + polyphase synthesis only (mp3d_batch_synth_only), %d streams x %d "
+                               "frames per GPU per step" % (n, F),
+                   "streams_per_gpu": n, "frames_per_stream": F, "hz": 44100,
+                   "parallelism": "streams sharded, 1 process per GPU, no data-path collective"},
+        "roofline": {
+            "kernel": "k_synth<xr>", "bound": "mfma", "unit": "TFLOP/s", "achieved": achieved_tf,
+            "peak": FP32_PEAK_TFLOPS, "frac": achieved_tf / FP32_PEAK_TFLOPS,
+            "traffic": pmc.get("k_synth_hbm_bytes_per_launch"),
+            "flop_per_frame": C2_FLOP_PER_FRAME, "frames_per_launch": fpl, "launch_us": kt["synth"],
+            "hbm_GBs_algorithmic": gbs, "hbm_frac": gbs / HBM_PEAK_GBS,
+            "bytes_per_frame": C2_BYTES_PER_FRAME,
+            "limiter": "22 FLOP/B against a machine balance of 19.7: both rooflines are reported"},
+        "kernel_us": kt,
+        "dominant_kernel": "k_synth",
+        "cpu_baseline": cpu,
+    }
 
 
 if __name__ == "__main__":

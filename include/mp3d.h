@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MP3D_ABI_VERSION 3
+#define MP3D_ABI_VERSION 4
 
 #if defined(__GNUC__) || defined(__clang__)
 #define MP3D_API __attribute__((visibility("default")))
@@ -84,6 +84,15 @@ MP3D_API int mp3d_decode_frame(mp3d_dec *dec, const uint8_t *buf, size_t bytes, 
  * not clipped; the int16 output is clamp(rint(x * 32768)) of these values) */
 MP3D_API int mp3d_decode_frame_f32(mp3d_dec *dec, const uint8_t *buf, size_t bytes, float *pcm /* <= 2304 */,
                           mp3d_frame_info *info);
+/* (ABI v4) either of the above by flags: MP3D_FRAME_F32 selects float32 PCM;
+ * MP3D_FRAME_LAST says buf holds the rest of the stream, so a final frame cut
+ * short (header and side info present) is decoded with its missing bytes as
+ * zeros -- as the batch path and FFmpeg do -- instead of MP3D_E_NEED_MORE;
+ * info->frame_bytes then counts the bytes that were present.              */
+#define MP3D_FRAME_F32 1
+#define MP3D_FRAME_LAST 2
+MP3D_API int mp3d_decode_frame_ex(mp3d_dec *dec, const uint8_t *buf, size_t bytes, void *pcm, int flags,
+                                  mp3d_frame_info *info);
 
 /* ---- batched decoder (many concurrent streams on one GPU) -------------- *
  * A batch handle keeps per-stream decoder state resident in HBM across
@@ -178,8 +187,8 @@ MP3D_API int mp3d_dec_stream_info(mp3d_dec *dec, mp3d_stream_info *out);
  * infos   [max_frames] or NULL, host or device.
  * n_frames   out: frame slots found (MP3D_E_CAPACITY if > max_frames).
  * sinfo   stream info (Xing/Info tag, gapless trim) or NULL.
- * Synchronous; the batch's per-stream state is clobbered (reset it before
- * using the handle for ordinary batch calls).                              */
+ * Synchronous.  The segments decode on scratch state: the handle's own
+ * per-stream state (for mp3d_batch_decode) is left untouched.              */
 MP3D_API int mp3d_batch_decode_long(mp3d_batch *b, const uint8_t *data, size_t bytes, int L, void *pcm, int f32,
                                     long long max_frames, mp3d_frame_info *infos, long long *n_frames,
                                     mp3d_stream_info *sinfo);
@@ -192,6 +201,22 @@ MP3D_API int mp3d_batch_decode_long(mp3d_batch *b, const uint8_t *data, size_t b
  * segments of one stream over several GPUs with it.                        */
 MP3D_API int mp3d_long_plan(const uint8_t *data, size_t bytes, int L, long long max_frames, uint64_t *frame_off,
                             long long *seg_start, long long *n_frames, int *max_warmup);
+
+/* ---- per-stream state save / restore (ABI v4) --------------------------- *
+ * A stream's decoder state -- bit-reservoir carry, IMDCT overlap, synthesis
+ * history, MPEG family, Xing/LAME tag, frame count -- is an opaque blob of
+ * mp3d_state_bytes() bytes, valid for handles of the same ABI version.
+ * batch_get_state copies the state of streams [first, first + n) out of the
+ * handle into buf; batch_set_state writes it into those slots (of this or
+ * another handle).  A player seeks by saving the state at a frame boundary
+ * and restoring it before decoding from that frame's bytes again; a server
+ * moves a stream between batches or GPUs the same way.  buf: host or device
+ * memory.  Both order after the handle's last call and return when done.  */
+MP3D_API size_t mp3d_state_bytes(void);
+MP3D_API int mp3d_batch_get_state(mp3d_batch *b, int first, int n, void *buf);
+MP3D_API int mp3d_batch_set_state(mp3d_batch *b, int first, int n, const void *buf);
+MP3D_API int mp3d_dec_get_state(mp3d_dec *dec, void *buf);
+MP3D_API int mp3d_dec_set_state(mp3d_dec *dec, const void *buf);
 
 /* ---- diagnostics -------------------------------------------------------- */
 MP3D_API const char *mp3d_strerror(int err);

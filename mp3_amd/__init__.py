@@ -47,9 +47,12 @@ EXPORTS = ["mp3d_dec_create", "mp3d_dec_create_on", "mp3d_dec_destroy", "mp3d_de
            "mp3d_batch_huffman_only", "mp3d_batch_synth_only", "mp3d_strerror", "mp3d_last_hip_error",
            "mp3d_abi_version", "mp3d_batch_set_timing", "mp3d_batch_kernel_times", "mp3d_batch_stream_info",
            "mp3d_dec_stream_info", "mp3d_batch_decode_long",
-           "mp3d_long_plan", "mp3d_batch_set_options", "mp3d_dec_set_options"]
+           "mp3d_long_plan", "mp3d_batch_set_options", "mp3d_dec_set_options", "mp3d_decode_frame_ex",
+           "mp3d_state_bytes", "mp3d_batch_get_state", "mp3d_batch_set_state", "mp3d_dec_get_state",
+           "mp3d_dec_set_state"]
 
 OPT_CRC_CHECK = 1  # MP3D_OPT_CRC_CHECK: drop frames whose CRC-16 mismatches
+FRAME_F32, FRAME_LAST = 1, 2  # mp3d_decode_frame_ex flags
 
 _lib = None
 
@@ -95,6 +98,12 @@ def lib():
                                      ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_int)]
         L.mp3d_batch_set_options.argtypes = [vp, i]
         L.mp3d_dec_set_options.argtypes = [vp, i]
+        L.mp3d_decode_frame_ex.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t, vp, i, ctypes.POINTER(FrameInfo)]
+        L.mp3d_state_bytes.restype = ctypes.c_size_t
+        L.mp3d_batch_get_state.argtypes = [vp, i, i, vp]
+        L.mp3d_batch_set_state.argtypes = [vp, i, i, vp]
+        L.mp3d_dec_get_state.argtypes = [vp, vp]
+        L.mp3d_dec_set_state.argtypes = [vp, vp]
         _lib = L
     return _lib
 
@@ -150,15 +159,29 @@ class Decoder:
         """MP3D_OPT_* flags (OPT_CRC_CHECK) for later decode calls."""
         _check(lib().mp3d_dec_set_options(self._h, int(flags)))
 
-    def decode_frame(self, buf, f32=False):
+    def decode_frame(self, buf, f32=False, last=False):
         """Returns (samples_per_channel, pcm [samples*channels], FrameInfo);
-        pcm is int16, or float32 (full scale 1.0, unclipped) with f32=True."""
+        pcm is int16, or float32 (full scale 1.0, unclipped) with f32=True.
+        last=True: buf holds the rest of the stream, so a final frame cut
+        short decodes with its missing bytes as zeros (MP3D_FRAME_LAST)."""
         pcm = np.zeros(2304, np.float32 if f32 else np.int16)
         info = FrameInfo()
         buf = bytes(buf)
-        fn = lib().mp3d_decode_frame_f32 if f32 else lib().mp3d_decode_frame
-        n = _check(fn(self._h, buf, len(buf), pcm.ctypes.data, ctypes.byref(info)))
+        flags = (FRAME_F32 if f32 else 0) | (FRAME_LAST if last else 0)
+        n = _check(lib().mp3d_decode_frame_ex(self._h, buf, len(buf), pcm.ctypes.data, flags, ctypes.byref(info)))
         return n, pcm[: n * max(info.channels, 1)], info
+
+    def get_state(self):
+        """Opaque decoder state (np.uint8 [state_bytes()]) for set_state."""
+        buf = np.zeros(state_bytes(), np.uint8)
+        _check(lib().mp3d_dec_get_state(self._h, buf.ctypes.data))
+        return buf
+
+    def set_state(self, buf):
+        buf = np.ascontiguousarray(buf, np.uint8)
+        if buf.size != state_bytes():
+            raise ValueError("state blob of %d bytes, expected %d" % (buf.size, state_bytes()))
+        _check(lib().mp3d_dec_set_state(self._h, buf.ctypes.data))
 
     def stream_info(self):
         """StreamInfo of the stream decoded so far (Xing/Info tag, gapless)."""
@@ -176,7 +199,7 @@ class Decoder:
         pos, out, nch = 0, [], 0
         while pos < len(data):
             try:
-                n, pcm, info = self.decode_frame(data[pos:], f32=f32)
+                n, pcm, info = self.decode_frame(data[pos:], f32=f32, last=True)
             except MP3DError:
                 break
             if info.frame_bytes <= 0:
@@ -251,6 +274,26 @@ class BatchDecoder:
         _check(fn(self._h, fp, off.ctypes.data, sz.ctypes.data, n, F, pp, ip, ctypes.c_void_p(stream) if stream else None))
         return pcm, infos
 
+    def get_state(self, first=0, n=None, out=None):
+        """State blobs of streams [first, first + n): np.uint8 [n, state_bytes()]
+        (or into `out`, a host array or device tensor of that size)."""
+        n = self.max_streams - first if n is None else int(n)
+        if out is None:
+            out = np.zeros((n, state_bytes()), np.uint8)
+        op, k = _ptr(out)
+        _check(lib().mp3d_batch_get_state(self._h, int(first), n, op))
+        return out
+
+    def set_state(self, buf, first=0):
+        """Restore state blobs [n, state_bytes()] into streams [first, first + n)."""
+        n = (buf.numel() if hasattr(buf, "numel") else np.asarray(buf).size) // state_bytes()
+        if hasattr(buf, "numel"):
+            bp, k = _ptr(buf)
+        else:
+            buf = np.ascontiguousarray(buf, np.uint8)
+            bp, k = buf.ctypes.data, buf
+        _check(lib().mp3d_batch_set_state(self._h, int(first), int(n), bp))
+
     def stream_info(self, n_streams):
         """[StreamInfo] of the first n_streams streams (after a decode call)."""
         arr = (StreamInfo * int(n_streams))()
@@ -266,7 +309,15 @@ class BatchDecoder:
         Returns (pcm[:n], infos[:n], StreamInfo)."""
         nbytes = data.numel() if hasattr(data, "numel") else len(data)
         if max_frames is None:
-            max_frames = max_frame_slots(nbytes)
+            if pcm is not None or infos is not None:
+                max_frames = min(len(x) for x in (pcm, infos) if x is not None)
+            else:  # exact: the host frame walk of the plan
+                host = data.cpu().numpy().tobytes() if hasattr(data, "cpu") else bytes(data)
+                max_frames = len(long_plan(host, segment_frames, max_frame_slots(nbytes))[0])
+        for x in (pcm, infos):
+            if x is not None and len(x) < max_frames:
+                raise ValueError("pcm / infos hold %d rows < max_frames %d" % (len(x), max_frames))
+        max_frames = max(1, int(max_frames))
         if pcm is None:
             pcm = np.zeros((max_frames, 2304), np.float32 if f32 else np.int16)
         if infos is None:
@@ -304,10 +355,15 @@ class BatchDecoder:
         return pcm
 
 
+def state_bytes():
+    """Bytes of one stream's opaque decoder state (mp3d_state_bytes)."""
+    return int(lib().mp3d_state_bytes())
+
+
 def max_frame_slots(nbytes):
-    """Upper bound on the frame slots in nbytes of stream (the smallest
-    Layer III frame is 96 B: 32 kbps at 48 kHz)."""
-    return int(nbytes) // 96 + 2
+    """Upper bound on the frame slots in nbytes of stream: the smallest
+    Layer III frame is 24 B (MPEG-2 LSF, 8 kbps at 24 kHz; MPEG-1: 96 B)."""
+    return int(nbytes) // 24 + 2
 
 
 def long_plan(data, segment_frames=32, max_frames=None):

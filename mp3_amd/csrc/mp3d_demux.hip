@@ -55,29 +55,38 @@ __device__ __forceinline__ uint32_t side_unit_bit(int nch, int gr, int ch, bool 
 /* serial header walk costs about one load latency per frame.              */
 /* ------------------------------------------------------------------------ */
 struct HdrWin {        /* 64 bytes at a stream position, spread over lanes 0..15 */
-    uint32_t le;       /* lane i: little-endian dword at (pos & ~3) + 4 i        */
+    uint32_t le;       /* lane i: little-endian dword at stream offset pos - mis + 4 i */
     uint32_t pos;
+    uint32_t mis;      /* (address of stream byte pos) & 3: the dwords are aligned  */
 };
 
+/* Every load is an ALIGNED dword that holds at least one byte of the stream
+ * [0, len), so it never leaves the pages of the caller's buffer, however the
+ * stream is placed; bytes outside the stream read as zero. */
 __device__ __forceinline__ HdrWin load_win(const uint8_t *p0, uint32_t len, uint32_t pos, int lane) {
     HdrWin w;
     w.pos = pos;
-    const uint32_t a = (pos & ~3u) + 4u * (uint32_t)lane;
-    /* a dword is read only if it starts inside the stream: it then cannot
-     * leave the caller's allocation */
-    w.le = (lane < 16 && a < len) ? *(const uint32_t *)(p0 + a) : 0u;
+    w.mis = (uint32_t)((uintptr_t)(p0 + pos) & 3u);
+    const int64_t a = (int64_t)pos - (int64_t)w.mis + 4 * lane; /* stream offset of the lane's dword */
+    uint32_t v = 0u;
+    if (lane < 16 && a < (int64_t)len) {
+        v = *(const uint32_t *)(p0 + a);
+        const int64_t over = a + 4 - (int64_t)len; /* bytes past the stream end */
+        if (over > 0) v &= 0xFFFFFFFFu >> (8 * over);
+    }
+    w.le = v;
     return w;
 }
 
-/* byte k of the window (uniform k; k + (pos & 3) < 64) */
+/* byte k of the window (uniform k; k + mis < 64) */
 __device__ __forceinline__ uint32_t win_byte(const HdrWin &w, uint32_t k) {
-    const uint32_t i = k + (w.pos & 3u);
+    const uint32_t i = k + w.mis;
     const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)w.le, (int)(i >> 2));
     return (d >> (8 * (i & 3u))) & 0xFFu;
 }
 
-/* 64 bits of the window's big-endian bit string starting at bit b of byte
- * position (w.pos & ~3) -- per lane b (lane-varying) */
+/* 64 bits of the window's big-endian bit string starting at bit b of the
+ * window's first dword (stream byte pos - mis) -- per lane b (lane-varying) */
 __device__ __forceinline__ uint64_t win_bits64(const HdrWin &w, uint32_t b) {
     const uint32_t be = __builtin_bswap32(w.le);
     const int wi = (int)(b >> 5);
@@ -104,7 +113,7 @@ __device__ bool crc16_ok(const HdrWin &w, uint32_t side_bytes, int lane) {
     uint32_t term = 0u;
     /* message byte i sits at frame byte 2 + i (header) or 4 + i (side info);
      * the cross-lane read runs in every lane (all source lanes active) */
-    const uint32_t k = (uint32_t)(lane < 34 ? lane : 33) + (lane < 2 ? 2u : 4u) + (w.pos & 3u);
+    const uint32_t k = (uint32_t)(lane < 34 ? lane : 33) + (lane < 2 ? 2u : 4u) + w.mis;
     const uint32_t d = (uint32_t)__shfl((int)w.le, (int)(k >> 2));
     if ((uint32_t)lane < n) {
         uint32_t c = ((d >> (8u * (k & 3u))) & 0xFFu) << 8;
@@ -231,7 +240,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                 inf.frame_bytes = fb; inf.channels = nch; inf.hz = (int)MP3D_SAMPLE_RATE[r.sr_idx];
                 inf.layer = 3; inf.bitrate_kbps = lsf ? MP3D_BITRATE_L3_LSF[h2 >> 4] : MP3D_BITRATE_L3[h2 >> 4];
                 /* side info: bit offsets relative to the window's dword base */
-                const uint32_t sbit = 8u * ((cur & 3u) + 4u + (uint32_t)crc);
+                const uint32_t sbit = 8u * (w.mis + 4u + (uint32_t)crc);
                 const int mdb = (int)(win_bits64(w, sbit) >> (lsf ? 56 : 55));
                 const int q = lane & 3, qgr = q >> 1, qch = q & 1;
                 const uint32_t ub = sbit + side_unit_bit(nch, qgr, qch, lsf);
@@ -361,7 +370,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                  * load under a branch the compiler's waitcnt pass loses track
                  * at the join and drains vmcnt before every store.  The high
                  * word is read only for a misaligned source (index select, not
-                 * a branch): it then still holds payload bytes. */
+                 * a branch): it then still holds payload bytes.  Both words
+                 * are aligned dwords holding at least one payload byte, so no
+                 * load leaves the pages of the caller's buffer. */
                 const uint32_t nwd = we - wb;
                 uint32_t v[6];
 #pragma unroll

@@ -295,8 +295,8 @@ struct mp3d_batch {
     int last_n = -1;
     bool timing = false;
     int opts = 0; /* MP3D_OPT_* */
+    hipStream_t last = nullptr; /* stream of the last call (caller's or own) */
     hipEvent_t ev[4] = {};
-    float times[4] = {0, 0, 0, 0};
 };
 
 static bool is_device_ptr(const void *p) {
@@ -370,8 +370,8 @@ extern "C" void mp3d_batch_destroy(mp3d_batch *b) {
                     b->d_infos, b->md, b->d_in, b->d_pcm, b->d_xr, b->d_bt, b->d_mx};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
-    for (int i = 0; i < 5; i++)
-        if (b->ev[i]) (void)hipEventDestroy(b->ev[i]);
+    for (hipEvent_t e : b->ev)
+        if (e) (void)hipEventDestroy(e);
     if (b->own) (void)hipStreamDestroy(b->own);
     delete b;
 }
@@ -390,11 +390,13 @@ extern "C" int mp3d_batch_set_options(mp3d_batch *b, int flags) {
     return MP3D_OK;
 }
 
+/* waits for this handle's work only: its own stream and the stream of its
+ * last call (a caller's hip_stream), never the whole device */
 extern "C" int mp3d_batch_sync(mp3d_batch *b) {
     if (!b) return MP3D_E_ARG;
     HIPCHK(hipSetDevice(b->device));
     HIPCHK(hipStreamSynchronize(b->own));
-    HIPCHK(hipDeviceSynchronize());
+    if (b->last && b->last != b->own) HIPCHK(hipStreamSynchronize(b->last));
     return MP3D_OK;
 }
 
@@ -448,6 +450,7 @@ static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offse
     if (!b || !frames || !offsets || !sizes || n <= 0 || F <= 0) return MP3D_E_ARG;
     if (n > b->max_streams || F > b->max_frames) return MP3D_E_CAPACITY;
     HIPCHK(hipSetDevice(b->device));
+    b->last = s;
     uint64_t total = 0;
     for (int i = 0; i < n; i++) total = std::max<uint64_t>(total, offsets[i] + sizes[i]);
     const uint8_t *din = frames;
@@ -483,33 +486,61 @@ static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *of
     bool sync_needed = false;
     int r = run_front(b, frames, offsets, sizes, n, F, s, &sync_needed);
     if (r) return r;
-    size_t pcm_bytes = (size_t)n * F * 2304 * (f32 ? sizeof(float) : sizeof(int16_t));
+    const size_t PB = f32 ? sizeof(float) : sizeof(int16_t), row = 2304 * PB;
+    const size_t pcm_bytes = (size_t)n * F * row;
     void *dpcm = pcm;
     bool pcm_host = !is_device_ptr(pcm);
     if (pcm_host) {
         r = grow((void **)&b->d_pcm, &b->pcm_cap, pcm_bytes);
         if (r) return r;
         dpcm = b->d_pcm;
-        /* frames without audio leave the caller's PCM untouched (internal
-         * callers that read only the audio rows skip the copy) */
-        if (!overwrite) HIPCHK(hipMemcpyAsync(dpcm, pcm, pcm_bytes, hipMemcpyHostToDevice, s));
     }
     DeviceCtx &dc = g_dev[b->device];
     launch_synth(b->rec, b->is_buf, b->meta, dc.tables, b->st, dpcm, f32, n, F, kinds, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[3], s));
     HIPCHK(hipGetLastError());
-    if (pcm_host) {
+    const size_t ib = sizeof(mp3d_frame_info) * (size_t)n * F;
+    const bool inf_host = infos && !is_device_ptr(infos);
+    if (infos && !inf_host) HIPCHK(hipMemcpyAsync(infos, b->d_infos, ib, hipMemcpyDeviceToDevice, s));
+    if (pcm_host && !overwrite) {
+        /* A host sink is read back whole, but each row keeps the caller's
+         * bytes the kernel did not write (rows without audio, the second
+         * half of a mono / LSF row): those few spans are saved from the
+         * caller's buffer and put back after the copy -- no host-to-device
+         * copy of the whole PCM buffer first. */
+        std::vector<mp3d_frame_info> tmp;
+        mp3d_frame_info *hi = inf_host ? infos : nullptr;
+        if (!hi) {
+            tmp.resize((size_t)n * F);
+            hi = tmp.data();
+        }
+        HIPCHK(hipMemcpyAsync(hi, b->d_infos, ib, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        std::vector<size_t> at;
+        std::vector<uint8_t> kept;
+        for (size_t i = 0; i < (size_t)n * F; i++) {
+            const size_t w = (size_t)hi[i].samples * (size_t)hi[i].channels * PB;
+            if (w >= row) continue;
+            at.push_back(i);
+            kept.insert(kept.end(), (const uint8_t *)pcm + i * row + w, (const uint8_t *)pcm + (i + 1) * row);
+        }
+        HIPCHK(hipMemcpyAsync(pcm, dpcm, pcm_bytes, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        size_t k = 0;
+        for (size_t i : at) {
+            const size_t w = (size_t)hi[i].samples * (size_t)hi[i].channels * PB;
+            memcpy((uint8_t *)pcm + i * row + w, kept.data() + k, row - w);
+            k += row - w;
+        }
+        return MP3D_OK;
+    }
+    if (pcm_host) { /* internal callers that read only the rows with audio */
         HIPCHK(hipMemcpyAsync(pcm, dpcm, pcm_bytes, hipMemcpyDeviceToHost, s));
         sync_needed = true;
     }
-    if (infos) {
-        size_t ib = sizeof(mp3d_frame_info) * (size_t)n * F;
-        if (is_device_ptr(infos)) {
-            HIPCHK(hipMemcpyAsync(infos, b->d_infos, ib, hipMemcpyDeviceToDevice, s));
-        } else {
-            HIPCHK(hipMemcpyAsync(infos, b->d_infos, ib, hipMemcpyDeviceToHost, s));
-            sync_needed = true;
-        }
+    if (inf_host) {
+        HIPCHK(hipMemcpyAsync(infos, b->d_infos, ib, hipMemcpyDeviceToHost, s));
+        sync_needed = true;
     }
     if (sync_needed) HIPCHK(hipStreamSynchronize(s));
     return MP3D_OK;
@@ -564,6 +595,7 @@ extern "C" int mp3d_batch_synth_only(mp3d_batch *b, const float *xr, const uint8
     if (sr < 0) return MP3D_E_ARG;
     HIPCHK(hipSetDevice(b->device));
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : b->own;
+    b->last = s;
     bool sync_needed = false;
     size_t nx = (size_t)n * F * 2 * nch;
     const float *dxr = xr;
@@ -753,6 +785,9 @@ extern "C" int mp3d_batch_decode_long(mp3d_batch *b, const uint8_t *data, size_t
     const int chunk = b->max_streams;
     void *seg_pcm = nullptr, *out_pcm = nullptr;
     int *d_a = nullptr;
+    /* the virtual streams decode on a state array of their own: the handle's
+     * per-stream state (reservoir, overlap, FIFO, tag) is left as it was */
+    StreamState *const own_st = b->st, *seg_st = nullptr;
     std::vector<int> a32;
     mp3d_frame_info *out_inf = nullptr;
     int rc = MP3D_OK;
@@ -766,6 +801,8 @@ extern "C" int mp3d_batch_decode_long(mp3d_batch *b, const uint8_t *data, size_t
         }                                                                                                              \
     } while (0)
     LCHK(hipMalloc(&seg_pcm, (size_t)std::min<long long>(chunk, K) * F * row));
+    LCHK(hipMalloc(&seg_st, sizeof(StreamState) * (size_t)std::min<long long>(chunk, K)));
+    b->st = seg_st;
     LCHK(hipMalloc(&d_a, sizeof(int) * K));
     a32.assign(a.begin(), a.end());
     LCHK(hipMemcpyAsync(d_a, a32.data(), sizeof(int) * K, hipMemcpyHostToDevice, s));
@@ -801,6 +838,8 @@ extern "C" int mp3d_batch_decode_long(mp3d_batch *b, const uint8_t *data, size_t
 done:
 #undef LCHK
     (void)hipStreamSynchronize(s);
+    b->st = own_st;
+    if (seg_st) (void)hipFree(seg_st);
     if (seg_pcm) (void)hipFree(seg_pcm);
     if (d_a) (void)hipFree(d_a);
     if (!pcm_dev && out_pcm) (void)hipFree(out_pcm);
@@ -902,7 +941,8 @@ static int host_frame_head(const uint8_t *p) {
     return 4 + ((p[1] & 1) ? 0 : 2) + (lsf ? (mono ? 9 : 17) : (mono ? 17 : 32));
 }
 
-static int decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, void *pcm, bool f32, mp3d_frame_info *info) {
+static int decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, void *pcm, bool f32, bool last,
+                        mp3d_frame_info *info) {
     if (!d || !buf) return MP3D_E_ARG;
     mp3d_frame_info tmp;
     if (!info) info = &tmp;
@@ -919,14 +959,18 @@ static int decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, void *pcm
         if (fb > 0) break;
         pos++;
     }
-    if (fb <= 0 || pos + (size_t)fb > bytes) {
+    /* a final frame cut short (MP3D_FRAME_LAST): decoded once its header and
+     * side info are present, the missing bytes reading as zeros (k_demux) */
+    const bool cut = fb > 0 && pos + (size_t)fb > bytes;
+    if (fb <= 0 || (cut && !(last && pos + (size_t)host_frame_head(buf + pos) <= bytes))) {
         info->frame_bytes = (int)std::min<size_t>(pos, bytes);
         return info->frame_bytes ? 0 : MP3D_E_NEED_MORE;
     }
+    const size_t have = cut ? bytes - pos : (size_t)fb;
     uint64_t off = 0;
     uint32_t sz = MP3D_PF_BYTES;
-    memcpy(d->h_in, buf + pos, (size_t)fb); /* fb <= MP3D_MAX_FRAME_BYTES */
-    memset(d->h_in + fb, 0, MP3D_PF_BYTES - (size_t)fb);
+    memcpy(d->h_in, buf + pos, have); /* have <= fb <= MP3D_MAX_FRAME_BYTES */
+    memset(d->h_in + have, 0, MP3D_PF_BYTES - have);
     /* PCM straight into pinned memory: only the audio rows are read back */
     int r = batch_decode(d->b, d->h_in, &off, &sz, 1, 1, d->h_out, f32, d->h_info, nullptr, true,
                          host_frame_kind(buf + pos)); /* 1 MPEG-1, 2 LSF */
@@ -936,18 +980,66 @@ static int decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, void *pcm
     d->frames++;
     if (fi.frame_bytes) d->kind = host_frame_kind(buf + pos);
     *info = fi;
-    info->frame_bytes = (int)pos + fi.frame_bytes;
+    info->frame_bytes = (int)pos + (int)std::min<size_t>((size_t)fi.frame_bytes, have);
     if (fi.samples && pcm) memcpy(pcm, out, (f32 ? sizeof(float) : sizeof(int16_t)) * (size_t)fi.samples * fi.channels);
     return fi.samples;
 }
 
 extern "C" int mp3d_decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, int16_t *pcm, mp3d_frame_info *info) {
-    return decode_frame(d, buf, bytes, pcm, false, info);
+    return decode_frame(d, buf, bytes, pcm, false, false, info);
 }
 
 extern "C" int mp3d_decode_frame_f32(mp3d_dec *d, const uint8_t *buf, size_t bytes, float *pcm,
                                      mp3d_frame_info *info) {
-    return decode_frame(d, buf, bytes, pcm, true, info);
+    return decode_frame(d, buf, bytes, pcm, true, false, info);
+}
+
+extern "C" int mp3d_decode_frame_ex(mp3d_dec *d, const uint8_t *buf, size_t bytes, void *pcm, int flags,
+                                    mp3d_frame_info *info) {
+    if (flags & ~(MP3D_FRAME_F32 | MP3D_FRAME_LAST)) return MP3D_E_ARG;
+    return decode_frame(d, buf, bytes, pcm, (flags & MP3D_FRAME_F32) != 0, (flags & MP3D_FRAME_LAST) != 0, info);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Per-stream state save / restore                                          */
+/* ------------------------------------------------------------------------ */
+extern "C" size_t mp3d_state_bytes(void) { return sizeof(StreamState); }
+
+static int state_copy(mp3d_batch *b, int first, int n, void *dst, const void *src, bool out) {
+    if (!b || !(out ? dst : src) || first < 0 || n <= 0) return MP3D_E_ARG;
+    if ((long long)first + n > b->max_streams) return MP3D_E_CAPACITY;
+    HIPCHK(hipSetDevice(b->device));
+    hipStream_t s = b->last ? b->last : b->own;
+    StreamState *at = b->st + first;
+    HIPCHK(hipMemcpyAsync(out ? dst : (void *)at, out ? (const void *)at : src, sizeof(StreamState) * (size_t)n,
+                          hipMemcpyDefault, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return MP3D_OK;
+}
+
+extern "C" int mp3d_batch_get_state(mp3d_batch *b, int first, int n, void *buf) {
+    return state_copy(b, first, n, buf, nullptr, true);
+}
+
+extern "C" int mp3d_batch_set_state(mp3d_batch *b, int first, int n, const void *buf) {
+    return state_copy(b, first, n, nullptr, buf, false);
+}
+
+extern "C" int mp3d_dec_get_state(mp3d_dec *d, void *buf) {
+    if (!d) return MP3D_E_ARG;
+    return mp3d_batch_get_state(d->b, 0, 1, buf);
+}
+
+extern "C" int mp3d_dec_set_state(mp3d_dec *d, const void *buf) {
+    if (!d || !buf) return MP3D_E_ARG;
+    const int r = mp3d_batch_set_state(d->b, 0, 1, buf);
+    if (r) return r;
+    /* host mirror of the family lock and "past the stream start" (ID3v2 skip) */
+    StreamState h;
+    HIPCHK(hipMemcpy(&h, d->b->st, sizeof(h), hipMemcpyDeviceToHost));
+    d->kind = h.kind;
+    d->frames = (long)h.frames + (h.tag_info ? 1 : 0);
+    return MP3D_OK;
 }
 
 /* ------------------------------------------------------------------------ */

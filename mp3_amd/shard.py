@@ -35,18 +35,38 @@ def max_over_ranks(seconds: float, device=None) -> float:
     return float(t.item())
 
 
-def gather_to_root(t: torch.Tensor, root: int = 0):
+def all_ranks(value: float, device=None) -> list:
+    """Every rank's `value` (rank order), on every rank ([value] when not
+    distributed) -- bench.py's per-rank frames/s."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [value]
+    if dist.get_backend() == "gloo":
+        device = "cpu"
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(o.item()) for o in out]
+
+
+def gather_to_root(t: torch.Tensor, root: int = 0, async_op: bool = False, out=None):
     """Gather every rank's equally-shaped tensor to `root` (list there, None
     elsewhere).  gloo has no 8/16-bit gather, so such tensors travel as int32
-    words there (PCM rows are 2304 int16 = 1152 words)."""
+    words there (PCM rows are 2304 int16 = 1152 words).  async_op=True
+    (RCCL): returns (list or None, work handle); the gather runs on the
+    process group's own stream after the work queued so far on the current
+    stream, and work.wait() makes the current stream wait for it.  out:
+    preallocated receive list on root (reused across steps), else allocated."""
     world, rank = dist.get_world_size(), dist.get_rank()
     src = t.contiguous()
     if dist.get_backend() == "gloo":
         src = src.cpu()  # gloo gathers host tensors
         if src.dtype in (torch.int16, torch.uint8, torch.int8):
             src = src.view(torch.int32)
-    out = [torch.empty_like(src) for _ in range(world)] if rank == root else None
-    dist.gather(src, out, dst=root)
+    if rank != root:
+        out = None
+    elif out is None or dist.get_backend() == "gloo":
+        out = [torch.empty_like(src) for _ in range(world)]
+    work = dist.gather(src, out, dst=root, async_op=async_op)
     if out is not None:
         out = [o.view(t.dtype) for o in out]
-    return out
+    return (out, work) if async_op else out

@@ -14,8 +14,11 @@
  * (SURVEY.md Appendix A.9).  Parity is pinned by committed golden PCM from
  * that oracle (tests/golden/), not by reference tests (none exist).
  *
- * Arithmetic is double precision throughout, so this file is an
- * independent high-precision restatement, not a bit-copy of the GPU path.
+ * Arithmetic is double precision throughout (orc_real = double), so this
+ * file is an independent high-precision restatement, not a bit-copy of the
+ * GPU path.  Built with -DORC_REAL=float (liboracle_f32.so, -O3) the same
+ * source is the single-precision CPU decoder that bench.py times as the CPU
+ * baseline; the tests check only the double build.
  */
 #include <math.h>
 #include <stdint.h>
@@ -25,6 +28,11 @@
 #include "../mp3_amd/csrc/mp3d_tables.h"
 
 #define ORC_API __attribute__((visibility("default")))
+
+#ifndef ORC_REAL
+#define ORC_REAL double
+#endif
+typedef ORC_REAL orc_real;
 
 /* ------------------------------------------------------------------------ */
 /* Header, ISO 2.4.1.3 / 2.4.2.3                                             */
@@ -148,8 +156,8 @@ typedef struct {
 } orc_tree;
 static orc_tree g_trees[MP3D_NUM_HTABS + 1]; /* last = count1 table A */
 static int g_trees_ready = 0;
-static double g_pow43[8207 + 16];
-static double g_imdct36[18][36], g_imdct12[6][12], g_win[4][36], g_synthN[64][32], g_D[512];
+static orc_real g_pow43[8207 + 16];
+static orc_real g_imdct36[18][36], g_imdct12[6][12], g_win[4][36], g_synthN[64][32], g_D[512];
 
 static void orc_tree_add(orc_tree *t, unsigned code, int len, int value) {
     int node = 0;
@@ -224,13 +232,13 @@ typedef struct {
     uint8_t hist[ORC_HIST]; /* main-data byte history (previous payloads) */
     int hist_len;           /* bytes in hist                              */
     int avail;              /* bytes after the previous main-data end     */
-    double overlap[2][32][18];
-    double V[2][1024];
+    orc_real overlap[2][32][18];
+    orc_real V[2][1024];
     /* taps of the last decoded frame (parity taps) */
     int16_t is[2][2][576];
     uint8_t sf[2][2][40];
     int32_t used_bits[2][2]; /* bits actually consumed by part2+part3 */
-    double xr[2][2][576]; /* after stereo, before reorder (config-2 input) */
+    orc_real xr[2][2][576]; /* after stereo, before reorder (config-2 input) */
     orc_side side;
     orc_hdr hdr;
     int frames;
@@ -408,7 +416,7 @@ static long orc_huffman(orc_bits *b, const orc_gr *g, int sr_idx, long end_bit, 
 
 /* Requantise, ISO 2.4.3.4: xr = sgn(is)|is|^(4/3) 2^(q/4) with quarter
  * exponent q per line (FFmpeg exponents_from_scale_factors layout). */
-static void orc_requant(const orc_gr *g, int sr_idx, const uint8_t *sf, const int16_t *is, double *xr,
+static void orc_requant(const orc_gr *g, int sr_idx, const uint8_t *sf, const int16_t *is, orc_real *xr,
                         int gain_adj) {
     int gain = g->global_gain - 210 + gain_adj;
     int shift = g->scalefac_scale + 1;
@@ -424,7 +432,7 @@ static void orc_requant(const orc_gr *g, int sr_idx, const uint8_t *sf, const in
     for (int i = 0; i < long_end; i++) {
         int pre = g->preflag ? MP3D_PRETAB[i] : 0;
         int q = gain - ((sf[j++] + pre) << shift);
-        double s = pow(2.0, 0.25 * q);
+        orc_real s = pow(2.0, 0.25 * q);
         for (int n = 0; n < MP3D_SFB_LONG_WIDTH[sr_idx][i]; n++, line++) {
             int v = is[line];
             xr[line] = v == 0 ? 0.0 : (v < 0 ? -g_pow43[-v] : g_pow43[v]) * s;
@@ -434,7 +442,7 @@ static void orc_requant(const orc_gr *g, int sr_idx, const uint8_t *sf, const in
     for (int i = short_start; i < 13 && long_end < 22; i++) {
         for (int w = 0; w < 3; w++) {
             int q = gain - (g->subblock_gain[w] << 3) - (sf[j++] << shift);
-            double s = pow(2.0, 0.25 * q);
+            orc_real s = pow(2.0, 0.25 * q);
             for (int n = 0; n < MP3D_SFB_SHORT_WIDTH[sr_idx][i]; n++, line++) {
                 int v = is[line];
                 xr[line] = v == 0 ? 0.0 : (v < 0 ? -g_pow43[-v] : g_pow43[v]) * s;
@@ -449,7 +457,7 @@ static void orc_requant(const orc_gr *g, int sr_idx, const uint8_t *sf, const in
  * LSF (13818-3 2.4.3.2, FFmpeg is_table_lsf) i0 = 2^(-1/4) (scalefac_compress
  * bit 0 = 0) or 2^(-1/2): odd is_pos -> (i0^((is_pos + 1) / 2), 1), even ->
  * (1, i0^(is_pos / 2)); FFmpeg treats is_pos >= 16 as "no intensity". */
-static int orc_is_ratio(const orc_gr *g1, int p, double *v1, double *v2) {
+static int orc_is_ratio(const orc_gr *g1, int p, orc_real *v1, orc_real *v2) {
     if (!g1->lsf) {
         if (p >= 7) return 0;
         double t = tan(p * M_PI / 12.0);
@@ -465,12 +473,12 @@ static int orc_is_ratio(const orc_gr *g1, int p, double *v1, double *v2) {
     return 1;
 }
 
-static void orc_stereo(const orc_gr *g1, int sr_idx, int mode_ext, const uint8_t *sf1, double *l, double *r) {
-    const double isq = 1.0 / sqrt(2.0);
+static void orc_stereo(const orc_gr *g1, int sr_idx, int mode_ext, const uint8_t *sf1, orc_real *l, orc_real *r) {
+    const orc_real isq = 1.0 / sqrt(2.0);
     if (!(mode_ext & 1)) {
         if (mode_ext & 2)
             for (int i = 0; i < 576; i++) {
-                double m = l[i], s = r[i];
+                orc_real m = l[i], s = r[i];
                 l[i] = (m + s) * isq;
                 r[i] = (m - s) * isq;
             }
@@ -495,7 +503,7 @@ static void orc_stereo(const orc_gr *g1, int sr_idx, int mode_ext, const uint8_t
         for (int w = 2; w >= 0; w--) {
             pos -= len;
             int do_is = 0;
-            double v1 = 0, v2 = 0;
+            orc_real v1 = 0, v2 = 0;
             if (!nz_short[w]) {
                 for (int j = 0; j < len; j++)
                     if (r[pos + j] != 0.0) { nz_short[w] = 1; break; }
@@ -503,13 +511,13 @@ static void orc_stereo(const orc_gr *g1, int sr_idx, int mode_ext, const uint8_t
             }
             if (do_is) {
                 for (int j = 0; j < len; j++) {
-                    double x = l[pos + j];
+                    orc_real x = l[pos + j];
                     l[pos + j] = x * v1;
                     r[pos + j] = x * v2;
                 }
             } else if (mode_ext & 2) {
                 for (int j = 0; j < len; j++) {
-                    double m = l[pos + j], s = r[pos + j];
+                    orc_real m = l[pos + j], s = r[pos + j];
                     l[pos + j] = (m + s) * isq;
                     r[pos + j] = (m - s) * isq;
                 }
@@ -521,7 +529,7 @@ static void orc_stereo(const orc_gr *g1, int sr_idx, int mode_ext, const uint8_t
         int len = MP3D_SFB_LONG_WIDTH[sr_idx][i];
         pos -= len;
         int do_is = 0;
-        double v1 = 0, v2 = 0;
+        orc_real v1 = 0, v2 = 0;
         if (!nz) {
             for (int j = 0; j < len; j++)
                 if (r[pos + j] != 0.0) { nz = 1; break; }
@@ -530,13 +538,13 @@ static void orc_stereo(const orc_gr *g1, int sr_idx, int mode_ext, const uint8_t
         }
         if (do_is) {
             for (int j = 0; j < len; j++) {
-                double x = l[pos + j];
+                orc_real x = l[pos + j];
                 l[pos + j] = x * v1;
                 r[pos + j] = x * v2;
             }
         } else if (mode_ext & 2) {
             for (int j = 0; j < len; j++) {
-                double m = l[pos + j], s = r[pos + j];
+                orc_real m = l[pos + j], s = r[pos + j];
                 l[pos + j] = (m + s) * isq;
                 r[pos + j] = (m - s) * isq;
             }
@@ -546,28 +554,28 @@ static void orc_stereo(const orc_gr *g1, int sr_idx, int mode_ext, const uint8_t
 
 /* Short-block reorder (ISO 2.4.3.4): window-grouped bands -> (freq, window)
  * interleave, so line 3f+w holds window w's frequency f of the band. */
-static void orc_reorder(int block_type, int mixed, int sr_idx, double *xr) {
+static void orc_reorder(int block_type, int mixed, int sr_idx, orc_real *xr) {
     if (block_type != 2) return;
-    double tmp[576];
+    orc_real tmp[576];
     int start = mixed ? (sr_idx == 8 ? 72 : 36) : 0, b0 = mixed ? 3 : 0; /* FFmpeg reorder_block */
     int p = start;
     for (int i = b0; i < 13; i++) {
         int len = MP3D_SFB_SHORT_WIDTH[sr_idx][i];
         for (int f = 0; f < len; f++)
             for (int w = 0; w < 3; w++) tmp[3 * f + w] = xr[p + w * len + f];
-        memcpy(xr + p, tmp, sizeof(double) * 3 * len);
+        memcpy(xr + p, tmp, sizeof(orc_real) * 3 * len);
         p += 3 * len;
     }
 }
 
 /* Alias reduction, ISO 2.4.3.4 with Annex B Table B.9 coefficients. */
-static void orc_alias(int block_type, int mixed, double *xr) {
+static void orc_alias(int block_type, int mixed, orc_real *xr) {
     int nsb = block_type == 2 ? (mixed ? 1 : 0) : 31;
     for (int sb = 1; sb <= nsb; sb++)
         for (int i = 0; i < 8; i++) {
-            double c = MP3D_ALIAS_C[i], den = sqrt(1.0 + c * c);
-            double cs = 1.0 / den, ca = c / den;
-            double bu = xr[18 * sb - 1 - i], bd = xr[18 * sb + i];
+            orc_real c = MP3D_ALIAS_C[i], den = sqrt(1.0 + c * c);
+            orc_real cs = 1.0 / den, ca = c / den;
+            orc_real bu = xr[18 * sb - 1 - i], bd = xr[18 * sb + i];
             xr[18 * sb - 1 - i] = bu * cs - bd * ca;
             xr[18 * sb + i] = bd * cs + bu * ca;
         }
@@ -575,14 +583,14 @@ static void orc_alias(int block_type, int mixed, double *xr) {
 
 /* IMDCT + windowing + overlap-add + frequency inversion (ISO 2.4.3.4).
  * out[slot][sb], slot 0..17. */
-static void orc_imdct(int block_type, int mixed, const double *xr, double ov[32][18], double out[18][32]) {
+static void orc_imdct(int block_type, int mixed, const orc_real *xr, orc_real ov[32][18], orc_real out[18][32]) {
     for (int sb = 0; sb < 32; sb++) {
-        double z[36];
-        const double *X = xr + 18 * sb;
+        orc_real z[36];
+        const orc_real *X = xr + 18 * sb;
         int bt = (mixed && block_type == 2 && sb < 2) ? 0 : block_type;
         if (bt != 2) {
             for (int i = 0; i < 36; i++) {
-                double acc = 0;
+                orc_real acc = 0;
                 for (int k = 0; k < 18; k++) acc += X[k] * g_imdct36[k][i];
                 z[i] = acc * g_win[bt][i];
             }
@@ -590,13 +598,13 @@ static void orc_imdct(int block_type, int mixed, const double *xr, double ov[32]
             memset(z, 0, sizeof(z));
             for (int w = 0; w < 3; w++)
                 for (int i = 0; i < 12; i++) {
-                    double acc = 0;
+                    orc_real acc = 0;
                     for (int k = 0; k < 6; k++) acc += X[3 * k + w] * g_imdct12[k][i];
                     z[6 * w + 6 + i] += acc * g_win[2][i];
                 }
         }
         for (int i = 0; i < 18; i++) {
-            double v = z[i] + ov[sb][i];
+            orc_real v = z[i] + ov[sb][i];
             ov[sb][i] = z[i + 18];
             if ((sb & 1) && (i & 1)) v = -v;
             out[i][sb] = v;
@@ -605,29 +613,29 @@ static void orc_imdct(int block_type, int mixed, const double *xr, double ov[32]
 }
 
 /* Polyphase synthesis filterbank, ISO Annex A flowchart (direct form). */
-static void orc_synth(double V[1024], const double S[32], double *pcm32) {
-    memmove(V + 64, V, sizeof(double) * (1024 - 64));
+static void orc_synth(orc_real V[1024], const orc_real S[32], orc_real *pcm32) {
+    memmove(V + 64, V, sizeof(orc_real) * (1024 - 64));
     for (int i = 0; i < 64; i++) {
-        double acc = 0;
+        orc_real acc = 0;
         for (int k = 0; k < 32; k++) acc += g_synthN[i][k] * S[k];
         V[i] = acc;
     }
-    double U[512];
+    orc_real U[512];
     for (int i = 0; i < 8; i++)
         for (int j = 0; j < 32; j++) {
             U[i * 64 + j] = V[i * 128 + j];
             U[i * 64 + 32 + j] = V[i * 128 + 96 + j];
         }
     for (int j = 0; j < 32; j++) {
-        double acc = 0;
+        orc_real acc = 0;
         for (int i = 0; i < 16; i++) acc += U[j + 32 * i] * g_D[j + 32 * i];
         pcm32[j] = acc;
     }
 }
 
 /* Stages a8..a10 for one granule of one channel (xr in bitstream order). */
-static void orc_granule_to_pcm(orc_dec *d, int ch, int block_type, int mixed, int sr_idx, double *xr, double *pcm576) {
-    double out[18][32];
+static void orc_granule_to_pcm(orc_dec *d, int ch, int block_type, int mixed, int sr_idx, orc_real *xr, orc_real *pcm576) {
+    orc_real out[18][32];
     orc_reorder(block_type, mixed, sr_idx, xr);
     orc_alias(block_type, mixed, xr);
     orc_imdct(block_type, mixed, xr, d->overlap[ch], out);
@@ -700,7 +708,7 @@ ORC_API int orc_decode_frame_f64(orc_dec *d, const uint8_t *buf, int bytes, doub
     }
     b.pos = start_bit;
 
-    double pcm_local[2][1152];
+    orc_real pcm_local[2][1152];
     memset(d->is, 0, sizeof(d->is));
     memset(d->sf, 0, sizeof(d->sf));
     memset(d->xr, 0, sizeof(d->xr));
@@ -725,7 +733,7 @@ ORC_API int orc_decode_frame_f64(orc_dec *d, const uint8_t *buf, int bytes, doub
             orc_gr *g = &s->gr[gr][ch];
             int bt = g->window_switching ? g->block_type : 0;
             int mx = g->window_switching && g->block_type == 2 ? g->mixed : 0;
-            double xr[576];
+            orc_real xr[576];
             memcpy(xr, d->xr[gr][ch], sizeof(xr));
             if (gr < gr0) bt = 0, mx = 0;
             orc_granule_to_pcm(d, ch, bt, mx, h.sr_idx, xr, &pcm_local[ch][576 * gr]);
@@ -747,7 +755,8 @@ ORC_API int orc_decode_frame_f64(orc_dec *d, const uint8_t *buf, int bytes, doub
         d->hist_len = total;
     }
     if (pcm) {
-        for (int ch = 0; ch < h.nch; ch++) memcpy(pcm + 1152 * ch, pcm_local[ch], sizeof(double) * 576 * h.ngr);
+        for (int ch = 0; ch < h.nch; ch++)
+            for (int i = 0; i < 576 * h.ngr; i++) pcm[1152 * ch + i] = pcm_local[ch][i];
     }
     d->frames++;
     return 576 * h.ngr;
@@ -770,7 +779,7 @@ ORC_API void orc_get_taps(const orc_dec *d, int16_t *is /*[2][2][576]*/, uint8_t
     if (is) memcpy(is, d->is, sizeof(d->is));
     if (sf) memcpy(sf, d->sf, sizeof(d->sf));
     if (xr)
-        for (int i = 0; i < 2 * 2 * 576; i++) xr[i] = (float)((const double *)d->xr)[i];
+        for (int i = 0; i < 2 * 2 * 576; i++) xr[i] = (float)((const orc_real *)d->xr)[i];
     if (side) {
         memset(side, 0, sizeof(int32_t) * 2 * 2 * 20);
         for (int gr = 0; gr < d->hdr.ngr; gr++)
@@ -918,9 +927,9 @@ ORC_API void orc_synth_only(orc_dec *d, const float *xr, const uint8_t *block_ty
                             int n_frames, int nch, int sr_idx, int16_t *pcm, float *pcm_f32) {
     for (int f = 0; f < n_frames; f++)
         for (int gr = 0; gr < 2; gr++) {
-            double out[2][576];
+            orc_real out[2][576];
             for (int ch = 0; ch < nch; ch++) {
-                double x[576];
+                orc_real x[576];
                 const float *src = xr + (((size_t)f * 2 + gr) * nch + ch) * 576;
                 for (int i = 0; i < 576; i++) x[i] = src[i];
                 int bt = block_type[(f * 2 + gr) * nch + ch], mx = mixed[(f * 2 + gr) * nch + ch];
@@ -928,7 +937,7 @@ ORC_API void orc_synth_only(orc_dec *d, const float *xr, const uint8_t *block_ty
             }
             for (int i = 0; i < 576; i++)
                 for (int ch = 0; ch < nch; ch++) {
-                    double v = out[ch][i];
+                    orc_real v = out[ch][i];
                     size_t o = ((size_t)f * 1152 + gr * 576 + i) * nch + ch;
                     if (pcm_f32) pcm_f32[o] = (float)v;
                     if (pcm) {

@@ -56,6 +56,26 @@ def stream(cfg: dict, seed: int, n_frames: int, truth=False):
     return (out, offs, tr.reshape(n_frames, 2, 2)) if truth else (out, offs)
 
 
+def c2_spectra(n_streams: int, n_frames: int, nch: int = 2, seed: int = 1_000_003 * 2):
+    """BASELINE configs[1] input: requantised spectra
+    xr [n, F, 2 gr, nch, 576] f32 ~ N(0, sigma_k^2), sigma_k = 0.05 (1 +
+    k/16)^-1.5; ~15 % of granules in start -> short -> short -> stop runs,
+    10 % of those short granules mixed.  Returns (xr, block_type, mixed)."""
+    rng = np.random.default_rng(seed)
+    sig = (0.05 * (1 + np.arange(576) / 16.0) ** -1.5).astype(np.float32)
+    xr = rng.standard_normal((n_streams, n_frames, 2, nch, 576), dtype=np.float32) * sig
+    bt = np.zeros((n_streams, n_frames, 2, nch), np.uint8)
+    mx = np.zeros((n_streams, n_frames, 2, nch), np.uint8)
+    for f in range(1, n_frames - 2, 8):
+        run = rng.random(n_streams) < 0.6
+        mix = run & (rng.random(n_streams) < 0.1)
+        bt[run, f, 1] = 1
+        bt[run, f + 1, :] = 2
+        bt[run, f + 2, 0] = 3
+        mx[mix, f + 1, :] = 1
+    return xr, bt, mx
+
+
 def batch(cfg: dict, seed_base: int, n_streams: int, n_frames: int, threads=8):
     L = lib()
     c = GenCfg(**cfg)
