@@ -32,7 +32,7 @@ void launch_huffman(const uint8_t *, const uint64_t *, const FrameRec *, const u
 void launch_synth(const FrameRec *, const int16_t *, const UnitMeta *, const DevTables *, StreamState *, void *, bool, int,
                   int, int, hipStream_t);
 void launch_synth_xr(const float *, const uint8_t *, const uint8_t *, const DevTables *, StreamState *, int16_t *, int,
-                     int, int, int, hipStream_t);
+                     int, int, int, int, float *, hipStream_t);
 void launch_gather_frames(const void *, void *, const void *, void *, const int *, int, int, int, int, int,
                           hipStream_t);
 } // namespace mp3d
@@ -290,6 +290,8 @@ struct mp3d_batch {
     float *d_xr = nullptr;
     uint8_t *d_bt = nullptr, *d_mx = nullptr;
     size_t xr_cap = 0;
+    float *st_tail = nullptr; /* segmented synth: final overlap + fifo per stream */
+    size_t tail_cap = 0;
     std::vector<uint64_t> last_off, md_off_host;
     std::vector<uint32_t> last_len;
     int last_n = -1;
@@ -367,7 +369,7 @@ extern "C" void mp3d_batch_destroy(mp3d_batch *b) {
     (void)hipSetDevice(b->device);
     if (b->own) (void)hipStreamSynchronize(b->own);
     void *ptrs[] = {b->st, b->rec, b->sideu, b->is_buf, b->meta, b->d_in_off, b->d_md_off, b->d_in_len,
-                    b->d_infos, b->md, b->d_in, b->d_pcm, b->d_xr, b->d_bt, b->d_mx};
+                    b->d_infos, b->md, b->d_in, b->d_pcm, b->d_xr, b->d_bt, b->d_mx, b->st_tail};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : b->ev)
@@ -625,9 +627,32 @@ extern "C" int mp3d_batch_synth_only(mp3d_batch *b, const float *xr, const uint8
     if (b->timing) {
         for (int i = 0; i < 3; i++) HIPCHK(hipEventRecord(b->ev[i], s));
     }
-    launch_synth_xr(dxr, dbt, dmx, dc.tables, b->st, dpcm, n, F, nch, sr, s);
+    /* Few streams leave the chip idle (one wave walks one stream): split
+     * each stream into frame-parallel segments (k_synth, one warm-up frame
+     * each) until ~2 rounds of resident waves (3 per SIMD) are in the grid,
+     * keeping segments >= 4 frames (warm-up overhead <= 25 %).
+     * MP3D_SEG_FRAMES overrides the segment length. */
+    int seg_len = F;
+    {
+        const long long want = 2LL * 3 * 4 * dc.n_cu;
+        if ((long long)n < want && F >= 8) {
+            const int nseg = (int)std::min<long long>((want + n - 1) / n, F / 4);
+            seg_len = (F + nseg - 1) / nseg;
+        }
+        const char *e = getenv("MP3D_SEG_FRAMES");
+        if (e && atoi(e) > 0) seg_len = std::min(F, atoi(e));
+    }
+    const size_t tail = sizeof(((StreamState *)0)->overlap) + sizeof(((StreamState *)0)->fifo);
+    if (seg_len < F) {
+        int r = grow((void **)&b->st_tail, &b->tail_cap, tail * (size_t)n);
+        if (r) return r;
+    }
+    launch_synth_xr(dxr, dbt, dmx, dc.tables, b->st, dpcm, n, F, nch, sr, seg_len, b->st_tail, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[3], s));
     HIPCHK(hipGetLastError());
+    if (seg_len < F) /* the last segments' state into StreamState (overlap, fifo are its tail) */
+        HIPCHK(hipMemcpy2DAsync(&b->st[0].overlap[0][0][0], sizeof(StreamState), b->st_tail, tail, tail, n,
+                                hipMemcpyDeviceToDevice, s));
     if (pcm_host) {
         HIPCHK(hipMemcpyAsync(pcm, dpcm, pcm_bytes, hipMemcpyDeviceToHost, s));
         sync_needed = true;

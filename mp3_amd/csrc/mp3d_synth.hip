@@ -165,7 +165,7 @@ __global__ void __launch_bounds__(64 * SYN_WAVES) __attribute__((amdgpu_waves_pe
 k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, const UnitMeta *__restrict__ meta,
         const float *__restrict__ xr_in, const uint8_t *__restrict__ xr_bt, const uint8_t *__restrict__ xr_mixed,
         const DevTables *__restrict__ tab, StreamState *__restrict__ st, void *__restrict__ pcm, int n_streams,
-        int F, int xr_nch, int xr_sr) {
+        int F, int xr_nch, int xr_sr, int seg_len, float *__restrict__ st_tail) {
     __shared__ __attribute__((aligned(16))) SynShared<LSF> T;
     __shared__ __attribute__((aligned(16))) SynWave Wv[SYN_WAVES];
     constexpr int NRATE = LSF ? 6 : 3;
@@ -200,8 +200,19 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
         __syncthreads();
     }
     const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); /* wave-uniform (SGPR) */
-    const int s = blockIdx.x * SYN_WAVES + wid;
-    if (s >= n_streams) return; /* after the only workgroup barrier */
+    /* Frame-parallel segments (SRC_XR): wave vs decodes frames
+     * [f0, f1) of stream s after a one-frame warm-up from zero state.  The
+     * warm-up frame's granule 0 fixes the IMDCT overlap (the last 18 outputs
+     * of a granule's IMDCT do not depend on the state), its granule 1 then
+     * yields exact S, X and the 15 carried X slots, so [f0, f1) is
+     * bit-identical to the sequential decode.  One segment (seg_len >= F):
+     * the stream's state in and out, as before. */
+    const int nseg = (F + seg_len - 1) / seg_len;
+    const int vs = blockIdx.x * SYN_WAVES + wid;
+    if (vs >= n_streams * nseg) return; /* after the only workgroup barrier */
+    const int s = vs / nseg, seg = vs - s * nseg;
+    const int f0 = seg * seg_len, f1 = min(F, f0 + seg_len);
+    const int fw = seg ? f0 - 1 : 0; /* first frame decoded (warm-up below f0) */
     if (!SRC_XR && (st[s].kind == 2) != LSF) return; /* the other variant's stream */
     SynWave &Wd = Wv[wid];
     float *const sBuf = Wd.buf;
@@ -213,15 +224,24 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
     StreamState &S = st[s];
     const int wa = tab->win_a[sb], wb = tab->win_b[sb];
     float ov[18];
-#pragma unroll
-    for (int i = 0; i < 18; i++) ov[i] = S.overlap[ch][sb][i];
     /* synthesis history: ha[k] = X_{k-14}[wa], hb[k] = X_{k-15}[wb] (slot
      * index relative to the granule's first slot; fifo[t] = slot t - 15)  */
     float ha[14], hb[15];
+    if (seg == 0) {
 #pragma unroll
-    for (int k = 0; k < 14; k++) ha[k] = S.fifo[ch][k + 1][wa];
+        for (int i = 0; i < 18; i++) ov[i] = S.overlap[ch][sb][i];
 #pragma unroll
-    for (int k = 0; k < 15; k++) hb[k] = S.fifo[ch][k][wb];
+        for (int k = 0; k < 14; k++) ha[k] = S.fifo[ch][k + 1][wa];
+#pragma unroll
+        for (int k = 0; k < 15; k++) hb[k] = S.fifo[ch][k][wb];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 18; i++) ov[i] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 14; k++) ha[k] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 15; k++) hb[k] = 0.f;
+    }
 
     /* Per-stream buffer resources: every granule access below is a buffer
      * instruction with a uniform byte offset in an SGPR and the lane offset
@@ -282,13 +302,13 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
         nmeta2 = load_words(g + GSTEP);
     };
     if (!SRC_XR) {
-        prefetch_full(0);
+        prefetch_full(2 * fw);
         /* explicit drain on the entry path, so the compiler's wait before
          * each prefetch use is set by the loop path (stores after it) */
         WAIT_VMCNT0();
     }
 
-    for (int f = 0; f < F; f++) {
+    for (int f = fw; f < f1; f++) {
         int nch, sr, mode = 0, mext = 0;
         const size_t fr = (size_t)s * F + f;
         if (SRC_XR) {
@@ -303,7 +323,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
             if (!(r4 & 0xFFFFu) || (first_gr & (REC_TAG | REC_DROP))) {
                 /* no audio in this frame: fetch the next frame's granule 0
                  * now and wait for it here, off the common path */
-                if (f + 1 < F) prefetch_full(2 * (f + 1));
+                if (f + 1 < f1) prefetch_full(2 * (f + 1));
                 WAIT_VMCNT0();
                 continue;
             }
@@ -502,7 +522,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                 }
                 /* the next granule's loads fly during phases I, M, W (issued
                  * after cis is consumed: fewer live registers in phase Q) */
-                if (LSF ? f + 1 < F : (gr == 0 || f + 1 < F)) prefetch(LSF ? 2 * f + 2 : 2 * f + gr + 1);
+                if (LSF ? f + 1 < f1 : (gr == 0 || f + 1 < f1)) prefetch(LSF ? 2 * f + 2 : 2 * f + gr + 1);
                 /* scatter in (short-block reordered) position */
 #pragma unroll
                 for (int i = 0; i < 5; i++) {
@@ -706,7 +726,9 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                     return (int)fminf(fmaxf(p, -32768.f), 32767.f);
                 };
                 const int so = f * 2304 * PB + gr * 576 * nch * PB;
-                if (F32) {
+                if (f < f0) {
+                    /* warm-up frame: state only, no PCM */
+                } else if (F32) {
                     /* float sink: the same sums, unscaled and unclipped (FFmpeg's
                      * float decoder convention); (L, R) = 8 B per lane and slot */
                     if (nch == 2) {
@@ -758,13 +780,20 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
             wave_sync(); /* X reads done before the next granule's xr */
         }
     }
-    /* state out */
+    /* state out: the stream's last segment.  With several segments the
+     * first one may still be reading S, so the state goes to st_tail (the
+     * overlap + fifo tail of StreamState, copied in by the host after the
+     * launch). */
+    if (f1 == F) {
+        float *ovo = nseg > 1 ? st_tail + (size_t)s * (sizeof(S.overlap) + sizeof(S.fifo)) / 4 : &S.overlap[0][0][0];
+        float *ffo = ovo + sizeof(S.overlap) / 4;
 #pragma unroll
-    for (int i = 0; i < 18; i++) S.overlap[ch][sb][i] = ov[i];
+        for (int i = 0; i < 18; i++) ovo[(ch * 32 + sb) * 18 + i] = ov[i];
 #pragma unroll
-    for (int k = 0; k < 14; k++) S.fifo[ch][k + 1][wa] = ha[k];
+        for (int k = 0; k < 14; k++) ffo[(ch * MP3D_FIFO_SLOTS + k + 1) * 32 + wa] = ha[k];
 #pragma unroll
-    for (int k = 0; k < 15; k++) S.fifo[ch][k][wb] = hb[k];
+        for (int k = 0; k < 15; k++) ffo[(ch * MP3D_FIFO_SLOTS + k) * 32 + wb] = hb[k];
+    }
 }
 /* ------------------------------------------------------------------------ */
 /* k_gather_frames: segmented long-stream decode (mp3d_batch_decode_long).  */
@@ -810,7 +839,8 @@ void launch_synth(const FrameRec *rec, const int16_t *is_buf, const UnitMeta *me
      * costs only its workgroup dispatch) */
 #define MP3D_SYNTH_LAUNCH(F32_, LSF_)                                                                            \
     hipLaunchKernelGGL((k_synth<false, F32_, LSF_>), grid, block, 0, strm, rec, is_buf, meta, (const float *)nullptr, \
-                       (const uint8_t *)nullptr, (const uint8_t *)nullptr, tab, st, pcm, n_streams, F, 2, 0)
+                       (const uint8_t *)nullptr, (const uint8_t *)nullptr, tab, st, pcm, n_streams, F, 2, 0, F,     \
+                       (float *)nullptr)
     if (f32) {
         if (kinds & 1) MP3D_SYNTH_LAUNCH(true, false);
         if (kinds & 2) MP3D_SYNTH_LAUNCH(true, true);
@@ -821,11 +851,15 @@ void launch_synth(const FrameRec *rec, const int16_t *is_buf, const UnitMeta *me
 #undef MP3D_SYNTH_LAUNCH
 }
 
+/* seg_len < F: frame-parallel segments (k_synth); st_tail then receives the
+ * streams' final overlap + fifo, which the caller copies into st */
 void launch_synth_xr(const float *xr, const uint8_t *bt, const uint8_t *mixed, const DevTables *tab, StreamState *st,
-                     int16_t *pcm, int n_streams, int F, int nch, int sr, hipStream_t strm) {
-    hipLaunchKernelGGL((k_synth<true, false, false>), dim3((n_streams + SYN_WAVES - 1) / SYN_WAVES), dim3(64 * SYN_WAVES), 0,
+                     int16_t *pcm, int n_streams, int F, int nch, int sr, int seg_len, float *st_tail,
+                     hipStream_t strm) {
+    const int waves = n_streams * ((F + seg_len - 1) / seg_len);
+    hipLaunchKernelGGL((k_synth<true, false, false>), dim3((waves + SYN_WAVES - 1) / SYN_WAVES), dim3(64 * SYN_WAVES), 0,
                        strm, (const FrameRec *)nullptr, (const int16_t *)nullptr, (const UnitMeta *)nullptr, xr, bt,
-                       mixed, tab, st, (void *)pcm, n_streams, F, nch, sr);
+                       mixed, tab, st, (void *)pcm, n_streams, F, nch, sr, seg_len, st_tail);
 }
 
 void launch_gather_frames(const void *src, void *dst, const void *isrc, void *idst, const int *a, int L, int F, int k0,

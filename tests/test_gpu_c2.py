@@ -1,0 +1,76 @@
+"""GPU: BASELINE configs[1] (C2) at its full size -- 1,024 streams x 64 frames
+of synthetic spectra through mp3d_batch_synth_only -- against the oracle
+(orc_synth_only, double precision) on a stream subset, PCM within 1 LSB.
+
+At 1,024 streams the library splits every stream into frame-parallel
+segments (k_synth, one warm-up frame each); the test also pins that the
+segmented decode is bit-identical to the one-wave-per-stream decode
+(MP3D_SEG_FRAMES = F), including the per-stream state carried into a second
+call."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import _gen
+import _oracle
+import mp3_amd
+
+pytestmark = pytest.mark.gpu
+
+N, F, NCH = 1024, 64, 2
+SUBSET = [0, 1, 2, 511, 777, 1023]
+
+
+def _oracle_pcm(xr, bt, mx, s, frames):
+    L = _oracle.lib()
+    d = L.orc_create()
+    ref = np.zeros((frames, 1152, NCH), np.int16)
+    L.orc_synth_only(d, np.ascontiguousarray(xr[s, :frames]).ctypes.data, np.ascontiguousarray(bt[s, :frames]).ctypes.data,
+                     np.ascontiguousarray(mx[s, :frames]).ctypes.data, frames, NCH, 0, ref.ctypes.data, None)
+    L.orc_destroy(d)
+    return ref
+
+
+def _run(xr, bt, mx, seg=None, calls=1):
+    """decode F frames per call, `calls` calls, device buffers; PCM [N, calls*F, 2304]"""
+    if seg is None:
+        os.environ.pop("MP3D_SEG_FRAMES", None)
+    else:
+        os.environ["MP3D_SEG_FRAMES"] = str(seg)
+    try:
+        dec = mp3_amd.BatchDecoder(N, F)
+        out = []
+        for c in range(calls):
+            sl = slice(c * F, (c + 1) * F)
+            d_xr, d_bt, d_mx = (torch.from_numpy(np.ascontiguousarray(a[:, sl])).cuda() for a in (xr, bt, mx))
+            pcm = torch.zeros((N, F, 2304), dtype=torch.int16, device="cuda")
+            dec.synth_only(d_xr, d_bt, d_mx, NCH, 44100, pcm=pcm)
+            torch.cuda.synchronize()
+            out.append(pcm.cpu().numpy())
+        return np.concatenate(out, axis=1)
+    finally:
+        os.environ.pop("MP3D_SEG_FRAMES", None)
+
+
+def test_c2_full_size_vs_oracle():
+    xr, bt, mx = _gen.c2_spectra(N, F, NCH)
+    assert (bt == 2).mean() > 0.05 and mx.any()
+    pcm = _run(xr, bt, mx)
+    for s in SUBSET:
+        ref = _oracle_pcm(xr, bt, mx, s, F)
+        got = pcm[s, :, :1152 * NCH].reshape(F, 1152, NCH)
+        assert np.abs(got.astype(np.int32) - ref.astype(np.int32)).max() <= 1, s
+
+
+def test_c2_segments_bit_identical_across_calls():
+    xr, bt, mx = _gen.c2_spectra(N, 2 * F, NCH, seed=4242)
+    seq = _run(xr, bt, mx, seg=F, calls=2)   # one wave per stream
+    for seg in (None, 4, 7):                  # library choice, short and ragged segments
+        got = _run(xr, bt, mx, seg=seg, calls=2)
+        assert np.array_equal(got, seq), seg
+    for s in SUBSET[:3]:
+        ref = _oracle_pcm(xr, bt, mx, s, 2 * F)
+        g = seq[s, :, :1152 * NCH].reshape(2 * F, 1152, NCH)
+        assert np.abs(g.astype(np.int32) - ref.astype(np.int32)).max() <= 1, s
