@@ -231,8 +231,8 @@ def launch_ranks(n):
             break
         time.sleep(0.2)
     relay.join(timeout=10)
-    for line in out:
-        sys.stdout.write(line.decode())
+    for line in out:  # the JSON line to stdout, anything else (library chatter) to stderr
+        (sys.stdout if line.startswith(b"{") else sys.stderr).write(line.decode())
     sys.stdout.flush()
     if rc:
         log("bench.py: a rank exited with status %d" % rc)

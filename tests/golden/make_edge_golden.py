@@ -34,7 +34,7 @@ sys.path.insert(0, str(HERE))
 sys.path.insert(0, str(HERE.parent))
 import ffmpeg_oracle  # noqa: E402
 import _gen  # noqa: E402
-from make_golden import to_int16  # noqa: E402
+from make_golden import record_hashes, to_int16  # noqa: E402
 
 
 def set_big_values(frame: bytearray, gr: int, ch: int, value: int):
@@ -132,6 +132,7 @@ def main():
                               our_frames=prev.get("our_frames"), note=prev.get("note"))
         print(name, hz, nch, len(data), ref.shape)
     man_path.write_text(json.dumps(manifest, indent=1, sort_keys=True))
+    record_hashes()
 
 
 if __name__ == "__main__":

@@ -8,8 +8,14 @@ its int16 output to WebAudio as float via n/32767 (n >= 0) and n/32768
 (n < 0), so the exact int16 samples are recovered below (all integral to
 within float32 rounding, asserted).
 
+Every script here merges its cases into manifest.json and then rewrites
+hashes.json (sha256 of every committed fixture file); tests/test_golden_repro.py
+checks both, and that the generator still reproduces each generated stream's
+committed bytes (so this script regenerates exactly what is committed).
+
 Usage:  python tests/golden/make_golden.py
 """
+import hashlib
 import json
 import pathlib
 import sys
@@ -53,8 +59,15 @@ def cases():
     return out
 
 
+def record_hashes():
+    """hashes.json: sha256 of every fixture file (.mp3 inputs, .npy PCM)."""
+    files = sorted(p for p in HERE.iterdir() if p.suffix in (".mp3", ".npy"))
+    h = {p.name: hashlib.sha256(p.read_bytes()).hexdigest() for p in files}
+    (HERE / "hashes.json").write_text(json.dumps(h, indent=1, sort_keys=True))
+
+
 def main():
-    manifest = {}
+    manifest = json.loads((HERE / "manifest.json").read_text()) if (HERE / "manifest.json").exists() else {}
     # real-world fixture: MathJax a11y "invalid_keypress.mp3" (Apache-2.0)
     fix = open(FIX_SRC, "rb").read()
     (HERE / "keypress_128k_js.mp3").write_bytes(fix)
@@ -75,6 +88,7 @@ def main():
         manifest[name] = dict(cfg=cfg, seed=seed, frames=N_FRAMES, hz=hz, nch=nch)
         print(name, hz, nch, len(data))
     (HERE / "manifest.json").write_text(json.dumps(manifest, indent=1, sort_keys=True))
+    record_hashes()
 
 
 if __name__ == "__main__":

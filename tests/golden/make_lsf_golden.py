@@ -27,7 +27,7 @@ sys.path.insert(0, str(HERE))
 sys.path.insert(0, str(HERE.parent))
 import ffmpeg_oracle  # noqa: E402
 import _gen  # noqa: E402
-from make_golden import to_int16  # noqa: E402
+from make_golden import record_hashes, to_int16  # noqa: E402
 
 HZ = [44100, 48000, 32000, 22050, 24000, 16000, 11025, 12000, 8000]
 N_FRAMES = 16
@@ -59,6 +59,7 @@ def main():
         manifest[name] = dict(cfg=cfg, seed=seed, frames=N_FRAMES, hz=hz, nch=nch, spf=576)
         print(name, hz, nch, len(data))
     (HERE / "manifest.json").write_text(json.dumps(manifest, indent=1, sort_keys=True))
+    record_hashes()
 
 
 if __name__ == "__main__":
