@@ -25,6 +25,7 @@ def build_hip(force=False):
     out = ROOT / "mp3_amd" / "libmp3d.so"
     srcs = [CSRC / "mp3d_demux.hip", CSRC / "mp3d_huffman.hip", CSRC / "mp3d_synth.hip", CSRC / "mp3d_host.cpp"]
     deps = srcs + [CSRC / "mp3d_internal.h", CSRC / "mp3d_tables.h", CSRC / "mp3d_consts.h", CSRC / "mp3d_device.h",
+                   CSRC / "mp3d_hostparse.h",
                    ROOT / "include" / "mp3d.h"]
     if force or _stale(out, deps):
         cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-fPIC", "-shared", "-std=c++17", "-fvisibility=hidden",

@@ -21,6 +21,7 @@
 #include "mp3d_internal.h"
 #include "mp3d_tables.h"
 #include "mp3d_consts.h"
+#include "mp3d_hostparse.h"
 
 namespace mp3d {
 hipError_t upload_synth_constants(const float *, const float *, const float *, const float *);
@@ -691,64 +692,6 @@ extern "C" int mp3d_batch_stream_info(mp3d_batch *b, int n, mp3d_stream_info *ou
 /* ------------------------------------------------------------------------ */
 /* Segmented decode of one long stream               */
 /* ------------------------------------------------------------------------ */
-static int host_frame_bytes(const uint8_t *p, int kind);
-static int host_frame_kind(const uint8_t *p);
-static int host_frame_head(const uint8_t *p);
-
-/* Frame slots of a stream exactly as k_demux enumerates them: ID3v2 skip,
- * resync on the next valid header, a cut-short final frame kept while its
- * header and side info are present.  payload = bytes after the side info. */
-static void walk_frames(const uint8_t *p, size_t len, std::vector<uint64_t> &off, std::vector<uint32_t> &payload) {
-    size_t cur = 0;
-    if (len >= 10 && p[0] == 'I' && p[1] == 'D' && p[2] == '3')
-        cur = 10 + (((size_t)(p[6] & 0x7F) << 21) | ((size_t)(p[7] & 0x7F) << 14) | ((size_t)(p[8] & 0x7F) << 7) |
-                    (p[9] & 0x7F)) +
-              ((p[5] & 0x10) ? 10 : 0);
-    int kind = 0; /* MPEG family lock, as k_demux */
-    while (cur + 4 <= len) {
-        int fb = -1;
-        for (; cur + 4 <= len; cur++)
-            if ((fb = host_frame_bytes(p + cur, kind)) > 0) break;
-        if (fb <= 0) break;
-        kind = host_frame_kind(p + cur);
-        const size_t need = (size_t)host_frame_head(p + cur);
-        if (cur + fb > len && cur + need > len) break;
-        off.push_back(cur);
-        payload.push_back(fb > (int)need ? (uint32_t)(fb - need) : 0u);
-        cur = cur + fb <= len ? cur + fb : len;
-    }
-}
-
-/* Split the stream into segments of L output frames decoded as independent
- * virtual streams of one batch call.  Segment k (k >= 1) starts at frame
- * a_k < kL, chosen so that the payloads of frames [a_k, kL - 2) hold >= 511
- * bytes (the largest main_data_begin).  Why that suffices (k_demux's
- * reservoir rule): the bytes available after a frame, P + plen - end, do not
- * depend on the history once the frame's main-data start P - mdb is inside
- * the virtual stream's md region, i.e. from frame kL - 2 on; frame kL - 1
- * then decodes from real bytes with the sequential decoder's reservoir
- * decision, and its second granule alone feeds frame kL's IMDCT overlap and
- * synthesis FIFO (15 slots < 18 per granule).  Output frames [kL, (k+1)L)
- * are therefore bit-exact with a sequential decode of the whole stream;
- * warm-up output is dropped. */
-static int long_plan(const uint8_t *p, size_t bytes, int L, long long max_frames, std::vector<uint64_t> &off,
-                     std::vector<long long> &a, int *wmax) {
-    std::vector<uint32_t> pay;
-    walk_frames(p, bytes, off, pay);
-    const long long N = (long long)off.size();
-    if (N > max_frames) return MP3D_E_CAPACITY;
-    const long long K = (N + L - 1) / L;
-    a.assign(K, 0);
-    *wmax = 0;
-    for (long long k = 0; k < K; k++) {
-        long long j = std::max(0LL, k * L - 2), acc = 0;
-        while (j > 0 && acc < MP3D_RES_BYTES - 1) acc += pay[--j];
-        a[k] = j;
-        *wmax = std::max(*wmax, (int)(k * L - j));
-    }
-    return MP3D_OK;
-}
-
 extern "C" int mp3d_long_plan(const uint8_t *data, size_t bytes, int L, long long max_frames, uint64_t *frame_off,
                               long long *seg_start, long long *n_frames, int *max_warmup) {
     if (!data || L <= 0 || max_frames < 0 || !n_frames) return MP3D_E_ARG;
@@ -946,52 +889,21 @@ extern "C" int mp3d_dec_stream_info(mp3d_dec *d, mp3d_stream_info *out) {
     return mp3d_batch_stream_info(d->b, 1, out);
 }
 
-/* Layer III frame bytes of the header at p, or -1 (k_demux hdr_frame_bytes):
- * MPEG-1 and MPEG-2 / 2.5 LSF; kind 0 any family, 1 MPEG-1 only, 2 LSF only */
-static int host_frame_kind(const uint8_t *p) { return ((p[1] >> 3) & 3) == 3 ? 1 : 2; }
-static int host_frame_bytes(const uint8_t *p, int kind) {
-    const int ver = (p[1] >> 3) & 3;
-    if (p[0] != 0xFF || (p[1] & 0xE0) != 0xE0 || ((p[1] >> 1) & 3) != 1 || ver == 1) return -1;
-    const int bi = p[2] >> 4, si = (p[2] >> 2) & 3;
-    if (bi == 0 || bi == 15 || si == 3) return -1;
-    const int k = host_frame_kind(p);
-    if (kind && k != kind) return -1;
-    const int hz = (int)MP3D_SAMPLE_RATE[si + (ver == 3 ? 0 : ver == 2 ? 3 : 6)];
-    return (k == 1 ? 144000 * (int)MP3D_BITRATE_L3[bi] : 72000 * (int)MP3D_BITRATE_L3_LSF[bi]) / hz +
-           ((p[2] >> 1) & 1);
-}
-/* header + CRC + side-info bytes */
-static int host_frame_head(const uint8_t *p) {
-    const bool mono = (p[3] >> 6) == 3, lsf = host_frame_kind(p) == 2;
-    return 4 + ((p[1] & 1) ? 0 : 2) + (lsf ? (mono ? 9 : 17) : (mono ? 17 : 32));
-}
-
 static int decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, void *pcm, bool f32, bool last,
                         mp3d_frame_info *info) {
     if (!d || !buf) return MP3D_E_ARG;
     mp3d_frame_info tmp;
     if (!info) info = &tmp;
     memset(info, 0, sizeof(*info));
-    size_t pos = 0;
-    if (d->frames == 0 && bytes >= 10 && buf[0] == 'I' && buf[1] == 'D' && buf[2] == '3') {
-        size_t sz = ((size_t)(buf[6] & 0x7F) << 21) | ((size_t)(buf[7] & 0x7F) << 14) | ((size_t)(buf[8] & 0x7F) << 7) |
-                    (buf[9] & 0x7F);
-        pos = 10 + sz + ((buf[5] & 0x10) ? 10 : 0);
-    }
+    size_t pos = 0, have = 0;
     int fb = -1;
-    while (pos + 4 <= bytes) {
-        fb = host_frame_bytes(buf + pos, d->kind);
-        if (fb > 0) break;
-        pos++;
+    /* next frame (ID3v2 / junk skipped); a final frame cut short only with
+     * MP3D_FRAME_LAST: decoded with the missing bytes as zeros (k_demux) */
+    const int loc = pf_locate(buf, bytes, d->kind, d->frames == 0, last, &pos, &fb, &have);
+    if (loc <= 0) {
+        info->frame_bytes = (int)pos;
+        return loc;
     }
-    /* a final frame cut short (MP3D_FRAME_LAST): decoded once its header and
-     * side info are present, the missing bytes reading as zeros (k_demux) */
-    const bool cut = fb > 0 && pos + (size_t)fb > bytes;
-    if (fb <= 0 || (cut && !(last && pos + (size_t)host_frame_head(buf + pos) <= bytes))) {
-        info->frame_bytes = (int)std::min<size_t>(pos, bytes);
-        return info->frame_bytes ? 0 : MP3D_E_NEED_MORE;
-    }
-    const size_t have = cut ? bytes - pos : (size_t)fb;
     uint64_t off = 0;
     uint32_t sz = MP3D_PF_BYTES;
     memcpy(d->h_in, buf + pos, have); /* have <= fb <= MP3D_MAX_FRAME_BYTES */
