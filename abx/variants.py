@@ -16,18 +16,27 @@ def variant(name, reps):
         srcs = {k: s.replace(a, b) for k, s in srcs.items()}
     d = "/tmp/vars/" + name
     os.makedirs(d, exist_ok=True)
-    for h in ["mp3d_internal.h", "mp3d_tables.h", "mp3d_consts.h", "mp3d_device.h"]:
+    for h in ["mp3d_internal.h", "mp3d_tables.h", "mp3d_consts.h", "mp3d_device.h", "mp3d_hostparse.h"]:
         shutil.copy("mp3_amd/csrc/" + h, d)
     for k, s in srcs.items():
         open(d + "/" + k, "w").write(s)
+    shutil.copy("mp3_amd/csrc/mp3d_host.cpp", d)
+    os.makedirs(d + "/../../include", exist_ok=True)
+    shutil.copy("include/mp3d.h", d + "/../../include/")
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
                            "-fvisibility=hidden", "-o", "abx/%s.so" % name] + [d + "/" + k for k in KERNELS] +
-                          ["mp3_amd/csrc/mp3d_host.cpp"])
+                          [d + "/mp3d_host.cpp"])
 
 
 W4H = ("__global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(",
        "__global__ void __launch_bounds__(HUFF_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 8))) k_huffman(")
 VARS = {
+    "BASE": [],
+    # r02: k_demux without the waves_per_eu(8, 8) attribute of commit 315cc86
+    "DMW0": [("__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) k_demux(",
+              "__global__ void __launch_bounds__(64) k_demux(")],
+    # r02: the synth-only (C2) variant at 4 waves / SIMD (131 -> 128 VGPRs)
+    "XW4": [("__attribute__((amdgpu_waves_per_eu(3, 8)))", "__attribute__((amdgpu_waves_per_eu(SRC_XR ? 4 : 3, 8)))")],
     "CAP2300": [("#define HUFF_CAPW 2400", "#define HUFF_CAPW 2300")],
     "LUT2400": [("#define HUFF_CAPW 2300", "#define HUFF_CAPW 2400")],
     "DM1": [("const bool lsf = hdr_kind(h1) == 2;", "const bool lsf = false;")],

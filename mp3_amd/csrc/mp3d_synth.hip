@@ -161,7 +161,10 @@ struct SynWave {                     /* one per wave (stream)                   
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 template <bool SRC_XR, bool F32, bool LSF>
-__global__ void __launch_bounds__(64 * SYN_WAVES) __attribute__((amdgpu_waves_per_eu(3, 8)))
+/* 3 waves / SIMD (168 VGPRs) for the decode variants; the synth-only entry
+ * (no requantise / stereo registers) fits 128 VGPRs: 4 waves / SIMD, -3.4 %
+ * k_synth time on C2 (A/B XW4, profiles/r02_ab.txt) */
+__global__ void __launch_bounds__(64 * SYN_WAVES) __attribute__((amdgpu_waves_per_eu(SRC_XR ? 4 : 3, 8)))
 k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, const UnitMeta *__restrict__ meta,
         const float *__restrict__ xr_in, const uint8_t *__restrict__ xr_bt, const uint8_t *__restrict__ xr_mixed,
         const DevTables *__restrict__ tab, StreamState *__restrict__ st, void *__restrict__ pcm, int n_streams,
