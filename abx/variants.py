@@ -30,7 +30,15 @@ def variant(name, reps):
 
 W4H = ("__global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(",
        "__global__ void __launch_bounds__(HUFF_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 8))) k_huffman(")
+LID = "__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u))"
 VARS = {
+    # r02 timing-only probes (wrong output): k_huffman with conflict-free window / LUT reads
+    "HW0": [("    const uint32_t w0 = bits[w], w1 = bits[w + 1], w2 = bits[w + 2];",
+             "    const uint32_t ln = " + LID + "; (void)w;\n    const uint32_t w0 = bits[ln], w1 = bits[ln + 64], w2 = bits[ln + 128];"),
+            ("    const uint32_t w0 = bits[w], w1 = bits[w + 1];",
+             "    const uint32_t ln = " + LID + "; (void)w;\n    const uint32_t w0 = bits[ln], w1 = bits[ln + 64];")],
+    "LUT0": [("const uint32_t e1 = s_lut[i1];", "const uint32_t e1 = s_lut[(i1 & ~63u) + (uint32_t)lane];"),
+             ("const uint32_t e = s_lut[i2];", "const uint32_t e = s_lut[(i2 & ~63u) + (uint32_t)lane];")],
     "BASE": [],
     # r02: k_demux without the waves_per_eu(8, 8) attribute of commit 315cc86
     "DMW0": [("__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) k_demux(",

@@ -1,0 +1,122 @@
+"""GPU: the BASELINE full-size workloads through size-independent properties
+(C3 oracle coverage was a 5-stream spot check), and
+the multi-rank path actually decoding (weak item 7).
+
+- C3 at its full size (65,536 streams x 32 frames): every frame decodes; a
+  stride sample of 256 streams matches the oracle within 1 LSB (oracle on a
+  host thread pool); two calls of 16 frames are bit-identical to one call
+  of 32 (state resident in HBM); a stream decodes the same alone as inside
+  the batch (no cross-stream coupling).
+- C4 rehearsal: two rank processes (gloo, sharing this box's one GPU) each
+  decode their shard of global stream ids; rank 0 gathers the PCM, which
+  must equal a single-process decode of the same global streams.
+"""
+import os
+import socket
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+import torch
+
+import _gen
+import _golden
+import _oracle
+import mp3_amd
+from mp3_amd import shard
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_check(buf, offs, sizes, pcm, infos, streams):
+    def one(s):
+        data = bytes(buf[offs[s]:offs[s] + sizes[s]])
+        o = _golden.to_int16(_oracle.decode_stream(data)[0])
+        g = mp3_amd.pcm_to_planar(pcm[s], infos[s])
+        if g.shape != o.shape:
+            return 1 << 20
+        return int(np.abs(g.astype(np.int32) - o.astype(np.int32)).max())
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        return max(ex.map(one, streams))
+
+
+def test_c3_full_size_properties():
+    n, F = 65536, 32
+    buf, offs, sizes = _gen.batch(_gen.C3, shard.BASE_SEED_C3, n, F, threads=16)
+    d_in = torch.from_numpy(buf).cuda()
+    pcm = torch.empty((n, F, 2304), dtype=torch.int16, device="cuda")
+    inf = torch.zeros((n, F, 6), dtype=torch.int32, device="cuda")
+    dec = mp3_amd.BatchDecoder(n, F)
+    dec.decode(d_in, offs, sizes, F, pcm=pcm, infos=inf)
+    torch.cuda.synchronize()
+    assert int((inf[..., 5] == 1152).sum()) == n * F
+    # the same streams in two calls of 16 frames: bit-identical (state in HBM)
+    infs = inf.cpu().numpy()
+    first = infs[:, : F // 2, 0].astype(np.int64).sum(1)  # bytes of frames 0 .. 15
+    half = mp3_amd.BatchDecoder(n, F // 2)
+    pa = torch.empty((n, F // 2, 2304), dtype=torch.int16, device="cuda")
+    pb = torch.empty_like(pa)
+    half.decode(d_in, offs, first.astype(np.uint32), F // 2, pcm=pa)
+    half.decode(d_in, offs + first.astype(np.uint64), (sizes - first).astype(np.uint32), F // 2, pcm=pb)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat([pa, pb], 1), pcm)
+    del pa, pb, half
+    host_pcm = pcm.cpu().numpy()
+    infos = infs.reshape(-1).view(mp3_amd.FRAME_INFO_DT).reshape(n, F)
+    worst = _oracle_check(buf, offs, sizes, host_pcm, infos, range(0, n, n // 256))
+    assert worst <= 1, worst
+    # a few streams alone == inside the batch
+    for s in (0, 12345, n - 1):
+        data = np.frombuffer(bytes(buf[offs[s]:offs[s] + sizes[s]]), np.uint8)
+        p1, _ = mp3_amd.BatchDecoder(1, F).decode(data, [0], [len(data)], F)
+        assert np.array_equal(p1[0], host_pcm[s]), s
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+RANK_SCRIPT = r"""
+import os, sys, numpy as np, torch, torch.distributed as dist
+sys.path.insert(0, os.environ["REPO"]); sys.path.insert(0, os.environ["REPO"] + "/tests")
+import _gen, mp3_amd
+from mp3_amd import shard
+dist.init_process_group("gloo")
+rank, world = dist.get_rank(), dist.get_world_size()
+n, F = int(os.environ["N"]), int(os.environ["F"])
+buf, offs, sizes = _gen.batch(_gen.C5, shard.shard_seed_base(rank, n), n, F, threads=4)
+dec = mp3_amd.BatchDecoder(n, F, device=0)
+d_in = torch.from_numpy(buf).cuda()
+pcm = torch.zeros((n, F, 2304), dtype=torch.int16, device="cuda")
+dec.decode(d_in, offs, sizes, F, pcm=pcm)
+torch.cuda.synchronize()
+got = shard.gather_to_root(pcm)
+if rank == 0:
+    np.save(os.environ["OUT"], torch.cat(got).cpu().numpy())
+dist.destroy_process_group()
+"""
+
+
+def test_two_ranks_decode_their_shards(tmp_path):
+    n, F, world = 96, 6, 2
+    out = tmp_path / "gathered.npy"
+    script = tmp_path / "rank.py"
+    script.write_text(RANK_SCRIPT)
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), REPO=str(_golden.GOLDEN.parents[1]), N=str(n), F=str(F), OUT=str(out))
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env))
+    for p in procs:
+        assert p.wait(timeout=300) == 0
+    gathered = np.load(out)
+    buf, offs, sizes = _gen.batch(_gen.C5, shard.BASE_SEED_C3, world * n, F, threads=4)
+    ref, _ = mp3_amd.BatchDecoder(world * n, F).decode(buf, offs, sizes, F)
+    assert np.array_equal(gathered, ref)

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("tag")
     ap.add_argument("--streams", type=int, default=65536)
     ap.add_argument("--frames", type=int, default=32)
+    ap.add_argument("--config", default="c3", help="key of the entry in profiles/pmc_traffic.json")
     a = ap.parse_args()
     src = ROOT / "gpurun_out" / ("prof_" + a.tag)
     dst = ROOT / "profiles"
@@ -59,17 +60,26 @@ def main():
             cs["mfma_util"] = cs["SQ_VALU_MFMA_BUSY_CYCLES"] / (cs["GRBM_GUI_ACTIVE"] / 8.0 * 1024)
             cs["mfma_f32_flop_per_launch"] = cs.get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0.0) * 512
     (dst / (a.tag + "_pmc.json")).write_text(json.dumps(out, indent=1, sort_keys=True))
-    # the MPEG-1 int16 decode variant (k_synth<SRC_XR=false, F32=false, LSF=false>)
-    key = next((k for k in out if k.replace(" ", "") in ("k_synth<false,false,false>", "k_synth<false>")), None)
+    # the MPEG-1 int16 decode variant (k_synth<SRC_XR=false, F32=false, LSF=false>), or the
+    # synth-only one for C2; entries per workload config, read by bench.py
+    want = ("k_synth<true,false,false>",) if a.config == "c2" else ("k_synth<false,false,false>", "k_synth<false>")
+    key = next((k for k in out if k.replace(" ", "") in want), None)
     synth = out.get(key, {})
     if "hbm_bytes_per_launch" in synth:
-        (dst / "pmc_traffic.json").write_text(json.dumps({
+        tp = dst / "pmc_traffic.json"
+        allp = json.loads(tp.read_text()) if tp.exists() else {}
+        if "tag" in allp:  # older flat layout (C3 only)
+            allp = {"c3": allp}
+        allp[a.config] = {
             "tag": a.tag, "streams": a.streams, "frames": a.frames,
             "k_synth_hbm_bytes_per_launch": synth["hbm_bytes_per_launch"],
             "k_synth_fetch_kib": synth["FETCH_SIZE"], "k_synth_write_kib": synth["WRITE_SIZE"],
             "k_synth_mfma_util": synth.get("mfma_util"),
             "k_synth_mfma_f32_flop_per_launch": synth.get("mfma_f32_flop_per_launch"),
-            "method": "2 x FETCH_SIZE + WRITE_SIZE, separate rocprofv3 --pmc passes (tools/profile.sh)"}, indent=1))
+            "step_hbm_bytes": sum(cs.get("hbm_bytes_per_launch", 0.0) for cs in out.values()),
+            "per_kernel_hbm_bytes": {k: cs.get("hbm_bytes_per_launch") for k, cs in out.items()},
+            "method": "2 x FETCH_SIZE + WRITE_SIZE, separate rocprofv3 --pmc passes (tools/profile.sh)"}
+        tp.write_text(json.dumps(allp, indent=1, sort_keys=True))
     for k, cs in sorted(out.items()):
         print(k, {c: "%.4g" % v for c, v in cs.items()})
 
