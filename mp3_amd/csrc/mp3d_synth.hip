@@ -161,10 +161,12 @@ struct SynWave {                     /* one per wave (stream)                   
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 template <bool SRC_XR, bool F32, bool LSF>
-/* 3 waves / SIMD (168 VGPRs) for the decode variants; the synth-only entry
- * (no requantise / stereo registers) fits 128 VGPRs: 4 waves / SIMD, -3.4 %
- * k_synth time on C2 (A/B XW4, profiles/r02_ab.txt) */
-__global__ void __launch_bounds__(64 * SYN_WAVES) __attribute__((amdgpu_waves_per_eu(SRC_XR ? 4 : 3, 8)))
+/* 3 waves / SIMD (168 VGPRs).  The synth-only entry would fit 4 waves /
+ * SIMD without its spectra prefetch (-3.4 % k_synth on C2, A/B XW4), but the
+ * one-granule-ahead prefetch at 3 waves is worth -13 % (A/B XPF3 vs XPF4,
+ * profiles/r02_ab.txt): a wave's exposed load latency costs more than a
+ * fourth wave hides. */
+__global__ void __launch_bounds__(64 * SYN_WAVES) __attribute__((amdgpu_waves_per_eu(3, 8)))
 k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, const UnitMeta *__restrict__ meta,
         const float *__restrict__ xr_in, const uint8_t *__restrict__ xr_bt, const uint8_t *__restrict__ xr_mixed,
         const DevTables *__restrict__ tab, StreamState *__restrict__ st, void *__restrict__ pcm, int n_streams,
@@ -304,6 +306,30 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
         nmeta = load_words(g);
         nmeta2 = load_words(g + GSTEP);
     };
+    /* SRC_XR (config 2): the next granule's spectra (lane: lines lane + 64 i
+     * of both channels) and block types (lanes 0..3: bt0, bt1, mixed0,
+     * mixed1) are loaded one granule ahead, like is[] on the decode path;
+     * granules past F read as zero (buffer range). */
+    float nxr[2][9];
+    uint32_t nbt = 0u;
+    const __amdgpu_buffer_rsrc_t r_xr = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(xr_in + (SRC_XR ? (size_t)s * F * 2 * xr_nch * 576 : 0)), 0, SRC_XR ? F * 2 * xr_nch * 2304 : 0,
+        0x00020000);
+    auto load_xr = [&](int g) {
+        const int lo = opaque(lane * 4);
+#pragma unroll
+        for (int c = 0; c < 2; c++)
+#pragma unroll
+            for (int i = 0; i < 9; i++)
+                nxr[c][i] = c < xr_nch ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                                      r_xr, lo + 256 * i + 2304 * c, g * xr_nch * 2304, 0))
+                                       : 0.f;
+        const int q = lane & 1;
+        const size_t ux = ((size_t)s * F * 2 + g) * xr_nch + q;
+        nbt = 0u;
+        if (lane < 4 && q < xr_nch && g < 2 * F) nbt = lane < 2 ? xr_bt[ux] : xr_mixed[ux];
+    };
+    if (SRC_XR) load_xr(2 * fw);
     if (!SRC_XR) {
         prefetch_full(2 * fw);
         /* explicit drain on the entry path, so the compiler's wait before
@@ -346,20 +372,26 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
             int bt0, mx0, bt1 = 0, mx1 = 0;
             /* ---------------- phase Q: requantise + stereo -> LDS ---------- */
             if (SRC_XR) {
-                const size_t ux = (fr * 2 + gr) * (size_t)nch;
-                bt0 = xr_bt[ux];
-                mx0 = bt0 == 2 ? xr_mixed[ux] : 0;
+                (void)fr;
+                float cx[2][9];
+#pragma unroll
+                for (int c = 0; c < 2; c++)
+#pragma unroll
+                    for (int i = 0; i < 9; i++) cx[c][i] = nxr[c][i];
+                bt0 = __builtin_amdgcn_readlane((int)nbt, 0);
+                mx0 = bt0 == 2 ? __builtin_amdgcn_readlane((int)nbt, 2) : 0;
                 if (nch == 2) {
-                    bt1 = xr_bt[ux + 1];
-                    mx1 = bt1 == 2 ? xr_mixed[ux + 1] : 0;
+                    bt1 = __builtin_amdgcn_readlane((int)nbt, 1);
+                    mx1 = bt1 == 2 ? __builtin_amdgcn_readlane((int)nbt, 3) : 0;
                 }
+                if (f + 1 < f1 || gr == 0) load_xr(2 * f + gr + 1); /* next granule, in flight through I, M, W */
                 const uint16_t *lv0 = (const uint16_t *)lvar[bt0 == 2 ? (mx0 ? 2 : 1) : 0];
                 const uint16_t *lv1 = (const uint16_t *)lvar[bt1 == 2 ? (mx1 ? 2 : 1) : 0];
 #pragma unroll
                 for (int i = 0; i < 9; i++) {
                     const int l = lane + 64 * i;
-                    sBuf[lv0[l] >> 6] = xr_in[ux * 576 + l];
-                    if (nch == 2) sBuf[576 + (lv1[l] >> 6)] = xr_in[(ux + 1) * 576 + l];
+                    sBuf[lv0[l] >> 6] = cx[0][i];
+                    if (nch == 2) sBuf[576 + (lv1[l] >> 6)] = cx[1][i];
                 }
             } else {
                 uint32_t cis[2][5];
