@@ -55,9 +55,12 @@ __device__ __forceinline__ uint32_t side_unit_bit(int nch, int gr, int ch, bool 
 /* serial header walk costs about one load latency per frame.              */
 /* ------------------------------------------------------------------------ */
 struct HdrWin {        /* 64 bytes at a stream position, spread over lanes 0..15 */
-    uint32_t le;       /* lane i: little-endian dword at stream offset pos - mis + 4 i */
+    uint32_t raw;      /* lane i: little-endian dword at stream offset pos - mis + 4 i */
+    uint32_t keep;     /* byte mask of raw inside the stream (applied at use: the   */
+                       /* load stays in flight until the window is read)           */
     uint32_t pos;
     uint32_t mis;      /* (address of stream byte pos) & 3: the dwords are aligned  */
+    __device__ __forceinline__ uint32_t le() const { return raw & keep; }
 };
 
 /* Every load is an ALIGNED dword that holds at least one byte of the stream
@@ -68,27 +71,23 @@ __device__ __forceinline__ HdrWin load_win(const uint8_t *p0, uint32_t len, uint
     w.pos = pos;
     w.mis = (uint32_t)((uintptr_t)(p0 + pos) & 3u);
     const int64_t a = (int64_t)pos - (int64_t)w.mis + 4 * lane; /* stream offset of the lane's dword */
-    uint32_t v = 0u;
-    if (lane < 16 && a < (int64_t)len) {
-        v = *(const uint32_t *)(p0 + a);
-        const int64_t over = a + 4 - (int64_t)len; /* bytes past the stream end */
-        if (over > 0) v &= 0xFFFFFFFFu >> (8 * over);
-    }
-    w.le = v;
+    const int64_t over = a + 4 - (int64_t)len;                   /* bytes past the stream end */
+    w.keep = (lane >= 16 || over >= 4) ? 0u : over > 0 ? 0xFFFFFFFFu >> (8 * over) : 0xFFFFFFFFu;
+    w.raw = w.keep ? *(const uint32_t *)(p0 + a) : 0u;
     return w;
 }
 
 /* byte k of the window (uniform k; k + mis < 64) */
 __device__ __forceinline__ uint32_t win_byte(const HdrWin &w, uint32_t k) {
     const uint32_t i = k + w.mis;
-    const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)w.le, (int)(i >> 2));
+    const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)w.le(), (int)(i >> 2));
     return (d >> (8 * (i & 3u))) & 0xFFu;
 }
 
 /* 64 bits of the window's big-endian bit string starting at bit b of the
  * window's first dword (stream byte pos - mis) -- per lane b (lane-varying) */
 __device__ __forceinline__ uint64_t win_bits64(const HdrWin &w, uint32_t b) {
-    const uint32_t be = __builtin_bswap32(w.le);
+    const uint32_t be = __builtin_bswap32(w.le());
     const int wi = (int)(b >> 5);
     const uint32_t x0 = (uint32_t)__shfl((int)be, wi), x1 = (uint32_t)__shfl((int)be, wi + 1),
                    x2 = (uint32_t)__shfl((int)be, wi + 2);
@@ -114,7 +113,7 @@ __device__ bool crc16_ok(const HdrWin &w, uint32_t side_bytes, int lane) {
     /* message byte i sits at frame byte 2 + i (header) or 4 + i (side info);
      * the cross-lane read runs in every lane (all source lanes active) */
     const uint32_t k = (uint32_t)(lane < 34 ? lane : 33) + (lane < 2 ? 2u : 4u) + w.mis;
-    const uint32_t d = (uint32_t)__shfl((int)w.le, (int)(k >> 2));
+    const uint32_t d = (uint32_t)__shfl((int)w.le(), (int)(k >> 2));
     if ((uint32_t)lane < n) {
         uint32_t c = ((d >> (8u * (k & 3u))) & 0xFFu) << 8;
 #pragma unroll
@@ -330,13 +329,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                 cur = len;
             }
         }
-        /* next frame's header window in flight while this payload copies */
-        if (cur + 4 <= len && f + 1 < F) w = load_win(p0, len, cur, lane);
         if (lane == 0) {
             rec[fi] = r;
             if (infos) infos[fi] = inf;
         }
         if (lane < 4) sideu[fi * 4 + lane] = sw;
+        /* next frame's header window in flight while this payload copies
+         * (issued after the record stores: a store issued behind a pending
+         * load made the compiler drain vmcnt(0) before it, i.e. wait for the
+         * window right here) */
+        if (cur + 4 <= len && f + 1 < F) w = load_win(p0, len, cur, lane);
         if (copy) {
             const uint8_t *src = p0 + src_off;
             const uint32_t Pm = r.payload_md, L = r.payload_avail;
