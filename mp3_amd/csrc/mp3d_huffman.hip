@@ -266,6 +266,9 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
             const int u = ubase + (int)order16[64 * rd + lane];
             const int fr = u >> 2, gr = (u >> 1) & 1, ch = u & 1;
             bool valid = u < n_units;
+            /* the stream's md base, loaded together with the frame record (not
+             * after it: one memory latency less per round) */
+            const uint64_t mdo = md_off[(valid ? fr : 0) / F];
             FrameRec r;
             uint64_t sq[4] = {0, 0, 0, 0};
             if (valid) {
@@ -305,7 +308,7 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                 if (lane >= o) incl += t;
             }
             const uint32_t off = incl - len;
-            const uint32_t *src = (const uint32_t *)(md + (dec ? md_off[fr / F] : 0)) + w0;
+            const uint32_t *src = (const uint32_t *)(md + (dec ? mdo : 0)) + w0;
 
             bool pending = dec;
             while (__ballot(pending)) {
