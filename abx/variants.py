@@ -43,6 +43,7 @@ VARS = {
     "XPF4": [],
     "DM2": [],
     "H2": [],
+    "W9": [],
     "XPF3": [("amdgpu_waves_per_eu(SRC_XR ? 4 : 3, 8)", "amdgpu_waves_per_eu(3, 8)")],
     # r02: k_demux without the waves_per_eu(8, 8) attribute of commit 315cc86
     "DMW0": [("__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) k_demux(",

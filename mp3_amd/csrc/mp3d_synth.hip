@@ -741,21 +741,29 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                 /* two output slots (2 tp, 2 tp + 1) at once: packed FMAs
                  * (v_pk_fma_f32, tap broadcast), half the VALU issues of the
                  * scalar form; the same fma order per slot, so bit-identical */
-                auto out2 = [&](int tp) {
-                    f32x2 o = {0.f, 0.f};
+                /* all 9 slot pairs accumulate side by side (tap i outer, slot
+                 * pair inner): 9 independent packed-FMA chains.  Written as one
+                 * chain per slot pair, the compiler emitted them back to back
+                 * into one register pair -- a 144-long dependent chain per
+                 * granule.  Same fma order per slot, so bit-identical. */
+                f32x2 acc[9];
 #pragma unroll
-                    for (int i = 0; i < 8; i++) {
+                for (int tp = 0; tp < 9; tp++) acc[tp] = (f32x2){0.f, 0.f};
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+#pragma unroll
+                    for (int tp = 0; tp < 9; tp++) {
                         const int ka = 2 * tp - 2 * i, kb = ka - 1;
                         f32x2 va, vb;
                         va.x = ka >= 0 ? xa[ka] : ha[ka + 14];
                         va.y = ka + 1 >= 0 ? xa[ka + 1] : ha[ka + 15];
                         vb.x = kb >= 0 ? xb[kb] : hb[kb + 15];
                         vb.y = kb + 1 >= 0 ? xb[kb + 1] : hb[kb + 16];
-                        o = __builtin_elementwise_fma((f32x2){Dw[2 * i], Dw[2 * i]}, va, o);
-                        o = __builtin_elementwise_fma((f32x2){Dw[2 * i + 1], Dw[2 * i + 1]}, vb, o);
+                        acc[tp] = __builtin_elementwise_fma((f32x2){Dw[2 * i], Dw[2 * i]}, va, acc[tp]);
+                        acc[tp] = __builtin_elementwise_fma((f32x2){Dw[2 * i + 1], Dw[2 * i + 1]}, vb, acc[tp]);
                     }
-                    return o;
-                };
+                }
+                auto out2 = [&](int tp) { return acc[tp]; };
                 auto to_pcm = [&](float v) {
                     const float p = rintf(v * 32768.f);
                     return (int)fminf(fmaxf(p, -32768.f), 32767.f);
