@@ -44,6 +44,23 @@ VARS = {
     "DM2": [],
     "H2": [],
     "W9": [],
+    "Q2": [],
+    # r02 sensitivity probes (same output): +64 dependent-free VALU per granule in k_synth phase W,
+    # +8 VALU per codeword in the Huffman big_values loop
+    "SV64": [("                auto out2 = [&](int tp) { return acc[tp]; };",
+              "                { float d0 = acc[0].x, d1 = acc[1].x, d2 = acc[2].x, d3 = acc[3].x;\n"
+              "#pragma unroll\n                  for (int q = 0; q < 16; q++) { __asm__ volatile(\"v_add_f32 %0, %0, %0\\n v_add_f32 %1, %1, %1\\n v_add_f32 %2, %2, %2\\n v_add_f32 %3, %3, %3\" : \"+v\"(d0), \"+v\"(d1), \"+v\"(d2), \"+v\"(d3)); }\n"
+              "                  if (d0 == 1.2345f && d1 == d2 && d3 == 0.5f) acc[8].y += 1e-30f; }\n"
+              "                auto out2 = [&](int tp) { return acc[tp]; };")],
+    "HV8": [("                    for (; k < bv2; k += 2) {",
+             "                    uint32_t hv_dummy = 0u;\n                    for (; k < bv2; k += 2) {"),
+            ("                        const uint32_t e = s_lut[i2];",
+             "                        const uint32_t e = s_lut[i2];\n"
+             "                        { uint32_t d0 = k, d1 = k + 1u;\n"
+             "                          __asm__ volatile(\"v_add_u32 %0, %0, %0\\n v_add_u32 %1, %1, %1\\n v_add_u32 %0, %0, %0\\n v_add_u32 %1, %1, %1\\n v_add_u32 %0, %0, %0\\n v_add_u32 %1, %1, %1\\n v_add_u32 %0, %0, %0\\n v_add_u32 %1, %1, %1\" : \"+v\"(d0), \"+v\"(d1));\n"
+             "                          hv_dummy ^= d0 ^ d1; }"),
+            ("                    m.used_bits = (uint16_t)(pos - start - seg);",
+             "                    m.used_bits = (uint16_t)(pos - start - seg) | (hv_dummy == 0x9E3779B9u ? 0x8000u : 0u);")],
     "XPF3": [("amdgpu_waves_per_eu(SRC_XR ? 4 : 3, 8)", "amdgpu_waves_per_eu(3, 8)")],
     # r02: k_demux without the waves_per_eu(8, 8) attribute of commit 315cc86
     "DMW0": [("__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) k_demux(",

@@ -292,19 +292,28 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
             }
         }
     };
-    /* steady state: is[g] masked by nmeta2's nz_end (granule g), then shift */
-    auto prefetch = [&](int g) {
-        const int nz0 = __builtin_amdgcn_readlane((int)nmeta2, 12) & 0xFFFF;
-        const int nz1 = __builtin_amdgcn_readlane((int)nmeta2, MW + 12) & 0xFFFF;
+    /* is[g] masked by granule g's nz_end from its meta words m (channel 1
+     * only in a stereo frame: FrameRec.nch, lane 37): every line >= nz_end
+     * then reads as 0 in registers, so phase Q needs no rzero mask */
+    auto load_is_masked = [&](int g, uint32_t m) {
+        const bool st = ((uint32_t)__builtin_amdgcn_readlane((int)m, 37) >> 24) == 2u;
+        const int nz0 = __builtin_amdgcn_readlane((int)m, 12) & 0xFFFF;
+        const int nz1 = st ? __builtin_amdgcn_readlane((int)m, MW + 12) & 0xFFFF : 0;
         load_is(g, nz0, nz1);
+    };
+    /* steady state: is[g] masked by nmeta2 (granule g's words), then shift */
+    auto prefetch = [&](int g) {
+        load_is_masked(g, nmeta2);
         nmeta = nmeta2;
         nmeta2 = load_words(g + GSTEP);
     };
-    /* entry and after a frame without audio: unmasked, then drained */
+    /* entry and after a frame without audio: the words first, drained, then
+     * the masked is[] (off the common path) */
     auto prefetch_full = [&](int g) {
-        load_is(g, 576, 576);
         nmeta = load_words(g);
         nmeta2 = load_words(g + GSTEP);
+        WAIT_VMCNT0();
+        load_is_masked(g, nmeta);
     };
     /* SRC_XR (config 2): the next granule's spectra (lane: lines lane + 64 i
      * of both channels) and block types (lanes 0..3: bt0, bt1, mixed0,
@@ -442,8 +451,12 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                     if (nch == 2) Wd.scale[1][lane] = band_scale(m10b, m11b, MW);
                 }
                 wave_sync();
-                const int nz[2] = {(int)(m12a & 0xFFFFu), nch == 2 ? (int)(m12b & 0xFFFFu) : 0};
-                float xv[2][10];
+                (void)m12a;
+                (void)m12b;
+                /* line pairs (2 i + e) kept as register pairs: the long-block
+                 * scatter stores them with one ds_write_b64, no moves */
+                f32x2 xp[2][5];
+#define XV(c, k) xp[c][(k) >> 1][(k) & 1]
                 bool big = false; /* some |is| >= 256 (escape) in this lane */
 #pragma unroll
                 for (int i = 0; i < 5; i++) {
@@ -455,12 +468,14 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
 #pragma unroll
                         for (int e = 0; e < 2; e++) {
                             const int l = l0 + e;
-                            int v = (int)(int16_t)(e ? (cis[c][i] >> 16) : (cis[c][i] & 0xFFFFu));
-                            v = l < nz[c] ? v : 0; /* rzero lines are not stored by k_huffman */
+                            (void)l;
+                            /* lines >= nz_end arrive as 0 (load_is_masked) */
+                            const int v = (int)(int16_t)(e ? (cis[c][i] >> 16) : (cis[c][i] & 0xFFFFu));
                             const int a = v < 0 ? -v : v;
                             big |= a >= 256;
                             const float mag = T.p43[a & 255] * Wd.scale[c][(e ? tv2 >> 16 : tv2) & 63u];
-                            xv[c][2 * i + e] = v < 0 ? -mag : mag;
+                            /* sign of is onto |is|^(4/3) scale (>= 0): the int's sign bit */
+                            XV(c, 2 * i + e) = __uint_as_float(__float_as_uint(mag) | ((uint32_t)v & 0x80000000u));
                         }
                     }
                 }
@@ -475,13 +490,12 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                         for (int c = 0; c < 2; c++) {
 #pragma unroll
                             for (int e = 0; e < 2; e++) {
-                                int v = (int)(int16_t)(e ? (cis[c][i] >> 16) : (cis[c][i] & 0xFFFFu));
-                                v = l0 + e < nz[c] ? v : 0;
+                                const int v = (int)(int16_t)(e ? (cis[c][i] >> 16) : (cis[c][i] & 0xFFFFu));
                                 const int a = v < 0 ? -v : v;
                                 if (a >= 256) {
                                     const uint32_t tv2 = lvar[var[c]][l0 >> 1];
                                     const float mag = pow43_big(a) * Wd.scale[c][(e ? tv2 >> 16 : tv2) & 63u];
-                                    xv[c][2 * i + e] = v < 0 ? -mag : mag;
+                                    XV(c, 2 * i + e) = v < 0 ? -mag : mag;
                                 }
                             }
                         }
@@ -500,8 +514,8 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                     for (int i = 0; i < 5; i++) {
                         const int l0 = 2 * lane + 128 * i;
                         const uint32_t tv2 = (i < 4 || lane < 32) ? lvar[var[1]][l0 >> 1] : 0u;
-                        if (xv[1][2 * i] != 0.f) nzR |= 1ull << (tv2 & 63u);
-                        if (xv[1][2 * i + 1] != 0.f) nzR |= 1ull << ((tv2 >> 16) & 63u);
+                        if (XV(1, 2 * i) != 0.f) nzR |= 1ull << (tv2 & 63u);
+                        if (XV(1, 2 * i + 1) != 0.f) nzR |= 1ull << ((tv2 >> 16) & 63u);
                     }
 #pragma unroll
                     for (int o = 1; o < 64; o <<= 1) nzR |= __shfl_xor(nzR, o);
@@ -536,23 +550,23 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
 #pragma unroll
                         for (int e = 0; e < 2; e++) {
                             const int k = 2 * i + e;
-                            const float lv = xv[0][k], rv = xv[1][k];
+                            const float lv = XV(0, k), rv = XV(1, k);
                             const int ipl = Wd.is[(e ? tv2 >> 16 : tv2) & 63u];
                             if (ipl != 0xFF) {
-                                xv[0][k] = lv * T.isr[ipl][0];
-                                xv[1][k] = lv * T.isr[ipl][1];
+                                XV(0, k) = lv * T.isr[ipl][0];
+                                XV(1, k) = lv * T.isr[ipl][1];
                             } else if (mext & 2) {
-                                xv[0][k] = (lv + rv) * isq;
-                                xv[1][k] = (lv - rv) * isq;
+                                XV(0, k) = (lv + rv) * isq;
+                                XV(1, k) = (lv - rv) * isq;
                             }
                         }
                     }
                 } else if (ms_fold) {
 #pragma unroll
                     for (int k = 0; k < 10; k++) {
-                        const float lv = xv[0][k], rv = xv[1][k];
-                        xv[0][k] = lv + rv;
-                        xv[1][k] = lv - rv;
+                        const float lv = XV(0, k), rv = XV(1, k);
+                        XV(0, k) = lv + rv;
+                        XV(1, k) = lv - rv;
                     }
                 }
                 /* the next granule's loads fly during phases I, M, W (issued
@@ -567,11 +581,11 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                         for (int c = 0; c < 2; c++) {
                             if (c < nch) {
                                 if (var[c] == 0) { /* long block: in place, one 8-B store */
-                                    *(float2 *)&sBuf[576 * c + l0] = make_float2(xv[c][2 * i], xv[c][2 * i + 1]);
+                                    *(f32x2 *)&sBuf[576 * c + l0] = xp[c][i];
                                 } else {
                                     const uint32_t tv2 = lvar[var[c]][l0 >> 1];
-                                    sBuf[576 * c + (tv2 >> 6 & 1023u)] = xv[c][2 * i];
-                                    sBuf[576 * c + (tv2 >> 22)] = xv[c][2 * i + 1];
+                                    sBuf[576 * c + (tv2 >> 6 & 1023u)] = XV(c, 2 * i);
+                                    sBuf[576 * c + (tv2 >> 22)] = XV(c, 2 * i + 1);
                                 }
                             }
                         }
@@ -579,6 +593,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                 }
             }
             wave_sync();
+#undef XV
             /* ---------------- phase I: alias + IMDCT + overlap ------------ */
             const int bt = ch ? bt1 : bt0, mixed = ch ? mx1 : mx0;
             float o18[18];
@@ -796,13 +811,22 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                     }
                 } else if (nch == 2) {
                     const int vo = opaque((sb + 32 * ch) * 4);
+                    /* rint(x 32768) -> int32 (v_cvt_i32_f32 saturates out-of-range
+                     * floats), then v_cvt_pk_i16_i32 saturates to int16 and packs
+                     * (L, R): clamp(rint(x 32768)) as before, 2 VALU less per pair */
+                    auto to_i32 = [&](float v) {
+                        int r;
+                        __asm__("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(rintf(v * 32768.f)));
+                        return r;
+                    };
 #pragma unroll
                     for (int tp = 0; tp < 9; tp++) {
                         const f32x2 o = out2(tp);
-                        const int p0 = to_pcm(o.x), p1 = to_pcm(o.y);
+                        const int p0 = to_i32(o.x), p1 = to_i32(o.y);
                         const auto r = __builtin_amdgcn_permlane32_swap(p0, p1, false, false);
-                        __builtin_amdgcn_raw_buffer_store_b32(((uint32_t)r[0] & 0xFFFFu) | ((uint32_t)r[1] << 16),
-                                                              r_pcm, vo + 256 * tp, so, 0);
+                        __builtin_amdgcn_raw_buffer_store_b32(
+                            __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16((int)r[0], (int)r[1])), r_pcm,
+                            vo + 256 * tp, so, 0);
                     }
                 } else {
                     const int vo = opaque(sb * 2);

@@ -74,3 +74,20 @@ def test_c2_segments_bit_identical_across_calls():
         ref = _oracle_pcm(xr, bt, mx, s, 2 * F)
         g = seq[s, :, :1152 * NCH].reshape(2 * F, 1152, NCH)
         assert np.abs(g.astype(np.int32) - ref.astype(np.int32)).max() <= 1, s
+
+
+def test_clipping_saturates_like_the_oracle():
+    """Spectra scaled far past full scale: int16 PCM saturates to -32768 / 32767
+    exactly where the oracle's clamp(rint(x 32768)) does (the decode paths
+    convert with saturating int32 / packed-int16 conversions)."""
+    n, F = 8, 6
+    xr, bt, mx = _gen.c2_spectra(n, F, NCH, seed=99)
+    xr = (xr * np.float32(40.0)).astype(np.float32)
+    pcm = mp3_amd.BatchDecoder(n, F).synth_only(xr, bt, mx, NCH, 44100)
+    clipped = 0
+    for s in range(n):
+        ref = _oracle_pcm(xr, bt, mx, s, F)
+        got = pcm[s, :, :1152 * NCH].reshape(F, 1152, NCH)
+        assert np.abs(got.astype(np.int32) - ref.astype(np.int32)).max() <= 1, s
+        clipped += int((np.abs(ref.astype(np.int32)) >= 32767).sum())
+    assert clipped > 1000
