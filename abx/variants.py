@@ -45,6 +45,7 @@ VARS = {
     "H2": [],
     "W9": [],
     "Q2": [],
+    "Q3": [],
     # r02 sensitivity probes (same output): +64 dependent-free VALU per granule in k_synth phase W,
     # +8 VALU per codeword in the Huffman big_values loop
     "SV64": [("                auto out2 = [&](int tp) { return acc[tp]; };",

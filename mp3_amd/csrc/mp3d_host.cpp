@@ -163,10 +163,18 @@ static void build_tables(DevTables &t) {
             }
             p += 3 * w;
         }
-        for (int i = 0; i < 576; i++) {
-            t.lvar[sr][0][i] = (uint16_t)(lb[i] | i << 6);
-            t.lvar[sr][1][i] = (uint16_t)(sidx[i] | sdst[i] << 6);
-            t.lvar[sr][2][i] = i < mix_end ? t.lvar[sr][0][i] : t.lvar[sr][1][i];
+        for (int k = 0; k < 288; k++) {
+            for (int v = 0; v < 3; v++) {
+                int band[2], pos[2];
+                for (int e = 0; e < 2; e++) {
+                    const int i = 2 * k + e;
+                    const bool lng = v == 0 || (v == 2 && i < mix_end);
+                    band[e] = lng ? lb[i] : sidx[i];
+                    pos[e] = lng ? i : sdst[i];
+                }
+                if (band[0] != band[1]) abort(); /* odd band width: impossible (ISO tables) */
+                t.lpair[sr][v][k] = (uint32_t)(4 * band[0]) | (uint32_t)pos[0] << 8 | (uint32_t)pos[1] << 18;
+            }
         }
     }
     build_huffman_lut(t);

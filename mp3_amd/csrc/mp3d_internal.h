@@ -104,9 +104,11 @@ struct DevTables {
     float dct_c[32][32];       /* C[m][sb] = cos(m (2 sb + 1) pi / 64)  */
     float dwin[32][16];        /* per output j: signed window taps       */
     /* per (sample-rate index 0..8, block variant long / short / mixed, bitstream
-     * line): bits 0..5 scale index (long band b, or 22 + 3 b + w for short
-     * band b window w), bits 6..15 position after the short reorder      */
-    uint16_t lvar[9][3][576];
+     * line pair 2k, 2k + 1): bits 0..7 = 4 x scale index of the pair (long
+     * band b, or 22 + 3 b + w for short band b window w; every band width is
+     * even, so a pair never straddles two bands), bits 8..17 / 18..27 the
+     * two lines' positions after the short reorder                       */
+    uint32_t lpair[9][3][288];
     uint8_t win_a[32];         /* V[j] = sgn * X[a[j]]                   */
     uint8_t win_b[32];         /* V[32 + j] = sgn * X[b[j]]              */
     uint16_t lut[MP3D_LUT_MAX];

@@ -139,26 +139,30 @@ __device__ __forceinline__ float pow43_big(int a) {
 }
 
 template <bool LSF> struct SynShared { /* read-only, one copy per workgroup        */
-    /* tab->lvar (u16 pairs) [rate][variant] of the variant's family: MPEG-1
+    /* tab->lpair [rate][variant][line pair] of the variant's family: MPEG-1
      * rates 0..2, or the six LSF rates 3..8                                */
-    uint32_t lvar[LSF ? 6 : 3][3][288];
+    uint32_t lpair[LSF ? 6 : 3][3][288];
     float ce[16][16], co[16][16];    /* matrixing A: C[2m][i], C[2m+1][i], i < 16  */
     float dw[32][16];                /* window taps per output j                   */
-    float p43[256];                  /* |is|^(4/3) for |is| < 256                  */
+    float p43s[512];                 /* sign(k - 256) |k - 256|^(4/3), k < 512     */
     float w36[4][36];                /* long-block windows (x IMDCT output scale)  */
     float isr[LSF ? 32 : 7][2];      /* intensity ratios: MPEG-1 [is_pos], LSF      */
                                      /* [intensity_scale * 16 + is_pos]            */
 };
-struct SynWave {                     /* one per wave (stream)                      */
+struct __attribute__((aligned(256))) SynWave { /* one per wave (stream)       */
+    /* 2^(q/4) per (ch, band idx): long b | 22 + 3 b + w.  256-B aligned rows,
+     * so a line pair's scale address is base | (lpair & 0xFC): one VALU op */
+    float scale[2][64];
     float buf[SYN_BUF];              /* xr -> S -> X hand-offs                     */
-    float scale[2][64];              /* 2^(q/4) per (ch, band idx): long b | 22 + 3 b + w */
     UnitMeta m[2];
     uint8_t is[64];                  /* intensity position per right band idx, 0xFF none */
 };
+typedef __attribute__((address_space(3))) const float lds_cf32;
 
 #define WAIT_VMCNT0() __builtin_amdgcn_s_waitcnt(0x0F70) /* vmcnt(0), other counters free */
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 
 template <bool SRC_XR, bool F32, bool LSF>
 /* 3 waves / SIMD (168 VGPRs).  The synth-only entry would fit 4 waves /
@@ -172,7 +176,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
         const DevTables *__restrict__ tab, StreamState *__restrict__ st, void *__restrict__ pcm, int n_streams,
         int F, int xr_nch, int xr_sr, int seg_len, float *__restrict__ st_tail) {
     __shared__ __attribute__((aligned(16))) SynShared<LSF> T;
-    __shared__ __attribute__((aligned(16))) SynWave Wv[SYN_WAVES];
+    __shared__ SynWave Wv[SYN_WAVES];
     constexpr int NRATE = LSF ? 6 : 3;
     if (!SRC_XR) {
         /* one variant per MPEG family (StreamState.kind, fixed by k_demux):
@@ -190,13 +194,14 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
     {
         const int tid = threadIdx.x;
         for (int i = tid; i < NRATE * 3 * 288; i += 64 * SYN_WAVES)
-            (&T.lvar[0][0][0])[i] = ((const uint32_t *)&tab->lvar[LSF ? 3 : 0][0][0])[i];
+            (&T.lpair[0][0][0])[i] = (&tab->lpair[LSF ? 3 : 0][0][0])[i];
         for (int i = tid; i < 256; i += 64 * SYN_WAVES) {
             const int r = i >> 4, c = i & 15;
             T.ce[r][c] = tab->dct_c[2 * r][c];
             T.co[r][c] = tab->dct_c[2 * r + 1][c];
-            T.p43[i] = tab->pow43[i];
         }
+        for (int i = tid; i < 512; i += 64 * SYN_WAVES)
+            T.p43s[i] = i >= 256 ? tab->pow43[i - 256] : -tab->pow43[256 - i];
         for (int i = tid; i < 32 * 16; i += 64 * SYN_WAVES) (&T.dw[0][0])[i] = (&tab->dwin[0][0])[i];
         for (int i = tid; i < 4 * 36; i += 64 * SYN_WAVES) (&T.w36[0][0])[i] = (&c_win36[0][0])[i];
         if (LSF) {
@@ -315,24 +320,26 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
         WAIT_VMCNT0();
         load_is_masked(g, nmeta);
     };
-    /* SRC_XR (config 2): the next granule's spectra (lane: lines lane + 64 i
-     * of both channels) and block types (lanes 0..3: bt0, bt1, mixed0,
-     * mixed1) are loaded one granule ahead, like is[] on the decode path;
-     * granules past F read as zero (buffer range). */
-    float nxr[2][9];
+    /* SRC_XR (config 2): the next granule's spectra (lane: line pairs
+     * lane + 64 i of both channels, as is[] on the decode path) and block
+     * types (lanes 0..3: bt0, bt1, mixed0, mixed1) are loaded one granule
+     * ahead; granules past F read as zero (buffer range). */
+    f32x2 nxr[2][5];
     uint32_t nbt = 0u;
     const __amdgpu_buffer_rsrc_t r_xr = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(xr_in + (SRC_XR ? (size_t)s * F * 2 * xr_nch * 576 : 0)), 0, SRC_XR ? F * 2 * xr_nch * 2304 : 0,
         0x00020000);
     auto load_xr = [&](int g) {
-        const int lo = opaque(lane * 4);
+        const int lo = opaque(lane * 8);
 #pragma unroll
         for (int c = 0; c < 2; c++)
 #pragma unroll
-            for (int i = 0; i < 9; i++)
-                nxr[c][i] = c < xr_nch ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                                      r_xr, lo + 256 * i + 2304 * c, g * xr_nch * 2304, 0))
-                                       : 0.f;
+            for (int i = 0; i < 5; i++) {
+                nxr[c][i] = (f32x2){0.f, 0.f};
+                if (c < xr_nch && (i < 4 || lane < 32))
+                    nxr[c][i] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                              r_xr, lo + 512 * i + 2304 * c, g * xr_nch * 2304, 0));
+            }
         const int q = lane & 1;
         const size_t ux = ((size_t)s * F * 2 + g) * xr_nch + q;
         nbt = 0u;
@@ -371,7 +378,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
             mext = (int)(r5 >> 20) & 3;
         }
         const bool active = ch < nch;
-        const uint32_t(*lvar)[288] = T.lvar[sr];
+        const uint32_t(*lpair)[288] = T.lpair[sr];
         for (int gr = 0; gr < (LSF ? 1 : 2); gr++) { /* LSF: one granule per frame */
             /* lane-derived indices are re-derived from an opaque copy each
              * granule so they are not hoisted and held live across the loop */
@@ -382,11 +389,11 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
             /* ---------------- phase Q: requantise + stereo -> LDS ---------- */
             if (SRC_XR) {
                 (void)fr;
-                float cx[2][9];
+                f32x2 cx[2][5];
 #pragma unroll
                 for (int c = 0; c < 2; c++)
 #pragma unroll
-                    for (int i = 0; i < 9; i++) cx[c][i] = nxr[c][i];
+                    for (int i = 0; i < 5; i++) cx[c][i] = nxr[c][i];
                 bt0 = __builtin_amdgcn_readlane((int)nbt, 0);
                 mx0 = bt0 == 2 ? __builtin_amdgcn_readlane((int)nbt, 2) : 0;
                 if (nch == 2) {
@@ -394,13 +401,24 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                     mx1 = bt1 == 2 ? __builtin_amdgcn_readlane((int)nbt, 3) : 0;
                 }
                 if (f + 1 < f1 || gr == 0) load_xr(2 * f + gr + 1); /* next granule, in flight through I, M, W */
-                const uint16_t *lv0 = (const uint16_t *)lvar[bt0 == 2 ? (mx0 ? 2 : 1) : 0];
-                const uint16_t *lv1 = (const uint16_t *)lvar[bt1 == 2 ? (mx1 ? 2 : 1) : 0];
+                const int xv[2] = {bt0 == 2 ? (mx0 ? 2 : 1) : 0, bt1 == 2 ? (mx1 ? 2 : 1) : 0};
 #pragma unroll
-                for (int i = 0; i < 9; i++) {
-                    const int l = lane + 64 * i;
-                    sBuf[lv0[l] >> 6] = cx[0][i];
-                    if (nch == 2) sBuf[576 + (lv1[l] >> 6)] = cx[1][i];
+                for (int i = 0; i < 5; i++) {
+                    if (i < 4 || lane < 32) {
+                        const int k = lane + 64 * i;
+#pragma unroll
+                        for (int c = 0; c < 2; c++) {
+                            if (c < nch) {
+                                if (xv[c] == 0) {
+                                    *(f32x2 *)&sBuf[576 * c + 2 * k] = cx[c][i];
+                                } else {
+                                    const uint32_t tv2 = lpair[xv[c]][k];
+                                    sBuf[576 * c + ((tv2 >> 8) & 1023u)] = cx[c][i][0];
+                                    sBuf[576 * c + ((tv2 >> 18) & 1023u)] = cx[c][i][1];
+                                }
+                            }
+                        }
+                    }
                 }
             } else {
                 uint32_t cis[2][5];
@@ -457,29 +475,34 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                  * scatter stores them with one ds_write_b64, no moves */
                 f32x2 xp[2][5];
 #define XV(c, k) xp[c][(k) >> 1][(k) & 1]
-                bool big = false; /* some |is| >= 256 (escape) in this lane */
+                /* per is[] word (two int16 lines): t = 4 (both halves + 256),
+                 * one packed u16 op, is the byte offset into the signed table
+                 * p43s; a half outside 0 .. 2047 (is >= 256 or < -256) is an
+                 * escape, collected over the words in bigacc and patched
+                 * below.  Both lines of a pair share one band (every long and
+                 * short band width is even, tests/test_tables.py): one scale
+                 * read per pair. */
+                uint32_t bigacc = 0u;
+                const uint32_t sc_base[2] = {(uint32_t)(uintptr_t)(lds_cf32 *)&Wd.scale[0][0],
+                                             (uint32_t)(uintptr_t)(lds_cf32 *)&Wd.scale[1][0]};
 #pragma unroll
                 for (int i = 0; i < 5; i++) {
                     const int l0 = 2 * lane + 128 * i;
                     const bool ok = i < 4 || lane < 32;
 #pragma unroll
                     for (int c = 0; c < 2; c++) {
-                        const uint32_t tv2 = ok ? lvar[var[c]][l0 >> 1] : 0u;
-#pragma unroll
-                        for (int e = 0; e < 2; e++) {
-                            const int l = l0 + e;
-                            (void)l;
-                            /* lines >= nz_end arrive as 0 (load_is_masked) */
-                            const int v = (int)(int16_t)(e ? (cis[c][i] >> 16) : (cis[c][i] & 0xFFFFu));
-                            const int a = v < 0 ? -v : v;
-                            big |= a >= 256;
-                            const float mag = T.p43[a & 255] * Wd.scale[c][(e ? tv2 >> 16 : tv2) & 63u];
-                            /* sign of is onto |is|^(4/3) scale (>= 0): the int's sign bit */
-                            XV(c, 2 * i + e) = __uint_as_float(__float_as_uint(mag) | ((uint32_t)v & 0x80000000u));
-                        }
+                        const uint32_t tv2 = ok ? lpair[var[c]][l0 >> 1] : 0u;
+                        /* lines >= nz_end arrive as 0 (load_is_masked) */
+                        const uint32_t t = __builtin_bit_cast(
+                            uint32_t, (__builtin_bit_cast(u16x2, cis[c][i]) << (uint16_t)2) + (u16x2){1024, 1024});
+                        bigacc |= t;
+                        const float sc = *(lds_cf32 *)(uintptr_t)(sc_base[c] | (tv2 & 0xFCu));
+                        const uint8_t *p43b = (const uint8_t *)T.p43s;
+                        XV(c, 2 * i) = *(const float *)(p43b + (t & 0x7FCu)) * sc;
+                        XV(c, 2 * i + 1) = *(const float *)(p43b + ((t >> 16) & 0x7FCu)) * sc;
                     }
                 }
-                if (__ballot(big)) {
+                if (__ballot((bigacc & 0xF800F800u) != 0u)) {
                     /* rare path (escapes |is| >= 256): patch those lines with
                      * the in-register |is|^(4/3); one block, so the loop above
                      * stays branch-free and its LDS reads batch */
@@ -492,9 +515,9 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                             for (int e = 0; e < 2; e++) {
                                 const int v = (int)(int16_t)(e ? (cis[c][i] >> 16) : (cis[c][i] & 0xFFFFu));
                                 const int a = v < 0 ? -v : v;
-                                if (a >= 256) {
-                                    const uint32_t tv2 = lvar[var[c]][l0 >> 1];
-                                    const float mag = pow43_big(a) * Wd.scale[c][(e ? tv2 >> 16 : tv2) & 63u];
+                                if ((uint32_t)(v + 256) >= 512u) {
+                                    const uint32_t tv2 = lpair[var[c]][l0 >> 1];
+                                    const float mag = pow43_big(a) * Wd.scale[c][(tv2 >> 2) & 63u];
                                     XV(c, 2 * i + e) = v < 0 ? -mag : mag;
                                 }
                             }
@@ -513,9 +536,8 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
 #pragma unroll
                     for (int i = 0; i < 5; i++) {
                         const int l0 = 2 * lane + 128 * i;
-                        const uint32_t tv2 = (i < 4 || lane < 32) ? lvar[var[1]][l0 >> 1] : 0u;
-                        if (XV(1, 2 * i) != 0.f) nzR |= 1ull << (tv2 & 63u);
-                        if (XV(1, 2 * i + 1) != 0.f) nzR |= 1ull << ((tv2 >> 16) & 63u);
+                        const uint32_t tv2 = (i < 4 || lane < 32) ? lpair[var[1]][l0 >> 1] : 0u;
+                        if (XV(1, 2 * i) != 0.f || XV(1, 2 * i + 1) != 0.f) nzR |= 1ull << ((tv2 >> 2) & 63u);
                     }
 #pragma unroll
                     for (int o = 1; o < 64; o <<= 1) nzR |= __shfl_xor(nzR, o);
@@ -546,12 +568,12 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
 #pragma unroll
                     for (int i = 0; i < 5; i++) {
                         const int l0 = 2 * lane + 128 * i;
-                        const uint32_t tv2 = (i < 4 || lane < 32) ? lvar[var[1]][l0 >> 1] : 0u;
+                        const uint32_t tv2 = (i < 4 || lane < 32) ? lpair[var[1]][l0 >> 1] : 0u;
+                        const int ipl = Wd.is[(tv2 >> 2) & 63u];
 #pragma unroll
                         for (int e = 0; e < 2; e++) {
                             const int k = 2 * i + e;
                             const float lv = XV(0, k), rv = XV(1, k);
-                            const int ipl = Wd.is[(e ? tv2 >> 16 : tv2) & 63u];
                             if (ipl != 0xFF) {
                                 XV(0, k) = lv * T.isr[ipl][0];
                                 XV(1, k) = lv * T.isr[ipl][1];
@@ -583,9 +605,9 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                                 if (var[c] == 0) { /* long block: in place, one 8-B store */
                                     *(f32x2 *)&sBuf[576 * c + l0] = xp[c][i];
                                 } else {
-                                    const uint32_t tv2 = lvar[var[c]][l0 >> 1];
-                                    sBuf[576 * c + (tv2 >> 6 & 1023u)] = XV(c, 2 * i);
-                                    sBuf[576 * c + (tv2 >> 22)] = XV(c, 2 * i + 1);
+                                    const uint32_t tv2 = lpair[var[c]][l0 >> 1];
+                                    sBuf[576 * c + ((tv2 >> 8) & 1023u)] = XV(c, 2 * i);
+                                    sBuf[576 * c + ((tv2 >> 18) & 1023u)] = XV(c, 2 * i + 1);
                                 }
                             }
                         }

@@ -40,6 +40,9 @@ def test_band_tables():
         nl = 8 if s < 3 else 6
         edge = int(t["MP3D_SFB_LONG_WIDTH"][s][:nl].sum())
         assert edge == int(t["MP3D_SFB_SHORT_WIDTH"][s][:3].sum()) * 3 == (72 if s == 8 else 36)
+        # every band width is even: a bitstream line pair (2k, 2k + 1) never
+        # straddles two bands (k_synth reads one scale per pair, DevTables.lpair)
+        assert not (t["MP3D_SFB_LONG_WIDTH"][s] % 2).any() and not (t["MP3D_SFB_SHORT_WIDTH"][s] % 2).any()
 
 
 def test_lsf_tables():
