@@ -3,14 +3,18 @@
 their output is wrong by construction.  Usage: python abx/variants.py"""
 import os
 import shutil
-import subprocess
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from mp3_amd import _build  # noqa: E402
 
 KERNELS = ["mp3d_demux.hip", "mp3d_huffman.hip", "mp3d_synth.hip"]
 
 
 def variant(name, reps):
     srcs = {k: open("mp3_amd/csrc/" + k).read() for k in KERNELS}
+    flags = [b for a, b in reps if a == "FLAGS"]
+    reps = [(a, b) for a, b in reps if a != "FLAGS"]
     for a, b in reps:
         assert any(a in s for s in srcs.values()), (name, a)
         srcs = {k: s.replace(a, b) for k, s in srcs.items()}
@@ -23,9 +27,7 @@ def variant(name, reps):
     shutil.copy("mp3_amd/csrc/mp3d_host.cpp", d)
     os.makedirs(d + "/../../include", exist_ok=True)
     shutil.copy("include/mp3d.h", d + "/../../include/")
-    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
-                           "-fvisibility=hidden", "-o", "abx/%s.so" % name] + [d + "/" + k for k in KERNELS] +
-                          [d + "/mp3d_host.cpp"])
+    _build.compile_hip(d, "abx/%s.so" % name, d + "/obj", extra=flags)
 
 
 W4H = ("__global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(",
@@ -46,6 +48,8 @@ VARS = {
     "W9": [],
     "Q2": [],
     "Q3": [],
+    "S1": [],
+    "NOSLP": [],  # now the default for mp3d_synth.hip (_build.FILE_FLAGS)
     # r02 sensitivity probes (same output): +64 dependent-free VALU per granule in k_synth phase W,
     # +8 VALU per codeword in the Huffman big_values loop
     "SV64": [("                auto out2 = [&](int tp) { return acc[tp]; };",

@@ -21,16 +21,38 @@ def _stale(target, deps):
     return any(d.stat().st_mtime > t for d in deps)
 
 
+# per-file code generation flags.  k_synth without the SLP vectorizer: its
+# packed pairs are written explicitly (f32x2 window FMAs); the vectorizer's
+# extra pairings cost moves, SGPR spills and +2.7 % k_synth time, while
+# k_demux is 6.7 % faster WITH it (A/B NOSLP, profiles/r02_ab.txt).
+FILE_FLAGS = {"mp3d_synth.hip": ["-fno-slp-vectorize"]}
+HIP_SRCS = ["mp3d_demux.hip", "mp3d_huffman.hip", "mp3d_synth.hip", "mp3d_host.cpp"]
+HIP_HDRS = ["mp3d_internal.h", "mp3d_tables.h", "mp3d_consts.h", "mp3d_device.h", "mp3d_hostparse.h"]
+
+
+def compile_hip(src_dir, out, obj_dir, extra=()):
+    """Each source to an object (its FILE_FLAGS), in parallel, then one link."""
+    src_dir, obj_dir = pathlib.Path(src_dir), pathlib.Path(obj_dir)
+    obj_dir.mkdir(parents=True, exist_ok=True)
+    base = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-fvisibility=hidden", "-Wall"]
+    procs, objs = [], []
+    for name in HIP_SRCS:
+        obj = obj_dir / (name + ".o")
+        objs.append(str(obj))
+        cmd = base + FILE_FLAGS.get(name, []) + list(extra) + ["-c", "-o", str(obj), str(src_dir / name)]
+        procs.append((cmd, subprocess.Popen(cmd)))
+    for cmd, p in procs:
+        if p.wait():
+            raise subprocess.CalledProcessError(p.returncode, cmd)
+    subprocess.check_call([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", str(out)] + objs)
+    return out
+
+
 def build_hip(force=False):
     out = ROOT / "mp3_amd" / "libmp3d.so"
-    srcs = [CSRC / "mp3d_demux.hip", CSRC / "mp3d_huffman.hip", CSRC / "mp3d_synth.hip", CSRC / "mp3d_host.cpp"]
-    deps = srcs + [CSRC / "mp3d_internal.h", CSRC / "mp3d_tables.h", CSRC / "mp3d_consts.h", CSRC / "mp3d_device.h",
-                   CSRC / "mp3d_hostparse.h",
-                   ROOT / "include" / "mp3d.h"]
+    deps = [CSRC / n for n in HIP_SRCS + HIP_HDRS] + [ROOT / "include" / "mp3d.h", pathlib.Path(__file__)]
     if force or _stale(out, deps):
-        cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-fPIC", "-shared", "-std=c++17", "-fvisibility=hidden",
-               "-Wall", "-o", str(out)] + [str(s) for s in srcs]
-        subprocess.check_call(cmd)
+        compile_hip(CSRC, out, ROOT / "mp3_amd" / "_obj")
     return out
 
 
