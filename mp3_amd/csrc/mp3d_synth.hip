@@ -159,6 +159,15 @@ struct __attribute__((aligned(256))) SynWave { /* one per wave (stream)       */
 };
 typedef __attribute__((address_space(3))) const float lds_cf32;
 
+/* per-lane select on a wave mask, opaque to the optimizer: written as
+ * `c ? t : f` the compiler sinks t's computation into a divergent branch
+ * (exec save / restore and register copies around each state update) */
+__device__ __forceinline__ float lane_sel(uint64_t m, float f, float t) {
+    float r;
+    __asm__("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+    return r;
+}
+
 #define WAIT_VMCNT0() __builtin_amdgcn_s_waitcnt(0x0F70) /* vmcnt(0), other counters free */
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -378,6 +387,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
             mext = (int)(r5 >> 20) & 3;
         }
         const bool active = ch < nch;
+        const uint64_t amask = __ballot(active); /* lanes of coded channels */
         const uint32_t(*lpair)[288] = T.lpair[sr];
         for (int gr = 0; gr < (LSF ? 1 : 2); gr++) { /* LSF: one granule per frame */
             /* lane-derived indices are re-derived from an opaque copy each
@@ -642,11 +652,16 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                  * the first one (mixed), none (short) */
                 const bool upper = (bt != 2 && sb >= 1) || (bt == 2 && mixed && sb == 1);
                 const bool lower = (bt != 2 && sb <= 30) || (bt == 2 && mixed && sb == 0);
+                /* both butterflies computed, then selected: written as
+                 * conditional stores the compiler built a divergent branch
+                 * plus ~50 register copies around it */
 #pragma unroll
                 for (int k = 0; k < 8; k++) {
                     const float lo = x[17 - k], hi = x[k];
-                    if (upper) x[k] = hi * MP3D_K_ALIAS_CS[k] + up[k] * MP3D_K_ALIAS_CA[k];
-                    if (lower) x[17 - k] = lo * MP3D_K_ALIAS_CS[k] - dn[k] * MP3D_K_ALIAS_CA[k];
+                    const float nh = fmaf(up[k], MP3D_K_ALIAS_CA[k], hi * MP3D_K_ALIAS_CS[k]);
+                    const float nl = fmaf(-dn[k], MP3D_K_ALIAS_CA[k], lo * MP3D_K_ALIAS_CS[k]);
+                    x[k] = upper ? nh : hi;
+                    x[17 - k] = lower ? nl : lo;
                 }
                 const bool long_imdct = bt != 2 || (mixed && sb < 2);
                 if (long_imdct) {
@@ -659,8 +674,8 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                         o18[17 - i] = fmaf(w[9 + i], wv[17 - i], ov[17 - i]);
                         const float n0 = w[8 - i] * wv[18 + i];
                         const float n1 = w[8 - i] * wv[35 - i];
-                        ov[i] = active ? n0 : ov[i];
-                        ov[17 - i] = active ? n1 : ov[17 - i];
+                        ov[i] = lane_sel(amask, ov[i], n0);
+                        ov[17 - i] = lane_sel(amask, ov[17 - i], n1);
                     }
                 } else {
                     /* z[6w+6+i] += y_w[i] * win12[i], w = 0..2, i = 0..11 */
@@ -690,7 +705,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
 #pragma unroll
                     for (int i = 0; i < 18; i++) {
                         const float n = i < 12 ? z[12 + i] : 0.f;
-                        ov[i] = active ? n : ov[i];
+                        ov[i] = lane_sel(amask, ov[i], n);
                     }
                 }
             }
@@ -862,9 +877,9 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                     }
                 }
 #pragma unroll
-                for (int k = 0; k < 14; k++) ha[k] = active ? xa[k + 4] : ha[k];
+                for (int k = 0; k < 14; k++) ha[k] = lane_sel(amask, ha[k], xa[k + 4]);
 #pragma unroll
-                for (int k = 0; k < 15; k++) hb[k] = active ? xb[k + 3] : hb[k];
+                for (int k = 0; k < 15; k++) hb[k] = lane_sel(amask, hb[k], xb[k + 3]);
             }
             wave_sync(); /* X reads done before the next granule's xr */
         }
