@@ -50,6 +50,7 @@ VARS = {
     "Q3": [],
     "S1": [],
     "A2": [],
+    "P1": [],
     "NOSLP": [],  # now the default for mp3d_synth.hip (_build.FILE_FLAGS)
     # r02 sensitivity probes (same output): +64 dependent-free VALU per granule in k_synth phase W,
     # +8 VALU per codeword in the Huffman big_values loop

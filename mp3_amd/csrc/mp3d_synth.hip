@@ -106,7 +106,9 @@ __device__ __forceinline__ void imdct36_w(const float *X, float *w) {
 #define SYN_WAVES 4
 #define SROW 36      /* LDS row stride of S (floats): 16-B rows, few conflicts */
 #define SYN_BUF 1296 /* floats: max(xr 2x576, S 36x36, X 36x36)              */
-#define XROW 36      /* LDS row stride of X: 16-B rows, conflict-free b128 writes */
+#define XROW 36      /* LDS row stride of X: 16-B rows, conflict-free b128 writes;
+                      * row n = X[n][0, 2, .., 30] then X[n][1, 3, .., 31] (the
+                      * even / odd matrixing halves as the MFMA leaves them) */
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -211,7 +213,10 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
         }
         for (int i = tid; i < 512; i += 64 * SYN_WAVES)
             T.p43s[i] = i >= 256 ? tab->pow43[i - 256] : -tab->pow43[256 - i];
-        for (int i = tid; i < 32 * 16; i += 64 * SYN_WAVES) (&T.dw[0][0])[i] = (&tab->dwin[0][0])[i];
+        /* int16 sinks: taps x 32768 (exact, a power of two), so the sums
+         * arrive in PCM units without a multiply per sample */
+        for (int i = tid; i < 32 * 16; i += 64 * SYN_WAVES)
+            (&T.dw[0][0])[i] = (&tab->dwin[0][0])[i] * (F32 ? 1.0f : 32768.0f);
         for (int i = tid; i < 4 * 36; i += 64 * SYN_WAVES) (&T.w36[0][0])[i] = (&c_win36[0][0])[i];
         if (LSF) {
             if (tid < 64) (&T.isr[0][0])[tid] = (&c_is_lsf[0][0][0])[tid];
@@ -754,13 +759,14 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                         co[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ao[ks], Bo[nt][ks], co[nt], 0, 0, 0);
                     }
                 wave_sync(); /* all S reads retired before X overwrites them */
-                /* D[row m = 4 q + r][col n] -> X[n][2m] (even), X[n][2m+1] (odd) */
+                /* D[row m = 4 q + r][col n]: X[n][2m] (even) at row n, 4 q + r;
+                 * X[n][2m+1] (odd) at 16 + 4 q + r -- one 16-B store each */
 #pragma unroll
                 for (int nt = 0; nt < 3; nt++) {
                     const int n = 16 * nt + r16;
                     if (n < 36) {
-                        *(f32x4 *)&sBuf[n * XROW + 8 * q] = (f32x4){ce[nt][0], co[nt][0], ce[nt][1], co[nt][1]};
-                        *(f32x4 *)&sBuf[n * XROW + 8 * q + 4] = (f32x4){ce[nt][2], co[nt][2], ce[nt][3], co[nt][3]};
+                        *(f32x4 *)&sBuf[n * XROW + 4 * q] = ce[nt];
+                        *(f32x4 *)&sBuf[n * XROW + 16 + 4 * q] = co[nt];
                     }
                 }
             }
@@ -781,7 +787,9 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                     Dw[4 * i] = d.x; Dw[4 * i + 1] = d.y; Dw[4 * i + 2] = d.z; Dw[4 * i + 3] = d.w;
                 }
                 float xa[18], xb[18];
-                const int pa = opaque(18 * ch * XROW + wa), pb = opaque(18 * ch * XROW + wb);
+                /* X index k sits at (k & 1) 16 + k / 2 of its row */
+                const int pa = opaque(18 * ch * XROW + (wa & 1) * 16 + (wa >> 1));
+                const int pb = opaque(18 * ch * XROW + (wb & 1) * 16 + (wb >> 1));
 #pragma unroll
                 for (int t = 0; t < 18; t++) {
                     xa[t] = sBuf[pa + t * XROW];
@@ -817,7 +825,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                 }
                 auto out2 = [&](int tp) { return acc[tp]; };
                 auto to_pcm = [&](float v) {
-                    const float p = rintf(v * 32768.f);
+                    const float p = rintf(v); /* taps pre-scaled by 32768 */
                     return (int)fminf(fmaxf(p, -32768.f), 32767.f);
                 };
                 const int so = f * 2304 * PB + gr * 576 * nch * PB;
@@ -853,7 +861,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
                      * (L, R): clamp(rint(x 32768)) as before, 2 VALU less per pair */
                     auto to_i32 = [&](float v) {
                         int r;
-                        __asm__("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(rintf(v * 32768.f)));
+                        __asm__("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(rintf(v))); /* taps x 32768 */
                         return r;
                     };
 #pragma unroll
