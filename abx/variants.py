@@ -51,6 +51,7 @@ VARS = {
     "S1": [],
     "A2": [],
     "P1": [],
+    "WK": [],
     "NOSLP": [],  # now the default for mp3d_synth.hip (_build.FILE_FLAGS)
     # r02 sensitivity probes (same output): +64 dependent-free VALU per granule in k_synth phase W,
     # +8 VALU per codeword in the Huffman big_values loop

@@ -411,6 +411,300 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
 
 
 /* ------------------------------------------------------------------------ */
+/* Wide batches: k_walk + k_mdcopy, the same results as k_demux.            */
+/* k_demux walks a stream with one wave, its per-frame decisions uniform,   */
+/* so they run on the scalar unit: ~330 scalar instructions per frame, and  */
+/* the CU's one scalar unit (shared by its 4 SIMDs) is the kernel's limit   */
+/* at C3 (SQ_INSTS_SALU, profiles/).  k_walk gives each stream ONE LANE:    */
+/* the header chain of 64 streams runs side by side as vector arithmetic,   */
+/* each lane staging a 64-B window of its stream at the frame position in   */
+/* LDS.  k_mdcopy then copies every frame's payload into the md region      */
+/* (one wave per stream; no frame waits on another's header).  k_walk       */
+/* leaves the md end and the next carry length in StreamState.pad_ for     */
+/* k_mdcopy, which moves the carry (StreamState.res) in and out.           */
+/* ------------------------------------------------------------------------ */
+#define WALK_WORDS 17 /* LDS dwords per lane: a 64-B window (+1: odd stride) */
+
+struct LaneWin {        /* one lane's 64-B window of its stream, staged in LDS */
+    uint32_t *w;        /* the lane's LDS words                                */
+    uint32_t pos, mis;  /* stream offset of window byte mis; mis = address & 15 */
+    __device__ __forceinline__ uint32_t byte(uint32_t k) const { /* stream byte pos + k, k < 64 - mis */
+        return ((const uint8_t *)w)[mis + k];
+    }
+    /* 64 bits of the big-endian bit string starting at bit b after pos */
+    __device__ __forceinline__ uint64_t bits64(uint32_t b) const {
+        const uint32_t a = 8u * mis + b, wi = a >> 5, sh = a & 31u;
+        const uint64_t hi = ((uint64_t)__builtin_bswap32(w[wi]) << 32) | __builtin_bswap32(w[wi + 1]);
+        const uint32_t x2 = __builtin_bswap32(w[wi + 2]);
+        return sh ? (hi << sh) | ((uint64_t)x2 >> (32 - sh)) : hi;
+    }
+};
+
+/* the four 16-B aligned blocks around stream offset pos: every block holds
+ * a stream byte (so none leaves the pages of the caller's buffer, which are
+ * 16-B aligned units) or is not loaded; bytes at or past len read as zero */
+__device__ __forceinline__ void walk_load(LaneWin &W, const uint8_t *p0, uint32_t len, uint32_t pos) {
+    W.pos = pos;
+    W.mis = (uint32_t)((uintptr_t)(p0 + pos) & 15u);
+    const uint4 *base = (const uint4 *)(p0 + pos - W.mis);
+    uint4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int64_t first = (int64_t)pos - (int64_t)W.mis + 16 * j; /* stream offset of the block */
+        v[j] = make_uint4(0u, 0u, 0u, 0u);
+        if (first < (int64_t)len) v[j] = base[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int64_t over = (int64_t)pos - (int64_t)W.mis + 16 * j + 16 - (int64_t)len; /* bytes past the end */
+        uint32_t q[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int64_t o = over - 4 * (3 - i); /* bytes of word i past the end */
+            q[i] = o >= 4 ? 0u : o > 0 ? q[i] & (0xFFFFFFFFu >> (8 * o)) : q[i];
+            W.w[4 * j + i] = q[i];
+        }
+    }
+}
+
+/* CRC-16 (poly 0x8005, init 0xFFFF, MSB first) over header bytes 2..3 and
+ * the side info (window bytes 6 ..), against bytes 4..5 -- one lane, bitwise;
+ * only for protected frames under MP3D_OPT_CRC_CHECK */
+__device__ __forceinline__ bool walk_crc_ok(const LaneWin &W, uint32_t side_bytes) {
+    uint32_t c = 0xFFFFu;
+    for (uint32_t i = 0; i < 2u + side_bytes; i++) {
+        const uint32_t m = W.byte(i < 2u ? 2u + i : 4u + i);
+        c ^= m << 8;
+#pragma unroll
+        for (int b = 0; b < 8; b++) c = crc_mulx(c);
+    }
+    return c == ((W.byte(4) << 8) | W.byte(5));
+}
+
+__global__ void __launch_bounds__(64) k_walk(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
+                                             const uint32_t *__restrict__ in_len, StreamState *__restrict__ st,
+                                             FrameRec *__restrict__ rec, uint64_t *__restrict__ sideu,
+                                             DevInfo *__restrict__ infos, int n_streams, int F, int opts) {
+    __shared__ uint32_t s_win[64 * WALK_WORDS];
+    const int lane = threadIdx.x;
+    const int s = blockIdx.x * 64 + lane;
+    if (s >= n_streams) return; /* no barrier below */
+    LaneWin W;
+    W.w = s_win + lane * WALK_WORDS;
+    const uint8_t *p0 = in + in_off[s];
+    const uint32_t len = in_len[s];
+    StreamState &S = st[s];
+    const int carry_in = S.res_len;
+    const bool stream_start = S.frames == 0;
+    int kind = S.kind;
+    uint32_t P = (uint32_t)carry_in;
+    int avail = carry_in;
+    uint32_t cur = 0;
+    walk_load(W, p0, len, 0);
+    if (stream_start && len >= 10 && W.byte(0) == 'I' && W.byte(1) == 'D' && W.byte(2) == '3') {
+        const uint32_t sz = (W.byte(6) & 0x7Fu) << 21 | (W.byte(7) & 0x7Fu) << 14 | (W.byte(8) & 0x7Fu) << 7 |
+                            (W.byte(9) & 0x7Fu);
+        cur = 10 + sz + ((W.byte(5) & 0x10u) ? 10u : 0u);
+    }
+    int decoded = 0;
+    for (int f = 0; f < F; f++) {
+        const size_t fi = (size_t)s * F + f;
+        /* ---- sync: the next valid header at or after cur (resync over junk) */
+        int fb = -1;
+        while (cur + 4 <= len) {
+            if (W.pos != cur) walk_load(W, p0, len, cur);
+            const uint32_t lim = min(46u, len - cur - 4);
+            uint32_t k = 0;
+            for (; k <= lim; k++) {
+                if (W.byte(k) == 0xFFu) {
+                    fb = hdr_frame_bytes(W.byte(k + 1), W.byte(k + 2), kind);
+                    if (fb > 0) break;
+                }
+            }
+            cur += k;
+            if (fb > 0) break;
+        }
+        FrameRec r;
+        r.frame_off = 0; r.md_bit = 0; r.payload_md = P; r.frame_bytes = 0; r.payload_len = 0;
+        r.hdr1 = r.hdr2 = r.hdr3 = 0; r.nch = 0; r.side_off = 4; r.first_gr = 0; r.sr_idx = 0; r.lsf = 0;
+        r.payload_avail = 0;
+        DevInfo inf = {0, 0, 0, 0, 0, 0};
+        uint64_t sw[4] = {0ull, 0ull, 0ull, 0ull};
+        if (fb > 0) {
+            if (W.pos != cur) walk_load(W, p0, len, cur);
+            const uint32_t h1 = W.byte(1), h2 = W.byte(2), h3 = W.byte(3);
+            const int nch = (h3 >> 6) == 3 ? 1 : 2;
+            const int crc = (h1 & 1) ? 0 : 2;
+            const bool lsf = hdr_kind(h1) == 2;
+            const int ngr = lsf ? 1 : 2;
+            const int side_bytes = lsf ? (nch == 1 ? 9 : 17) : (nch == 1 ? 17 : 32);
+            kind = hdr_kind(h1);
+            const uint32_t need = 4u + (uint32_t)crc + (uint32_t)side_bytes;
+            if (cur + (uint32_t)fb <= len || cur + need <= len) {
+                const uint32_t have = min(len - cur, (uint32_t)fb);
+                const int plen = fb - 4 - crc - side_bytes;
+                r.frame_off = in_off[s] + cur;
+                r.frame_bytes = (uint16_t)fb;
+                r.payload_len = (uint16_t)(plen > 0 ? plen : 0);
+                r.hdr1 = (uint8_t)h1; r.hdr2 = (uint8_t)h2; r.hdr3 = (uint8_t)h3;
+                r.nch = (uint8_t)nch;
+                r.side_off = (uint8_t)(4 + crc);
+                r.sr_idx = (uint8_t)hdr_sr_idx(h1, h2);
+                r.lsf = (uint8_t)lsf;
+                inf.frame_bytes = fb; inf.channels = nch; inf.hz = (int)MP3D_SAMPLE_RATE[r.sr_idx];
+                inf.layer = 3; inf.bitrate_kbps = lsf ? MP3D_BITRATE_L3_LSF[h2 >> 4] : MP3D_BITRATE_L3[h2 >> 4];
+                const uint32_t sbit = 8u * (4u + (uint32_t)crc);
+                const int mdb = (int)(W.bits64(sbit) >> (lsf ? 56 : 55));
+                uint32_t p23[2][2] = {{0u, 0u}, {0u, 0u}};
+                bool anybad = false;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int qgr = q >> 1, qch = q & 1;
+                    if (qch < nch && qgr < ngr) {
+                        const uint32_t ub = sbit + side_unit_bit(nch, qgr, qch, lsf);
+                        uint64_t v59;
+                        uint32_t low5;
+                        if (lsf) { /* the 63-bit LSF unit in the MPEG-1 layout (k_demux) */
+                            const uint64_t v63 = W.bits64(ub) >> 1;
+                            const uint32_t sfc9 = (uint32_t)(v63 >> 25) & 511u;
+                            const uint64_t low25 = v63 & 0x1FFFFFFull;
+                            const bool is_right = (h3 >> 6) == 1 && ((h3 >> 4) & 1) && qch == 1;
+                            v59 = ((v63 >> 34) << 30) | ((uint64_t)(sfc9 & 15u) << 26) | ((low25 >> 2) << 3) |
+                                  ((uint64_t)is_right << 2) | (low25 & 3u);
+                            low5 = sfc9 >> 4;
+                        } else {
+                            v59 = W.bits64(ub) >> 5;
+                            low5 = (uint32_t)(W.bits64(sbit + 9 + (nch == 1 ? 5 : 3) + 4 * qch) >> 60) << 1;
+                        }
+                        p23[qgr][qch] = (uint32_t)(v59 >> 47);
+                        anybad |= ((v59 >> 38) & 0x1FFu) > 288u || (v59 & (7ull << 23)) == (4ull << 23);
+                        sw[q] = (v59 << 5) | low5;
+                    }
+                }
+                const bool crc_bad = (opts & MP3D_OPT_CRC_CHECK) && crc && !walk_crc_ok(W, (uint32_t)side_bytes);
+                const bool bad = plen < 0 || anybad || crc_bad;
+                const uint32_t tgo = 4u + (uint32_t)crc + (uint32_t)side_bytes;
+                const bool tag = stream_start && f == 0 && plen >= 4 && have == (uint32_t)fb &&
+                                 ((W.byte(tgo) == 'X' && W.byte(tgo + 1) == 'i' && W.byte(tgo + 2) == 'n' &&
+                                   W.byte(tgo + 3) == 'g') ||
+                                  (W.byte(tgo) == 'I' && W.byte(tgo + 1) == 'n' && W.byte(tgo + 2) == 'f' &&
+                                   W.byte(tgo + 3) == 'o'));
+                if (tag) {
+                    r.first_gr = REC_TAG;
+                    S.tag_info = parse_info_tag(p0 + cur + tgo, (uint32_t)fb - tgo, S.tag_frames);
+                } else if (bad) {
+                    r.first_gr = REC_DROP;
+                    r.payload_len = (uint16_t)(fb - 4);
+                    avail = fb - 4 < MP3D_RES_BYTES ? fb - 4 : MP3D_RES_BYTES;
+                    P += (uint32_t)r.payload_len;
+                } else {
+                    int gr0 = 0;
+                    uint32_t mdbit;
+                    if (mdb <= avail) {
+                        mdbit = (P - (uint32_t)mdb) * 8u;
+                    } else {
+                        uint32_t bits = (uint32_t)avail * 8u;
+                        while (gr0 < ngr && (int)(bits >> 3) < mdb) {
+                            bits += p23[gr0][0] + p23[gr0][1];
+                            gr0++;
+                        }
+                        mdbit = (P - (uint32_t)avail) * 8u + bits - 8u * (uint32_t)mdb;
+                    }
+                    /* units past nch / ngr hold 0 */
+                    const uint32_t end = mdbit + (gr0 == 0 ? p23[0][0] + p23[0][1] : 0u) +
+                                         (gr0 <= 1 ? p23[1][0] + p23[1][1] : 0u);
+                    r.md_bit = mdbit;
+                    r.first_gr = (uint8_t)gr0;
+                    P += (uint32_t)plen;
+                    const int64_t after = (int64_t)P - (int64_t)((end + 7u) >> 3);
+                    avail = after < 0 ? 0 : (int)after;
+                    inf.samples = lsf ? 576 : 1152;
+                    decoded++;
+                }
+                const uint32_t body = (r.first_gr & REC_DROP) ? 4u : need;
+                const uint32_t av = have > body ? have - body : 0u;
+                r.payload_avail = (uint16_t)(av < r.payload_len ? av : r.payload_len);
+                cur = have == (uint32_t)fb ? cur + (uint32_t)fb : len;
+            } else {
+                cur = len;
+            }
+        }
+        rec[fi] = r;
+        if (infos) infos[fi] = inf;
+        ulonglong2 *sd = (ulonglong2 *)&sideu[fi * 4];
+        sd[0] = make_ulonglong2(sw[0], sw[1]);
+        sd[1] = make_ulonglong2(sw[2], sw[3]);
+        /* the next frame's window in flight while this frame's records store */
+        if (cur + 4 <= len && f + 1 < F) walk_load(W, p0, len, cur);
+    }
+    int c = avail < MP3D_RES_BYTES ? avail : MP3D_RES_BYTES;
+    if ((uint32_t)c > P) c = (int)P;
+    S.frames += decoded;
+    S.kind = kind;
+    S.pad_[0] = (int32_t)P; /* md end, for k_mdcopy */
+    S.pad_[1] = c;          /* next carry length   */
+}
+
+/* k_mdcopy: one wave per stream.  Carry-in, then every frame's payload (the
+ * k_demux copy, fed from the FrameRec k_walk wrote), then the next carry. */
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
+k_mdcopy(const uint8_t *__restrict__ in, uint8_t *__restrict__ md, const uint64_t *__restrict__ md_off,
+         StreamState *__restrict__ st, const FrameRec *__restrict__ rec, int F) {
+    const int s = blockIdx.x;
+    const int lane = threadIdx.x;
+    uint8_t *dst = md + md_off[s];
+    StreamState &S = st[s];
+    const int carry_in = S.res_len;
+    for (int i = lane; i < (carry_in + 3) / 4; i += 64) ((uint32_t *)dst)[i] = ((const uint32_t *)S.res)[i];
+    __threadfence_block(); /* carry words may spill past carry_in into payload 0's head */
+    for (int f = 0; f < F; f++) {
+        const FrameRec r = rec[(size_t)s * F + f];
+        if (!r.frame_bytes || (r.first_gr & REC_TAG)) continue;
+        const uint32_t side_bytes = r.lsf ? (r.nch == 1 ? 9u : 17u) : (r.nch == 1 ? 17u : 32u);
+        const uint32_t body = (r.first_gr & REC_DROP) ? 4u : (uint32_t)r.side_off + side_bytes;
+        const uint8_t *hb0 = in + r.frame_off;
+        const uint8_t *src = hb0 + body;
+        const uint32_t Pm = r.payload_md, L = r.payload_avail;
+        for (uint32_t i = L + lane; i < r.payload_len; i += 64) dst[Pm + i] = 0; /* cut-short final frame */
+        const uint32_t h = min((4u - (Pm & 3u)) & 3u, L);
+        const uint32_t wb = (Pm + h) >> 2, we = (Pm + L) >> 2;
+        const uint32_t t0 = 4u * we > Pm + h ? 4u * we - Pm : h;
+        const uint8_t hbv = *((uint32_t)lane < h ? src + lane : hb0);
+        const uint8_t tbv = *((uint32_t)lane < L - t0 ? src + t0 + lane : hb0);
+        if (wb < we) {
+            const uint8_t *sb = src + (4u * wb - Pm);
+            const uint32_t mis = (uint32_t)((uintptr_t)sb & 3u);
+            const uint32_t sh = mis * 8u;
+            const uint32_t *swd = (const uint32_t *)(sb - mis);
+            const uint32_t nwd = we - wb;
+            uint32_t v[6];
+#pragma unroll
+            for (int j = 0; j < 6; j++) {
+                const uint32_t k = 64u * j + (uint32_t)lane;
+                const uint32_t kk = k < nwd ? k : 0u;
+                v[j] = __builtin_amdgcn_alignbit(swd[sh ? kk + 1 : kk], swd[kk], sh);
+            }
+#pragma unroll
+            for (int j = 0; j < 6; j++) {
+                const uint32_t k = 64u * j + (uint32_t)lane;
+                if (k < nwd) ((uint32_t *)dst)[wb + k] = v[j];
+            }
+            for (uint32_t k = 384u + (uint32_t)lane; k < nwd; k += 64) {
+                const uint32_t l = swd[k];
+                ((uint32_t *)dst)[wb + k] = sh ? __builtin_amdgcn_alignbit(swd[k + 1], l, sh) : l;
+            }
+        }
+        if ((uint32_t)lane < h) dst[Pm + lane] = hbv;
+        if ((uint32_t)lane < L - t0) dst[Pm + t0 + lane] = tbv;
+    }
+    __syncthreads();
+    const uint32_t P = (uint32_t)S.pad_[0];
+    const int c = S.pad_[1];
+    for (int i = lane; i < c; i += 64) S.res[i] = dst[P - c + i];
+    if (lane == 0) S.res_len = c;
+}
+
+/* ------------------------------------------------------------------------ */
 /* Host-side launchers                                                       */
 /* ------------------------------------------------------------------------ */
 hipError_t upload_demux_constants(const uint16_t *frame_bytes) {
@@ -429,9 +723,17 @@ hipError_t upload_demux_constants(const uint16_t *frame_bytes) {
     return hipMemcpyToSymbol(HIP_SYMBOL(c_crc_init), in, sizeof(in));
 }
 
+/* wide: k_walk + k_mdcopy (batches of many streams); else one k_demux wave
+ * per stream (fewer launches: the per-frame decoder, small batches) */
 void launch_demux(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len, uint8_t *md,
                   const uint64_t *md_off, StreamState *st, FrameRec *rec, uint64_t *sideu, void *infos, int n_streams,
-                  int F, int opts, hipStream_t strm) {
+                  int F, int opts, bool wide, hipStream_t strm) {
+    if (wide) {
+        hipLaunchKernelGGL(k_walk, dim3((n_streams + 63) / 64), dim3(64), 0, strm, in, in_off, in_len, st, rec, sideu,
+                           (DevInfo *)infos, n_streams, F, opts);
+        hipLaunchKernelGGL(k_mdcopy, dim3(n_streams), dim3(64), 0, strm, in, md, md_off, st, (const FrameRec *)rec, F);
+        return;
+    }
     hipLaunchKernelGGL(k_demux, dim3(n_streams), dim3(64), 0, strm, in, in_off, in_len, md, md_off, st, rec, sideu,
                        (DevInfo *)infos, F, opts);
 }

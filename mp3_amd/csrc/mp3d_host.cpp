@@ -27,7 +27,7 @@ namespace mp3d {
 hipError_t upload_synth_constants(const float *, const float *, const float *, const float *);
 hipError_t upload_demux_constants(const uint16_t *);
 void launch_demux(const uint8_t *, const uint64_t *, const uint32_t *, uint8_t *, const uint64_t *, StreamState *,
-                  FrameRec *, uint64_t *, void *, int, int, int, hipStream_t);
+                  FrameRec *, uint64_t *, void *, int, int, int, bool, hipStream_t);
 void launch_huffman(const uint8_t *, const uint64_t *, const FrameRec *, const uint64_t *, const DevTables *, int16_t *,
                     UnitMeta *, int, int, int, hipStream_t);
 void launch_synth(const FrameRec *, const int16_t *, const UnitMeta *, const DevTables *, StreamState *, void *, bool, int,
@@ -429,6 +429,16 @@ extern "C" int mp3d_batch_kernel_times(mp3d_batch *b, float *us3) {
     return MP3D_OK;
 }
 
+/* batches from this many streams take k_walk + k_mdcopy */
+#define MP3D_WIDE_STREAMS 256
+/* MP3D_DEMUX=lane | wave forces the demux path (tests run both) */
+static bool demux_wide(int n) {
+    const char *e = getenv("MP3D_DEMUX");
+    if (e && !strcmp(e, "lane")) return true;
+    if (e && !strcmp(e, "wave")) return false;
+    return n >= MP3D_WIDE_STREAMS;
+}
+
 /* Upload stream geometry (cached when unchanged) and size the md region. */
 static int prepare_geometry(mp3d_batch *b, const uint64_t *offsets, const uint32_t *sizes, int n, hipStream_t s) {
     bool same = b->last_n == n && !memcmp(b->last_off.data(), offsets, sizeof(uint64_t) * n) &&
@@ -476,9 +486,10 @@ static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offse
     if (r) return r;
     DeviceCtx &dc = g_dev[b->device];
     if (b->timing) HIPCHK(hipEventRecord(b->ev[0], s));
-    /* demux + main-data gather in one pass */
+    /* demux + main-data gather: lane-per-stream walk + payload copy for wide
+     * batches, one wave per stream below MP3D_WIDE_STREAMS (fewer launches) */
     launch_demux(din, b->d_in_off, b->d_in_len, b->md, b->d_md_off, b->st, b->rec, b->sideu, b->d_infos, n, F,
-                 b->opts, s);
+                 b->opts, demux_wide(n), s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[1], s));
     launch_huffman(b->md, b->d_md_off, b->rec, b->sideu, dc.tables, b->is_buf, b->meta, n, F, dc.n_cu, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[2], s));
