@@ -52,6 +52,10 @@ VARS = {
     "A2": [],
     "P1": [],
     "WK": [],
+    "MC2": [],
+    "MC3": [],
+    "WL16": [("#define WALK_LANES 64", "#define WALK_LANES 16")],
+    "WL32": [("#define WALK_LANES 64", "#define WALK_LANES 32")],
     "NOSLP": [],  # now the default for mp3d_synth.hip (_build.FILE_FLAGS)
     # r02 sensitivity probes (same output): +64 dependent-free VALU per granule in k_synth phase W,
     # +8 VALU per codeword in the Huffman big_values loop

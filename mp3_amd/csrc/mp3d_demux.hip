@@ -424,6 +424,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
 /* k_mdcopy, which moves the carry (StreamState.res) in and out.           */
 /* ------------------------------------------------------------------------ */
 #define WALK_WORDS 17 /* LDS dwords per lane: a 64-B window (+1: odd stride) */
+#define WALK_LANES 64 /* streams per wave (lanes past it idle)              */
 
 struct LaneWin {        /* one lane's 64-B window of its stream, staged in LDS */
     uint32_t *w;        /* the lane's LDS words                                */
@@ -487,8 +488,8 @@ __global__ void __launch_bounds__(64) k_walk(const uint8_t *__restrict__ in, con
                                              DevInfo *__restrict__ infos, int n_streams, int F, int opts) {
     __shared__ uint32_t s_win[64 * WALK_WORDS];
     const int lane = threadIdx.x;
-    const int s = blockIdx.x * 64 + lane;
-    if (s >= n_streams) return; /* no barrier below */
+    const int s = blockIdx.x * WALK_LANES + lane;
+    if (lane >= WALK_LANES || s >= n_streams) return; /* no barrier below */
     LaneWin W;
     W.w = s_win + lane * WALK_WORDS;
     const uint8_t *p0 = in + in_off[s];
@@ -645,59 +646,103 @@ __global__ void __launch_bounds__(64) k_walk(const uint8_t *__restrict__ in, con
     S.pad_[1] = c;          /* next carry length   */
 }
 
-/* k_mdcopy: one wave per stream.  Carry-in, then every frame's payload (the
- * k_demux copy, fed from the FrameRec k_walk wrote), then the next carry. */
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
-k_mdcopy(const uint8_t *__restrict__ in, uint8_t *__restrict__ md, const uint64_t *__restrict__ md_off,
-         StreamState *__restrict__ st, const FrameRec *__restrict__ rec, int F) {
-    const int s = blockIdx.x;
-    const int lane = threadIdx.x;
+/* k_mdcopy: one wave per stream, 4 streams per workgroup.  Carry-in, then
+ * the payloads four frames at a time (16 lanes each, so four frames' loads
+ * are in flight together), then the next carry.  Each lane first loads the
+ * copy descriptor of one frame (lane f: frame f of a 64-frame chunk), so the
+ * frame loop reads no record from memory.  Payload words: the destination
+ * is written in aligned words, each from one 8-B source load funnel-shifted
+ * by the source misalignment (the k_demux copy; edge bytes and a cut-short
+ * tail as there).  All loads of an iteration are straight-line and
+ * unconditional (lanes without work re-read a valid word): a load under a
+ * branch makes the compiler's waitcnt pass drain vmcnt(0) at the join.  An
+ * aligned source loads words (k - 1, k) instead of (k, k + 1), so no load
+ * passes the payload's last word (word -1 is side info or header). */
+#define MDC_WAVES 4
+#define MDC_ROUNDS 8 /* 16-lane rounds per frame in the unrolled part: 512 B */
+__global__ void __launch_bounds__(64 * MDC_WAVES) k_mdcopy(const uint8_t *__restrict__ in, uint8_t *__restrict__ md,
+                                                         const uint64_t *__restrict__ md_off,
+                                                         StreamState *__restrict__ st,
+                                                         const FrameRec *__restrict__ rec, int n_streams, int F) {
+    const int lane = threadIdx.x & 63;
+    /* wave-uniform (SGPR): the buffer resource below must not be per lane */
+    const int s = blockIdx.x * MDC_WAVES + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (s >= n_streams) return; /* wave-level sync only below */
     uint8_t *dst = md + md_off[s];
+    const __amdgpu_buffer_rsrc_t r_md = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 0x7FFFFFFF, 0x00020000);
     StreamState &S = st[s];
     const int carry_in = S.res_len;
     for (int i = lane; i < (carry_in + 3) / 4; i += 64) ((uint32_t *)dst)[i] = ((const uint32_t *)S.res)[i];
     __threadfence_block(); /* carry words may spill past carry_in into payload 0's head */
-    for (int f = 0; f < F; f++) {
-        const FrameRec r = rec[(size_t)s * F + f];
-        if (!r.frame_bytes || (r.first_gr & REC_TAG)) continue;
-        const uint32_t side_bytes = r.lsf ? (r.nch == 1 ? 9u : 17u) : (r.nch == 1 ? 17u : 32u);
-        const uint32_t body = (r.first_gr & REC_DROP) ? 4u : (uint32_t)r.side_off + side_bytes;
-        const uint8_t *hb0 = in + r.frame_off;
-        const uint8_t *src = hb0 + body;
-        const uint32_t Pm = r.payload_md, L = r.payload_avail;
-        for (uint32_t i = L + lane; i < r.payload_len; i += 64) dst[Pm + i] = 0; /* cut-short final frame */
-        const uint32_t h = min((4u - (Pm & 3u)) & 3u, L);
-        const uint32_t wb = (Pm + h) >> 2, we = (Pm + L) >> 2;
-        const uint32_t t0 = 4u * we > Pm + h ? 4u * we - Pm : h;
-        const uint8_t hbv = *((uint32_t)lane < h ? src + lane : hb0);
-        const uint8_t tbv = *((uint32_t)lane < L - t0 ? src + t0 + lane : hb0);
-        if (wb < we) {
-            const uint8_t *sb = src + (4u * wb - Pm);
-            const uint32_t mis = (uint32_t)((uintptr_t)sb & 3u);
-            const uint32_t sh = mis * 8u;
-            const uint32_t *swd = (const uint32_t *)(sb - mis);
-            const uint32_t nwd = we - wb;
-            uint32_t v[6];
+    const int qf = lane >> 4, ql = lane & 15;
+    for (int c0 = 0; c0 < F; c0 += 64) {
+        /* lane f: copy descriptor of frame c0 + f */
+        uint32_t d_fo0 = 0u, d_fo1 = 0u, d_pmd = 0u, d_len = 0u, d_body = 0u;
+        if (c0 + lane < F) {
+            const FrameRec r = rec[(size_t)s * F + c0 + lane];
+            const bool copy = r.frame_bytes && !(r.first_gr & REC_TAG);
+            const uint32_t side_bytes = r.lsf ? (r.nch == 1 ? 9u : 17u) : (r.nch == 1 ? 17u : 32u);
+            d_fo0 = (uint32_t)r.frame_off;
+            d_fo1 = (uint32_t)(r.frame_off >> 32);
+            d_pmd = r.payload_md;
+            d_len = (uint32_t)r.payload_len | (uint32_t)r.payload_avail << 16;
+            d_body = copy ? ((r.first_gr & REC_DROP) ? 4u : (uint32_t)r.side_off + side_bytes) : 0u;
+        }
+        /* drained here, once: otherwise the compiler waits for vmcnt(0) at
+         * the descriptors' first use in every iteration, i.e. for the
+         * previous frames' stores */
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        const int nf = min(64, F - c0);
+        for (int f0 = 0; f0 < nf; f0 += 4) {
+            /* the descriptor of this quarter's frame, read in every lane (a
+             * cross-lane read from a lane outside the branch below would
+             * not see its value) */
+            const int fl = min(f0 + qf, 63);
+            const uint32_t body = (uint32_t)__shfl((int)d_body, fl);
+            const uint64_t fo = (uint64_t)(uint32_t)__shfl((int)d_fo0, fl) |
+                                (uint64_t)(uint32_t)__shfl((int)d_fo1, fl) << 32;
+            const uint32_t Pm = (uint32_t)__shfl((int)d_pmd, fl), lens = (uint32_t)__shfl((int)d_len, fl);
+            if (f0 + qf < nf && body) {
+                const uint32_t plen = lens & 0xFFFFu, L = lens >> 16;
+                const uint8_t *hb0 = in + fo;
+                const uint8_t *src = hb0 + body;
+                const uint32_t h = min((4u - (Pm & 3u)) & 3u, L);
+                const uint32_t wb = (Pm + h) >> 2, we = (Pm + L) >> 2;
+                const uint32_t t0 = 4u * we > Pm + h ? 4u * we - Pm : h;
+                const uint8_t *sb = src + (4u * wb - Pm);
+                const uint32_t mis = (uint32_t)((uintptr_t)sb & 3u), sh = mis * 8u;
+                const uint32_t nwd = we - wb;
+                /* (pointer arithmetic only: an integer round trip would make
+                 * these flat loads, which wait on both counters) */
+                const uint32_t *lp = nwd ? (const uint32_t *)(sb - mis) - (sh ? 0 : 1)
+                                         : (const uint32_t *)(hb0 - ((uintptr_t)hb0 & 3u));
+                const uint8_t hbv = *((uint32_t)ql < h ? src + ql : hb0);
+                const uint8_t tbv = *((uint32_t)ql < L - t0 ? src + t0 + ql : hb0);
+                uint32_t v[MDC_ROUNDS];
 #pragma unroll
-            for (int j = 0; j < 6; j++) {
-                const uint32_t k = 64u * j + (uint32_t)lane;
-                const uint32_t kk = k < nwd ? k : 0u;
-                v[j] = __builtin_amdgcn_alignbit(swd[sh ? kk + 1 : kk], swd[kk], sh);
-            }
+                for (int j = 0; j < MDC_ROUNDS; j++) {
+                    const uint32_t k = 16u * j + (uint32_t)ql;
+                    const uint2 x = *(const uint2 *)(lp + (k < nwd ? k : 0u));
+                    v[j] = __builtin_amdgcn_alignbit(x.y, sh ? x.x : x.y, sh);
+                }
+                /* stores masked by an out-of-range offset, not a branch (the
+                 * compiler would sink each load into its store's branch) */
 #pragma unroll
-            for (int j = 0; j < 6; j++) {
-                const uint32_t k = 64u * j + (uint32_t)lane;
-                if (k < nwd) ((uint32_t *)dst)[wb + k] = v[j];
-            }
-            for (uint32_t k = 384u + (uint32_t)lane; k < nwd; k += 64) {
-                const uint32_t l = swd[k];
-                ((uint32_t *)dst)[wb + k] = sh ? __builtin_amdgcn_alignbit(swd[k + 1], l, sh) : l;
+                for (int j = 0; j < MDC_ROUNDS; j++) {
+                    const uint32_t k = 16u * j + (uint32_t)ql;
+                    __builtin_amdgcn_raw_buffer_store_b32(v[j], r_md, k < nwd ? 4u * (wb + k) : 0x80000000u, 0, 0);
+                }
+                for (uint32_t k = 16u * MDC_ROUNDS + (uint32_t)ql; k < nwd; k += 16) {
+                    const uint2 x = *(const uint2 *)(lp + k);
+                    ((uint32_t *)dst)[wb + k] = __builtin_amdgcn_alignbit(x.y, sh ? x.x : x.y, sh);
+                }
+                for (uint32_t i = L + ql; i < plen; i += 16) dst[Pm + i] = 0; /* cut-short final frame */
+                if ((uint32_t)ql < h) dst[Pm + ql] = hbv;
+                if ((uint32_t)ql < L - t0) dst[Pm + t0 + ql] = tbv;
             }
         }
-        if ((uint32_t)lane < h) dst[Pm + lane] = hbv;
-        if ((uint32_t)lane < L - t0) dst[Pm + t0 + lane] = tbv;
     }
-    __syncthreads();
+    __threadfence_block();
     const uint32_t P = (uint32_t)S.pad_[0];
     const int c = S.pad_[1];
     for (int i = lane; i < c; i += 64) S.res[i] = dst[P - c + i];
@@ -729,9 +774,10 @@ void launch_demux(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_
                   const uint64_t *md_off, StreamState *st, FrameRec *rec, uint64_t *sideu, void *infos, int n_streams,
                   int F, int opts, bool wide, hipStream_t strm) {
     if (wide) {
-        hipLaunchKernelGGL(k_walk, dim3((n_streams + 63) / 64), dim3(64), 0, strm, in, in_off, in_len, st, rec, sideu,
+        hipLaunchKernelGGL(k_walk, dim3((n_streams + WALK_LANES - 1) / WALK_LANES), dim3(64), 0, strm, in, in_off, in_len, st, rec, sideu,
                            (DevInfo *)infos, n_streams, F, opts);
-        hipLaunchKernelGGL(k_mdcopy, dim3(n_streams), dim3(64), 0, strm, in, md, md_off, st, (const FrameRec *)rec, F);
+        hipLaunchKernelGGL(k_mdcopy, dim3((n_streams + MDC_WAVES - 1) / MDC_WAVES), dim3(64 * MDC_WAVES), 0, strm, in,
+                           md, md_off, st, (const FrameRec *)rec, n_streams, F);
         return;
     }
     hipLaunchKernelGGL(k_demux, dim3(n_streams), dim3(64), 0, strm, in, in_off, in_len, md, md_off, st, rec, sideu,
