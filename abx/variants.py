@@ -54,6 +54,7 @@ VARS = {
     "WK": [],
     "MC2": [],
     "MC3": [],
+    "OV1": [],
     "WL16": [("#define WALK_LANES 64", "#define WALK_LANES 16")],
     "WL32": [("#define WALK_LANES 64", "#define WALK_LANES 32")],
     "NOSLP": [],  # now the default for mp3d_synth.hip (_build.FILE_FLAGS)
