@@ -102,7 +102,9 @@ static void build_huffman_lut(DevTables &t) {
                 lut[base + p] = (uint16_t)(0x8000u | ((uint32_t)subbits[p] << 11) | (uint32_t)abs4);
             }
         for (size_t i = 0; i < code.size(); i++) {
-            uint16_t leaf = (uint16_t)((len[i] << 8) | val[i]);
+            /* big_values leaves: bits 13 / 14 flag x != 0 / y != 0 (a sign bit follows) */
+            const uint32_t sgn = ti < MP3D_NUM_HTABS ? ((val[i] >> 4) != 0) << 13 | ((val[i] & 15) != 0) << 14 : 0u;
+            uint16_t leaf = (uint16_t)((len[i] << 8) | val[i] | sgn);
             if ((int)len[i] <= b1) {
                 uint32_t first = code[i] << (b1 - len[i]), cnt = 1u << (b1 - len[i]);
                 for (uint32_t k = 0; k < cnt; k++) lut[base + first + k] = leaf;

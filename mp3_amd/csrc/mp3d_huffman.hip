@@ -154,32 +154,6 @@ __device__ __attribute__((noinline)) uint32_t read_sf_lsf(lds_cu32 bits, uint32_
     return pos;
 }
 
-/* is[] row writer: words (2 x int16) are shifted through 4 registers and
- * stored 16 B at a time (one dwordx4 per 8 lines instead of 4 dword stores) */
-struct RowWriter {
-    int16_t *out;
-    uint32_t w0, w1, w2, w3;
-    int nw; /* words pushed */
-    __device__ __forceinline__ void push(uint32_t v) {
-        w0 = w1;
-        w1 = w2;
-        w2 = w3;
-        w3 = v;
-        nw++;
-        if ((nw & 3) == 0) *(uint4 *)(out + 2 * (nw - 4)) = make_uint4(w0, w1, w2, w3);
-    }
-    /* flush the last partial 16-B chunk.  Lines from 2 nw (UnitMeta.nz_end)
-     * to 575 are the rzero region: NOT stored (k_synth masks them), which
-     * removes ~2/3 of the row stores -- one row per lane is the slow,
-     * uncoalesced store pattern of this kernel. */
-    __device__ __forceinline__ void finish() {
-        const int r = nw & 3;
-        if (r == 3) *(uint4 *)(out + 2 * (nw - 3)) = make_uint4(w1, w2, w3, 0u);
-        else if (r == 2) *(uint2 *)(out + 2 * (nw - 2)) = make_uint2(w2, w3);
-        else if (r == 1) *(uint32_t *)(out + 2 * (nw - 1)) = w3;
-    }
-};
-
 __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restrict__ md, const uint64_t *__restrict__ md_off,
                                                         const FrameRec *__restrict__ rec,
                                                         const uint64_t *__restrict__ sideu,
@@ -384,48 +358,60 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                     }
                     r1 = r1 < bv2 ? r1 : bv2;
                     r2 = r2 < bv2 ? r2 : bv2;
-                    RowWriter rw;
-                    rw.out = is_buf + (size_t)u * 576;
-                    rw.nw = 0;
-                    rw.w0 = rw.w1 = rw.w2 = rw.w3 = 0u;
+                    /* big_values pairs in groups of 4 (one 16-B row store per
+                     * group, 8 lines; rows are 72 such groups): k is uniform,
+                     * the wave runs while any lane has pairs left, and a pair
+                     * at or past the lane's big_values, or starting at or past
+                     * the part2_3 end (FFmpeg: a truncated unit's remaining
+                     * lines read as zeros), stores a zero word and consumes no
+                     * bits -- the count1 lines then overwrite the group's tail */
+                    int16_t *row = is_buf + (size_t)u * 576;
                     int k = 0;
                     const uint32_t end_bit = start + seg + p23;
-                    for (; k < bv2; k += 2) {
-                        const uint32_t ts = k < r1 ? ts0 : (k < r2 ? ts1 : ts2);
-                        const uint32_t tb = ts & 0xFFFFu, b1 = (ts >> 16) & 15u, lin = ts >> 24;
-                        uint32_t hi, lo;
-                        win64(bits, pos, hi, lo);
-                        const uint32_t i1 = tb + (hi >> (32 - b1));
-                        const uint32_t e1 = s_lut[i1];
-                        /* second level, branch-free: i2 = i1 for a leaf */
-                        const uint32_t nb = (e1 >> 11) & 15u;
-                        const uint32_t sub =
-                            ((e1 & 0x7FFu) << 2) + (uint32_t)((((uint64_t)hi << b1) & 0xFFFFFFFFull) >> (32u - nb));
-                        const uint32_t i2 = (e1 & 0x8000u) ? sub : i1;
-                        const uint32_t e = s_lut[i2];
-                        const uint32_t x = (e >> 4) & 15u, y = e & 15u, len_c = (e >> 8) & 31u;
-                        /* linbits and signs follow the code: <= 28 bits, all in
-                         * the window (code <= 19 bits) */
-                        uint32_t rb = shl64hi(hi, lo, len_c);
-                        const uint32_t nx = x == 15u ? lin : 0u, ny = y == 15u ? lin : 0u;
-                        const uint32_t ex = nx ? rb >> (32 - nx) : 0u;
-                        rb <<= nx;
-                        const uint32_t sx = x != 0u, sgx = rb >> 31;
-                        rb <<= sx;
-                        const uint32_t ey = ny ? rb >> (32 - ny) : 0u;
-                        rb <<= ny;
-                        const uint32_t sy = y != 0u, sgy = rb >> 31;
-                        /* FFmpeg: no pair starts at or past the part2_3 end
-                         * (a truncated unit's remaining lines read as zeros) */
-                        const bool live = pos < end_bit;
-                        pos += live ? len_c + nx + sx + ny + sy : 0u;
-                        int X = (int)(x + ex), Y = (int)(y + ey);
-                        X = !live ? 0 : (sx && sgx) ? -X : X;
-                        Y = !live ? 0 : (sy && sgy) ? -Y : Y;
-                        rw.push((uint32_t)(uint16_t)X | ((uint32_t)(uint16_t)Y << 16));
+                    for (; __ballot(k < bv2); k += 8) {
+                        uint32_t wv[4];
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            const int kk = k + 2 * j;
+                            const uint32_t ts = kk < r1 ? ts0 : (kk < r2 ? ts1 : ts2);
+                            const uint32_t tb = ts & 0xFFFFu, b1 = (ts >> 16) & 15u, lin = ts >> 24;
+                            uint32_t hi, lo;
+                            win64(bits, pos, hi, lo);
+                            const uint32_t i1 = tb + (hi >> (32 - b1));
+                            const uint32_t e1 = s_lut[i1];
+                            /* second level, branch-free: i2 = i1 for a leaf */
+                            const uint32_t nb = (e1 >> 11) & 15u;
+                            const uint32_t sub =
+                                ((e1 & 0x7FFu) << 2) + (uint32_t)((((uint64_t)hi << b1) & 0xFFFFFFFFull) >> (32u - nb));
+                            const uint32_t i2 = (e1 & 0x8000u) ? sub : i1;
+                            const uint32_t e = s_lut[i2];
+                            const uint32_t x = (e >> 4) & 15u, y = e & 15u, len_c = (e >> 8) & 31u;
+                            const uint32_t sx = (e >> 13) & 1u, sy = (e >> 14) & 1u;
+                            /* after the code: [x linbits][x sign][y linbits][y sign],
+                             * <= 28 bits, all in the window (code <= 19 bits); a
+                             * zero-width field extracts 0 (v_bfe_u32) */
+                            const uint32_t rb = shl64hi(hi, lo, len_c);
+                            const uint32_t nx = x == 15u ? lin : 0u, ny = y == 15u ? lin : 0u;
+                            const uint32_t ex = __builtin_amdgcn_ubfe(rb, 32u - nx, nx);
+                            const uint32_t q1 = nx + sx;
+                            const uint32_t sgx = __builtin_amdgcn_ubfe(rb, 32u - q1, 1u);
+                            const uint32_t ey = __builtin_amdgcn_ubfe(rb, 32u - q1 - ny, ny);
+                            const uint32_t q2 = q1 + ny + sy;
+                            const uint32_t sgy = __builtin_amdgcn_ubfe(rb, 32u - q2, 1u);
+                            const bool live = kk < bv2 && pos < end_bit;
+                            pos += live ? len_c + q2 : 0u;
+                            /* x = 0 gives X = 0 whatever the (absent) sign bit */
+                            int X = (int)(x + ex), Y = (int)(y + ey);
+                            X = sgx ? -X : X;
+                            Y = sgy ? -Y : Y;
+                            wv[j] = live ? (uint32_t)(uint16_t)X | ((uint32_t)(uint16_t)Y << 16) : 0u;
+                        }
+                        *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
                     }
+                    k = bv2;
                     /* count1 quadruples until the part2_3 end; a quadruple that
-                     * overreads it is discarded (FFmpeg) */
+                     * overreads it is discarded (FFmpeg); one
+                     * 8-B store each (lines k .. k + 3) */
                     const bool c1b = (side >> 5) & 1;
                     while (k <= 572 && pos < end_bit) {
                         const uint32_t hw = win32(bits, pos);
@@ -448,12 +434,11 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                         if (q2) { bit--; if ((sbits >> bit) & 1) q2 = -1; }
                         if (q3) { bit--; if ((sbits >> bit) & 1) q3 = -1; }
                         pos += lq + ns;
-                        rw.push((uint32_t)(uint16_t)q0 | ((uint32_t)(uint16_t)q1 << 16));
-                        rw.push((uint32_t)(uint16_t)q2 | ((uint32_t)(uint16_t)q3 << 16));
+                        *(uint2 *)(row + k) = make_uint2((uint32_t)(uint16_t)q0 | ((uint32_t)(uint16_t)q1 << 16),
+                                                         (uint32_t)(uint16_t)q2 | ((uint32_t)(uint16_t)q3 << 16));
                         k += 4;
                     }
-                    const int nz_end = 2 * rw.nw;
-                    rw.finish();
+                    const int nz_end = k;
                     UnitMeta m;
                     m.global_gain = (uint8_t)(side >> 35);
                     m.block_type = (uint8_t)(ws ? (side >> 28) & 3 : 0);

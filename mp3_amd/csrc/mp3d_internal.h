@@ -88,7 +88,8 @@ struct StreamState {
 };
 
 /* Huffman LUT layout (u16 entries, two levels, first level <= 8 bits):
- * leaf:    bit15 = 0, bits 8..12 code length, bits 4..7 x, bits 0..3 y
+ * leaf:    bit15 = 0, bits 8..12 code length, bits 4..7 x, bits 0..3 y,
+ *          big_values tables: bit 13 x != 0, bit 14 y != 0 (sign bits)
  * pointer: bit15 = 1, bits 11..14 sub-index bits, bits 0..10 absolute
  *          sub-table index / 4 (sub-tables are 4-entry aligned)          */
 #define MP3D_LUT_TABLES 16 /* 15 big_values code tables + count1 table A   */
