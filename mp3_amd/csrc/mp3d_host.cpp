@@ -29,7 +29,7 @@ hipError_t upload_demux_constants(const uint16_t *);
 void launch_demux(const uint8_t *, const uint64_t *, const uint32_t *, uint8_t *, const uint64_t *, StreamState *,
                   FrameRec *, uint64_t *, void *, int, int, int, bool, hipStream_t);
 void launch_huffman(const uint8_t *, const uint64_t *, const FrameRec *, const uint64_t *, const DevTables *, int16_t *,
-                    UnitMeta *, int, int, int, hipStream_t);
+                    UnitMeta *, int, int, int, bool, hipStream_t);
 void launch_synth(const FrameRec *, const int16_t *, const UnitMeta *, const DevTables *, StreamState *, void *, bool, int,
                   int, int, hipStream_t);
 void launch_synth_xr(const float *, const uint8_t *, const uint8_t *, const DevTables *, StreamState *, int16_t *, int,
@@ -441,6 +441,16 @@ static bool demux_wide(int n) {
     return n >= MP3D_WIDE_STREAMS;
 }
 
+/* batches of at most this many units (frame granule channels) decode one
+ * unit per wave (k_huffman_wave); MP3D_HUFF=wave | lane forces the kernel */
+#define MP3D_WAVE_HUFF_UNITS 1024
+static bool huffman_wave(int n_units) {
+    const char *e = getenv("MP3D_HUFF");
+    if (e && !strcmp(e, "wave")) return true;
+    if (e && !strcmp(e, "lane")) return false;
+    return n_units <= MP3D_WAVE_HUFF_UNITS;
+}
+
 /* Upload stream geometry (cached when unchanged) and size the md region. */
 static int prepare_geometry(mp3d_batch *b, const uint64_t *offsets, const uint32_t *sizes, int n, hipStream_t s) {
     bool same = b->last_n == n && !memcmp(b->last_off.data(), offsets, sizeof(uint64_t) * n) &&
@@ -493,7 +503,8 @@ static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offse
     launch_demux(din, b->d_in_off, b->d_in_len, b->md, b->d_md_off, b->st, b->rec, b->sideu, b->d_infos, n, F,
                  b->opts, demux_wide(n), s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[1], s));
-    launch_huffman(b->md, b->d_md_off, b->rec, b->sideu, dc.tables, b->is_buf, b->meta, n, F, dc.n_cu, s);
+    launch_huffman(b->md, b->d_md_off, b->rec, b->sideu, dc.tables, b->is_buf, b->meta, n, F, dc.n_cu,
+                   huffman_wave(n * F * 4), s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[2], s));
     HIPCHK(hipGetLastError());
     return MP3D_OK;

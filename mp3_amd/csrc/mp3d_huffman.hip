@@ -154,18 +154,13 @@ __device__ __attribute__((noinline)) uint32_t read_sf_lsf(lds_cu32 bits, uint32_
     return pos;
 }
 
-__global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restrict__ md, const uint64_t *__restrict__ md_off,
-                                                        const FrameRec *__restrict__ rec,
-                                                        const uint64_t *__restrict__ sideu,
-                                                        const DevTables *__restrict__ tab, int16_t *__restrict__ is_buf,
-                                                        UnitMeta *__restrict__ meta, int n_units, int F) {
-    __shared__ uint16_t s_lut[MP3D_LUT_MAX];
-    __shared__ __attribute__((aligned(16))) uint32_t s_bits[HUFF_WAVES][HUFF_CAPW + 4];
-    __shared__ uint32_t s_tsel[32]; /* table_select -> LUT base | bits1 << 16 | linbits << 24 */
-    __shared__ uint16_t s_lbnd[9][24]; /* long sfb start line per sample-rate index (23 bounds) */
-    __shared__ uint8_t s_slen[32];     /* MPEG-1 slen1 | slen2 per scalefac_compress          */
+/* the block's LDS tables: the LUT (+ a 2-entry all-zero table for
+ * table_select 0, 4, 14), table_select -> LUT base | bits1 << 16 | linbits
+ * << 24, long sfb start lines per sample-rate index, MPEG-1 slen pairs */
+__device__ __forceinline__ void huff_tables(const DevTables *tab, uint16_t *s_lut, uint32_t *s_tsel,
+                                            uint16_t (*s_lbnd)[24], uint8_t *s_slen) {
     const int lut_n = tab->lut_hdr.base[MP3D_LUT_TABLES - 1] + (1 << tab->lut_hdr.bits1[MP3D_LUT_TABLES - 1]);
-    const int zbase = (lut_n + 1) & ~1; /* 2-entry all-zero table for table_select 0, 4, 14 */
+    const int zbase = (lut_n + 1) & ~1;
     for (int i = threadIdx.x; i < (lut_n + 1) / 2; i += blockDim.x)
         ((uint32_t *)s_lut)[i] = ((const uint32_t *)tab->lut)[i];
     if (threadIdx.x == 0) ((uint32_t *)s_lut)[zbase / 2] = 0u;
@@ -184,6 +179,19 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                                     : (uint32_t)tab->lut_hdr.base[t] | ((uint32_t)tab->lut_hdr.bits1[t] << 16) |
                                           ((uint32_t)MP3D_LINBITS[threadIdx.x] << 24);
     }
+}
+
+__global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restrict__ md, const uint64_t *__restrict__ md_off,
+                                                        const FrameRec *__restrict__ rec,
+                                                        const uint64_t *__restrict__ sideu,
+                                                        const DevTables *__restrict__ tab, int16_t *__restrict__ is_buf,
+                                                        UnitMeta *__restrict__ meta, int n_units, int F) {
+    __shared__ uint16_t s_lut[MP3D_LUT_MAX];
+    __shared__ __attribute__((aligned(16))) uint32_t s_bits[HUFF_WAVES][HUFF_CAPW + 4];
+    __shared__ uint32_t s_tsel[32]; /* table_select -> LUT base | bits1 << 16 | linbits << 24 */
+    __shared__ uint16_t s_lbnd[9][24]; /* long sfb start line per sample-rate index (23 bounds) */
+    __shared__ uint8_t s_slen[32];     /* MPEG-1 slen1 | slen2 per scalefac_compress          */
+    huff_tables(tab, s_lut, s_tsel, s_lbnd, s_slen);
     __syncthreads();
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t *bits = s_bits[wv];
@@ -484,10 +492,289 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
 }
 
 /* ------------------------------------------------------------------------ */
+/* k_huffman_wave: one WAVE per unit, for small batches (the per-frame      */
+/* decoder), where one unit's codeword chain is the whole critical path.     */
+/* Each round, lane L decodes the pair (or count1 quadruple) that would      */
+/* start at bit pos + L with the region's table; the real chain then hops    */
+/* through those speculative decodes by cross-lane reads (next start = this */
+/* start + this length): a few scalar steps per codeword instead of three   */
+/* dependent LDS reads.  A round ends at a region boundary, at the part2_3  */
+/* end, or where the next codeword starts past offset 63.  The decoded words */
+/* collect one per lane of an accumulator and store 256 B at a time.  Same  */
+/* results as k_huffman (FFmpeg: pairs at or past the part2_3 end are zeros; */
+/* a quadruple that overreads it is discarded).                             */
+/* ------------------------------------------------------------------------ */
+#define HW_UNITS 4
+#define HW_WORDS 520 /* staged md words per unit: four 4095-bit units + margin */
+
+__device__ __forceinline__ void hw_win64(const uint32_t *bits, uint32_t pos, uint32_t &hi, uint32_t &lo) {
+    uint32_t w = pos >> 5;
+    w = w < HW_WORDS ? w : HW_WORDS;
+    const uint32_t sh = 32u - (pos & 31u);
+    const uint32_t w0 = bits[w], w1 = bits[w + 1], w2 = bits[w + 2];
+    hi = (uint32_t)((((uint64_t)w0 << 32) | w1) >> sh);
+    lo = (uint32_t)((((uint64_t)w1 << 32) | w2) >> sh);
+}
+
+/* one big_values pair at bit p with table word ts (the k_huffman pair decode):
+ * total bits and the packed (x, y) word */
+__device__ __forceinline__ void hw_pair(const uint16_t *s_lut, const uint32_t *bits, uint32_t p, uint32_t ts,
+                                        uint32_t &tl, uint32_t &word) {
+    const uint32_t tb = ts & 0xFFFFu, b1 = (ts >> 16) & 15u, lin = ts >> 24;
+    uint32_t hi, lo;
+    hw_win64(bits, p, hi, lo);
+    const uint32_t i1 = tb + (hi >> (32 - b1));
+    const uint32_t e1 = s_lut[i1];
+    const uint32_t nb = (e1 >> 11) & 15u;
+    const uint32_t sub = ((e1 & 0x7FFu) << 2) + (uint32_t)((((uint64_t)hi << b1) & 0xFFFFFFFFull) >> (32u - nb));
+    const uint32_t e = s_lut[(e1 & 0x8000u) ? sub : i1];
+    const uint32_t x = (e >> 4) & 15u, y = e & 15u, len_c = (e >> 8) & 31u;
+    const uint32_t sx = (e >> 13) & 1u, sy = (e >> 14) & 1u;
+    const uint32_t rb = shl64hi(hi, lo, len_c);
+    const uint32_t nx = x == 15u ? lin : 0u, ny = y == 15u ? lin : 0u;
+    const uint32_t ex = __builtin_amdgcn_ubfe(rb, 32u - nx, nx);
+    const uint32_t q1 = nx + sx;
+    const uint32_t sgx = __builtin_amdgcn_ubfe(rb, 32u - q1, 1u);
+    const uint32_t ey = __builtin_amdgcn_ubfe(rb, 32u - q1 - ny, ny);
+    const uint32_t q2 = q1 + ny + sy;
+    const uint32_t sgy = __builtin_amdgcn_ubfe(rb, 32u - q2, 1u);
+    int X = (int)(x + ex), Y = (int)(y + ey);
+    X = sgx ? -X : X;
+    Y = sgy ? -Y : Y;
+    tl = len_c + q2;
+    word = (uint32_t)(uint16_t)X | ((uint32_t)(uint16_t)Y << 16);
+}
+
+struct HwOut { /* the unit's is[] row, one word per lane of acc, 64 words per store */
+    uint32_t *row;
+    uint32_t acc;
+    int nw;
+    int lane;
+    __device__ __forceinline__ void emit(uint32_t w) { /* w uniform */
+        /* v_writelane_b32 with the lane select in m0 (two SGPR operands
+         * would exceed gfx9's one constant-bus read) */
+        __asm__("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(acc) : "s"(w), "s"(nw & 63) : "m0");
+        nw++;
+        if ((nw & 63) == 0) row[nw - 64 + lane] = acc;
+    }
+    __device__ __forceinline__ void flush() {
+        if ((nw & 63) && lane < (nw & 63)) row[(nw & ~63) + lane] = acc;
+    }
+};
+
+__global__ void __launch_bounds__(64 * HW_UNITS) k_huffman_wave(const uint8_t *__restrict__ md,
+                                                              const uint64_t *__restrict__ md_off,
+                                                              const FrameRec *__restrict__ rec,
+                                                              const uint64_t *__restrict__ sideu,
+                                                              const DevTables *__restrict__ tab,
+                                                              int16_t *__restrict__ is_buf,
+                                                              UnitMeta *__restrict__ meta, int n_units, int F) {
+    __shared__ uint16_t s_lut[MP3D_LUT_MAX];
+    __shared__ __attribute__((aligned(16))) uint32_t s_bits[HW_UNITS][HW_WORDS + 4];
+    __shared__ uint32_t s_tsel[32];
+    __shared__ uint16_t s_lbnd[9][24];
+    __shared__ uint8_t s_slen[32];
+    huff_tables(tab, s_lut, s_tsel, s_lbnd, s_slen);
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int u = blockIdx.x * HW_UNITS + wv;
+    if (u >= n_units) return; /* after the only barrier */
+    uint32_t *bits = s_bits[wv];
+    const uint32_t qbase = tab->lut_hdr.base[MP3D_LUT_TABLES - 1];
+    const int qb1 = tab->lut_hdr.bits1[MP3D_LUT_TABLES - 1];
+    const int fr = u >> 2, gr = (u >> 1) & 1, ch = u & 1;
+    const FrameRec r = rec[fr];
+    const bool valid = r.frame_bytes && !(r.first_gr & (REC_TAG | REC_DROP)) && ch < r.nch && (gr == 0 || !r.lsf);
+    if (!valid) return;
+    uint64_t sq[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) sq[q] = sideu[(u & ~3) + q];
+    const int first_gr = r.first_gr & 3;
+    const int nch = r.nch;
+    const bool dec = gr >= first_gr;
+    const int q = u & 3;
+    const uint64_t side = sq[q];
+    if (!dec) {
+        /* granule lost to a reservoir underflow: silence (FFmpeg) */
+        uint4 *out = (uint4 *)(is_buf + (size_t)u * 576);
+        for (int i = lane; i < 72; i += 64) out[i] = make_uint4(0u, 0u, 0u, 0u);
+        if (lane == 0) {
+            UnitMeta m;
+#pragma unroll
+            for (int i = 0; i < 10; i++) ((uint32_t *)m.sf)[i] = 0u;
+            const int ws = (int)(side >> 30) & 1;
+            m.global_gain = (uint8_t)(side >> 35);
+            m.block_type = (uint8_t)(ws ? (side >> 28) & 3 : 0);
+            m.mixed = (uint8_t)(ws && ((side >> 28) & 3) == 2 ? (side >> 27) & 1 : 0);
+            m.scalefac_scale = (uint8_t)((side >> 6) & 1);
+            m.preflag = (uint8_t)(r.lsf ? 0 : (int)((side >> 7) & 1));
+            m.sbg[0] = (uint8_t)(ws ? (side >> 14) & 7 : 0);
+            m.sbg[1] = (uint8_t)(ws ? (side >> 11) & 7 : 0);
+            m.sbg[2] = (uint8_t)(ws ? (side >> 8) & 7 : 0);
+            m.nz_end = 0;
+            m.part2_3_length = 0;
+            m.used_bits = 0;
+            m.flags = (uint16_t)(1 | (r.lsf ? ((side >> 31) & 1) << 1 : 0));
+            meta[u] = m;
+        }
+        return;
+    }
+    const uint32_t p23 = (uint32_t)(side >> 52);
+    uint32_t before = 0;
+#pragma unroll
+    for (int qq = 0; qq < 3; qq++)
+        if (qq < q && (qq >> 1) >= first_gr && (qq & 1) < nch) before += (uint32_t)(sq[qq] >> 52);
+    const uint32_t start = r.md_bit + before;
+    const int scfsi_raw = (int)(side >> 1) & 15;
+    const bool long_blk = !(((side >> 30) & 1) && ((side >> 28) & 3) == 2);
+    const int scfsi = (gr == 1 && long_blk) ? scfsi_raw : 0;
+    const bool need_g0 = scfsi && first_gr == 0;
+    const uint32_t g0_start = r.md_bit + (ch ? (uint32_t)(sq[0] >> 52) : 0u);
+    const uint32_t lo_bit = need_g0 ? g0_start : start;
+    const uint32_t w0 = lo_bit >> 5;
+    uint32_t len = ((start + p23 + 31) >> 5) + 4 - w0;
+    len = len < HW_WORDS ? len : HW_WORDS;
+    const uint32_t *src = (const uint32_t *)(md + md_off[fr / F]) + w0;
+    for (uint32_t i = lane; i < len; i += 64) bits[i] = bswap32(src[i]);
+    wave_sync();
+    const uint32_t seg = 0u - 32u * w0; /* md bit -> staged bit */
+    uint32_t pos = start + seg;
+    int lsf_pre = 0;
+    if (r.lsf) {
+        uint32_t p0 = 0;
+        if (lane == 0) p0 = read_sf_lsf((lds_cu32)bits, pos, side, (uint8_t *)&meta[u], &lsf_pre);
+        pos = (uint32_t)__builtin_amdgcn_readlane((int)p0, 0);
+        lsf_pre = __builtin_amdgcn_readlane(lsf_pre, 0);
+    } else {
+        uint32_t sfw[10];
+#pragma unroll
+        for (int i = 0; i < 10; i++) sfw[i] = 0u;
+        if (need_g0) read_sf(bits, g0_start + seg, sq[ch], 0, sfw, s_slen);
+        pos = read_sf(bits, pos, side, scfsi, sfw, s_slen);
+        if (lane == 0) {
+            uint8_t *mrec = (uint8_t *)&meta[u];
+            *(uint4 *)mrec = make_uint4(sfw[0], sfw[1], sfw[2], sfw[3]);
+            *(uint4 *)(mrec + 16) = make_uint4(sfw[4], sfw[5], sfw[6], sfw[7]);
+            *(uint2 *)(mrec + 32) = make_uint2(sfw[8], sfw[9]);
+        }
+    }
+    const int ws = (int)(side >> 30) & 1;
+    const int bv2 = 2 * ((int)(side >> 43) & 0x1FF);
+    int r1, r2;
+    uint32_t ts0, ts1, ts2;
+    if (ws) {
+        const bool sh = ((side >> 28) & 3) == 2;
+        r1 = r.sr_idx < 3 ? 36 : sh ? (r.sr_idx == 8 ? 72 : 36) : (r.sr_idx == 8 ? 108 : 54);
+        r2 = 576;
+        ts0 = s_tsel[(side >> 22) & 31];
+        ts1 = s_tsel[(side >> 17) & 31];
+        ts2 = ts1;
+    } else {
+        const int rc0 = (int)(side >> 11) & 15, rc1 = (int)(side >> 8) & 7;
+        const int b1 = rc0 + 1;
+        int b2 = rc0 + rc1 + 2;
+        if (b2 > 22) b2 = 22;
+        r1 = s_lbnd[r.sr_idx][b1];
+        r2 = s_lbnd[r.sr_idx][b2];
+        ts0 = s_tsel[(side >> 25) & 31];
+        ts1 = s_tsel[(side >> 20) & 31];
+        ts2 = s_tsel[(side >> 15) & 31];
+    }
+    r1 = r1 < bv2 ? r1 : bv2;
+    r2 = r2 < bv2 ? r2 : bv2;
+    HwOut out;
+    out.row = (uint32_t *)(is_buf + (size_t)u * 576);
+    out.acc = 0u;
+    out.nw = 0;
+    out.lane = lane;
+    const uint32_t end_bit = start + seg + p23;
+    int k = 0;
+    while (k < bv2) {
+        if (pos >= end_bit) { /* the rest of big_values reads as zeros */
+            for (; k < bv2; k += 2) out.emit(0u);
+            break;
+        }
+        const uint32_t ts = k < r1 ? ts0 : (k < r2 ? ts1 : ts2);
+        const int kend = k < r1 ? r1 : (k < r2 ? r2 : bv2);
+        uint32_t tl, wd;
+        hw_pair(s_lut, bits, pos + (uint32_t)lane, ts, tl, wd);
+        uint32_t o = 0;
+        do {
+            out.emit((uint32_t)__builtin_amdgcn_readlane((int)wd, (int)o));
+            o += (uint32_t)__builtin_amdgcn_readlane((int)tl, (int)o);
+            k += 2;
+        } while (k < kend && o < 64u && pos + o < end_bit);
+        pos += o;
+    }
+    const bool c1b = (side >> 5) & 1;
+    while (k <= 572 && pos < end_bit) {
+        const uint32_t p = pos + (uint32_t)lane;
+        uint32_t w = p >> 5;
+        w = w < HW_WORDS ? w : HW_WORDS;
+        const uint32_t hw = (uint32_t)((((uint64_t)bits[w] << 32) | bits[w + 1]) >> (32u - (p & 31u)));
+        uint32_t v, lq;
+        if (c1b) {
+            v = 15u - (hw >> 28);
+            lq = 4u;
+        } else {
+            const uint32_t e = s_lut[qbase + (hw >> (32 - qb1))];
+            v = e & 15u;
+            lq = (e >> 8) & 31u;
+        }
+        const uint32_t ns = __builtin_popcount(v);
+        const uint32_t sbits = (hw << lq) >> (32 - (ns ? ns : 1));
+        int bit = (int)ns;
+        int q0 = (v >> 3) & 1, q1 = (v >> 2) & 1, q2 = (v >> 1) & 1, q3 = v & 1;
+        if (q0) { bit--; if ((sbits >> bit) & 1) q0 = -1; }
+        if (q1) { bit--; if ((sbits >> bit) & 1) q1 = -1; }
+        if (q2) { bit--; if ((sbits >> bit) & 1) q2 = -1; }
+        if (q3) { bit--; if ((sbits >> bit) & 1) q3 = -1; }
+        const uint32_t tq = lq + ns;
+        const uint32_t wa = (uint32_t)(uint16_t)q0 | ((uint32_t)(uint16_t)q1 << 16);
+        const uint32_t wb = (uint32_t)(uint16_t)q2 | ((uint32_t)(uint16_t)q3 << 16);
+        uint32_t o = 0;
+        bool over = false;
+        do {
+            const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)tq, (int)o);
+            if (pos + o + t > end_bit) {
+                over = true;
+                break;
+            }
+            out.emit((uint32_t)__builtin_amdgcn_readlane((int)wa, (int)o));
+            out.emit((uint32_t)__builtin_amdgcn_readlane((int)wb, (int)o));
+            o += t;
+            k += 4;
+        } while (k <= 572 && o < 64u && pos + o < end_bit);
+        pos += o;
+        if (over) break;
+    }
+    out.flush();
+    if (lane == 0) {
+        UnitMeta m;
+        m.global_gain = (uint8_t)(side >> 35);
+        m.block_type = (uint8_t)(ws ? (side >> 28) & 3 : 0);
+        m.mixed = (uint8_t)(ws && ((side >> 28) & 3) == 2 ? (side >> 27) & 1 : 0);
+        m.scalefac_scale = (uint8_t)((side >> 6) & 1);
+        m.preflag = (uint8_t)(r.lsf ? lsf_pre : (int)((side >> 7) & 1));
+        m.sbg[0] = (uint8_t)(ws ? (side >> 14) & 7 : 0);
+        m.sbg[1] = (uint8_t)(ws ? (side >> 11) & 7 : 0);
+        m.sbg[2] = (uint8_t)(ws ? (side >> 8) & 7 : 0);
+        m.nz_end = (uint16_t)(2 * out.nw);
+        m.part2_3_length = (uint16_t)p23;
+        m.used_bits = (uint16_t)(pos - start - seg);
+        m.flags = (uint16_t)(r.lsf ? ((side >> 31) & 1) << 1 : 0);
+        *(uint4 *)((uint8_t *)&meta[u] + 40) = *(const uint4 *)((const uint8_t *)&m + 40);
+    }
+}
+
+/* ------------------------------------------------------------------------ */
 /* Host-side launchers                                                       */
 /* ------------------------------------------------------------------------ */
+/* wave: one wave per unit (k_huffman_wave; small batches), else one lane
+ * per unit (k_huffman) */
 void launch_huffman(const uint8_t *md, const uint64_t *md_off, const FrameRec *rec, const uint64_t *sideu,
-                    const DevTables *tab, int16_t *is_buf, UnitMeta *meta, int n_streams, int F, int n_cu,
+                    const DevTables *tab, int16_t *is_buf, UnitMeta *meta, int n_streams, int F, int n_cu, bool wave,
                     hipStream_t strm) {
     int n_units = n_streams * F * 4;
     int supers = (n_units + HUFF_SUPER - 1) / HUFF_SUPER;
@@ -495,6 +782,11 @@ void launch_huffman(const uint8_t *md, const uint64_t *md_off, const FrameRec *r
      * blocks as CUs free up, so uneven super-chunks balance themselves */
     int blocks = (supers + HUFF_WAVES - 1) / HUFF_WAVES;
     (void)n_cu;
+    if (wave) {
+        hipLaunchKernelGGL(k_huffman_wave, dim3((n_units + HW_UNITS - 1) / HW_UNITS), dim3(64 * HW_UNITS), 0, strm, md,
+                           md_off, rec, sideu, tab, is_buf, meta, n_units, F);
+        return;
+    }
     hipLaunchKernelGGL(k_huffman, dim3(blocks), dim3(HUFF_BLOCK), 0, strm, md, md_off, rec, sideu, tab, is_buf, meta,
                        n_units, F);
 }

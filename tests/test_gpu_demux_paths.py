@@ -1,10 +1,13 @@
-"""GPU: the two demux paths -- one wave per stream (k_demux; small batches,
-the per-frame decoder) and one lane per stream (k_walk + k_mdcopy; batches
-from MP3D_WIDE_STREAMS streams) -- produce identical PCM, frame infos and
-stream infos, call after call (carry, tags, family lock), on every golden
-fixture, generated streams of both families, CRC-protected streams under
-both CRC options, unaligned stream placements and garbage with embedded
-sync words.  MP3D_DEMUX forces a path."""
+"""GPU: the kernel variants chosen by batch width produce identical PCM,
+frame infos and stream infos, call after call (carry, tags, family lock), on
+every golden fixture, generated streams of both families, CRC-protected
+streams under both CRC options, unaligned stream placements and garbage with
+embedded sync words:
+- demux: one wave per stream (k_demux; small batches, the per-frame decoder)
+  vs one lane per stream (k_walk + k_mdcopy; from MP3D_WIDE_STREAMS
+  streams), forced by MP3D_DEMUX;
+- Huffman: one wave per unit (k_huffman_wave; up to MP3D_WAVE_HUFF_UNITS
+  units) vs one lane per unit (k_huffman), forced by MP3D_HUFF."""
 import os
 
 import numpy as np
@@ -42,10 +45,10 @@ def _corpus():
     return streams
 
 
-def _run(path, streams, F, opts, pad):
+def _run(path, streams, F, opts, pad, var="MP3D_DEMUX"):
     """two calls per stream: bytes [0, n/2), then [n/2, n) with the state
     carried (cut-short frames, mid-frame resync, reservoir carry)"""
-    os.environ["MP3D_DEMUX"] = path
+    os.environ[var] = path
     try:
         chunks, offs, o = [], [], 0
         for s, d in enumerate(streams):
@@ -66,7 +69,7 @@ def _run(path, streams, F, opts, pad):
             out.append((pcm.copy(), inf.copy(), info))
         return out
     finally:
-        os.environ.pop("MP3D_DEMUX", None)
+        os.environ.pop(var, None)
 
 
 @pytest.mark.parametrize("opts", [0, mp3_amd.OPT_CRC_CHECK])
@@ -79,3 +82,33 @@ def test_paths_identical(opts, pad):
         assert np.array_equal(ia, ib)
         assert np.array_equal(pa, pb)
         assert sa == sb
+
+
+@pytest.mark.parametrize("opts", [0, mp3_amd.OPT_CRC_CHECK])
+def test_huffman_kernels_identical(opts):
+    streams = _corpus()
+    a = _run("lane", streams, 16, opts, True, var="MP3D_HUFF")
+    b = _run("wave", streams, 16, opts, True, var="MP3D_HUFF")
+    for (pa, ia, sa), (pb, ib, sb) in zip(a, b):
+        assert np.array_equal(ia, ib)
+        assert np.array_equal(pa, pb)
+        assert sa == sb
+
+
+def test_huffman_kernels_identical_integer_stage():
+    """is[] rows (up to nz_end) and scalefactors of both Huffman kernels"""
+    streams = _corpus()
+    sz = np.array([len(d) for d in streams], np.uint32)
+    of = np.concatenate([[0], np.cumsum(sz)[:-1]]).astype(np.uint64)
+    blob = np.frombuffer(b"".join(streams) + b"\0" * 64, np.uint8)
+    res = {}
+    dec = mp3_amd.BatchDecoder(len(streams), 16)  # one handle: units no kernel writes hold the same bytes
+    for path in ("lane", "wave"):
+        os.environ["MP3D_HUFF"] = path
+        try:
+            dec.reset()
+            res[path] = dec.huffman_only(blob, of, sz, 16)
+        finally:
+            os.environ.pop("MP3D_HUFF", None)
+    assert np.array_equal(res["lane"][0], res["wave"][0])
+    assert np.array_equal(res["lane"][1], res["wave"][1])
