@@ -478,8 +478,11 @@ static int prepare_geometry(mp3d_batch *b, const uint64_t *offsets, const uint32
 
 /* Front half shared by decode and huffman_only: input staging, k_demux,
  * k_huffman. */
+/* mapped: frames (and dev_infos) are host memory the device reads / writes
+ * directly (the per-frame decoder's pinned buffers): no staging copies */
 static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets, const uint32_t *sizes, int n,
-                     int F, hipStream_t s, bool *sync_needed) {
+                     int F, hipStream_t s, bool *sync_needed, bool mapped = false,
+                     mp3d_frame_info *dev_infos = nullptr) {
     if (!b || !frames || !offsets || !sizes || n <= 0 || F <= 0) return MP3D_E_ARG;
     if (n > b->max_streams || F > b->max_frames) return MP3D_E_CAPACITY;
     HIPCHK(hipSetDevice(b->device));
@@ -487,7 +490,7 @@ static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offse
     uint64_t total = 0;
     for (int i = 0; i < n; i++) total = std::max<uint64_t>(total, offsets[i] + sizes[i]);
     const uint8_t *din = frames;
-    if (!is_device_ptr(frames)) {
+    if (!mapped && !is_device_ptr(frames)) {
         int r = grow((void **)&b->d_in, &b->in_cap, total + 64);
         if (r) return r;
         HIPCHK(hipMemcpyAsync(b->d_in, frames, total, hipMemcpyHostToDevice, s));
@@ -500,8 +503,8 @@ static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offse
     if (b->timing) HIPCHK(hipEventRecord(b->ev[0], s));
     /* demux + main-data gather: lane-per-stream walk + payload copy for wide
      * batches, one wave per stream below MP3D_WIDE_STREAMS (fewer launches) */
-    launch_demux(din, b->d_in_off, b->d_in_len, b->md, b->d_md_off, b->st, b->rec, b->sideu, b->d_infos, n, F,
-                 b->opts, demux_wide(n), s);
+    launch_demux(din, b->d_in_off, b->d_in_len, b->md, b->d_md_off, b->st, b->rec, b->sideu,
+                 dev_infos ? (void *)dev_infos : b->d_infos, n, F, b->opts, demux_wide(n), s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[1], s));
     launch_huffman(b->md, b->d_md_off, b->rec, b->sideu, dc.tables, b->is_buf, b->meta, n, F, dc.n_cu,
                    huffman_wave(n * F * 4), s);
@@ -513,18 +516,21 @@ static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offse
 /* decode into int16 (f32 = false) or float32 PCM, both [n][F][2304] */
 /* kinds: k_synth family variants to launch (bit 0 MPEG-1, bit 1 LSF); 3 for
  * a batch, one bit for the per-frame decoder, which knows its frame's family */
+/* mapped: frames, pcm and infos are device-accessible pinned host memory
+ * (the per-frame decoder): the kernels read and write them in place and the
+ * call ends with one stream sync */
 static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets, const uint32_t *sizes, int n,
                         int F, void *pcm, bool f32, mp3d_frame_info *infos, void *hip_stream, bool overwrite,
-                        int kinds = 3) {
+                        int kinds = 3, bool mapped = false) {
     if (!b || !pcm) return MP3D_E_ARG;
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : b->own;
-    bool sync_needed = false;
-    int r = run_front(b, frames, offsets, sizes, n, F, s, &sync_needed);
+    bool sync_needed = mapped;
+    int r = run_front(b, frames, offsets, sizes, n, F, s, &sync_needed, mapped, mapped ? infos : nullptr);
     if (r) return r;
     const size_t PB = f32 ? sizeof(float) : sizeof(int16_t), row = 2304 * PB;
     const size_t pcm_bytes = (size_t)n * F * row;
     void *dpcm = pcm;
-    bool pcm_host = !is_device_ptr(pcm);
+    bool pcm_host = !mapped && !is_device_ptr(pcm);
     if (pcm_host) {
         r = grow((void **)&b->d_pcm, &b->pcm_cap, pcm_bytes);
         if (r) return r;
@@ -535,8 +541,8 @@ static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *of
     if (b->timing) HIPCHK(hipEventRecord(b->ev[3], s));
     HIPCHK(hipGetLastError());
     const size_t ib = sizeof(mp3d_frame_info) * (size_t)n * F;
-    const bool inf_host = infos && !is_device_ptr(infos);
-    if (infos && !inf_host) HIPCHK(hipMemcpyAsync(infos, b->d_infos, ib, hipMemcpyDeviceToDevice, s));
+    const bool inf_host = infos && !mapped && !is_device_ptr(infos);
+    if (infos && !inf_host && !mapped) HIPCHK(hipMemcpyAsync(infos, b->d_infos, ib, hipMemcpyDeviceToDevice, s));
     if (pcm_host && !overwrite) {
         /* A host sink is read back whole, but each row keeps the caller's
          * bytes the kernel did not write (rows without audio, the second
@@ -742,7 +748,7 @@ extern "C" int mp3d_long_plan(const uint8_t *data, size_t bytes, int L, long lon
 
 static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets, const uint32_t *sizes, int n,
                         int F, void *pcm, bool f32, mp3d_frame_info *infos, void *hip_stream, bool overwrite,
-                        int kinds);
+                        int kinds, bool mapped);
 
 extern "C" int mp3d_batch_decode_long(mp3d_batch *b, const uint8_t *data, size_t bytes, int L, void *pcm, int f32,
                                       long long max_frames, mp3d_frame_info *infos, long long *n_frames,
@@ -863,6 +869,11 @@ struct mp3d_dec {
     uint8_t *h_in = nullptr;            /* pinned: the frame, zero-padded      */
     float *h_out = nullptr;             /* pinned: one frame of PCM            */
     mp3d_frame_info *h_info = nullptr;  /* pinned: its frame info              */
+    /* device addresses of the three (mapped): the kernels read the frame and
+     * write PCM + info in place, no copies (null: staged copies instead) */
+    uint8_t *m_in = nullptr;
+    float *m_out = nullptr;
+    mp3d_frame_info *m_info = nullptr;
 };
 
 static void dec_free(mp3d_dec *d) {
@@ -888,6 +899,15 @@ extern "C" int mp3d_dec_create_on(int device, mp3d_dec **out) {
         hipHostMalloc((void **)&d->h_info, sizeof(mp3d_frame_info)) != hipSuccess) {
         dec_free(d);
         return MP3D_E_NOMEM;
+    }
+    if (!getenv("MP3D_PF_STAGED") && hipHostGetDevicePointer((void **)&d->m_in, d->h_in, 0) == hipSuccess &&
+        hipHostGetDevicePointer((void **)&d->m_out, d->h_out, 0) == hipSuccess &&
+        hipHostGetDevicePointer((void **)&d->m_info, d->h_info, 0) == hipSuccess) {
+    } else {
+        (void)hipGetLastError();
+        d->m_in = nullptr;
+        d->m_out = nullptr;
+        d->m_info = nullptr;
     }
     *out = d;
     return MP3D_OK;
@@ -940,9 +960,13 @@ static int decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, void *pcm
     uint32_t sz = MP3D_PF_BYTES;
     memcpy(d->h_in, buf + pos, have); /* have <= fb <= MP3D_MAX_FRAME_BYTES */
     memset(d->h_in + have, 0, MP3D_PF_BYTES - have);
-    /* PCM straight into pinned memory: only the audio rows are read back */
-    int r = batch_decode(d->b, d->h_in, &off, &sz, 1, 1, d->h_out, f32, d->h_info, nullptr, true,
-                         host_frame_kind(buf + pos)); /* 1 MPEG-1, 2 LSF */
+    /* mapped pinned buffers: the kernels read the frame and write PCM + info
+     * in place (three launches + one sync); else staged copies */
+    const bool mapped = d->m_in != nullptr;
+    int r = mapped ? batch_decode(d->b, d->m_in, &off, &sz, 1, 1, d->m_out, f32, d->m_info, nullptr, true,
+                                  host_frame_kind(buf + pos), true)
+                   : batch_decode(d->b, d->h_in, &off, &sz, 1, 1, d->h_out, f32, d->h_info, nullptr, true,
+                                  host_frame_kind(buf + pos)); /* 1 MPEG-1, 2 LSF */
     if (r) return r;
     const mp3d_frame_info fi = *d->h_info;
     const float *out = d->h_out;

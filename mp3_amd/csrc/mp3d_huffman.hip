@@ -551,9 +551,7 @@ struct HwOut { /* the unit's is[] row, one word per lane of acc, 64 words per st
     int nw;
     int lane;
     __device__ __forceinline__ void emit(uint32_t w) { /* w uniform */
-        /* v_writelane_b32 with the lane select in m0 (two SGPR operands
-         * would exceed gfx9's one constant-bus read) */
-        __asm__("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(acc) : "s"(w), "s"(nw & 63) : "m0");
+        acc = lane == (nw & 63) ? w : acc;
         nw++;
         if ((nw & 63) == 0) row[nw - 64 + lane] = acc;
     }
