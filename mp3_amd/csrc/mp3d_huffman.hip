@@ -681,6 +681,14 @@ __global__ void __launch_bounds__(64 * HW_UNITS) k_huffman_wave(const uint8_t *_
     }
     r1 = r1 < bv2 ? r1 : bv2;
     r2 = r2 < bv2 ? r2 : bv2;
+    /* all of these are wave-uniform; said so, so that the chain loop runs on
+     * scalar registers (LDS-derived values otherwise stay per lane) */
+    r1 = __builtin_amdgcn_readfirstlane(r1);
+    r2 = __builtin_amdgcn_readfirstlane(r2);
+    ts0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)ts0);
+    ts1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)ts1);
+    ts2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)ts2);
+    pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)pos);
     HwOut out;
     out.row = (uint32_t *)(is_buf + (size_t)u * 576);
     out.acc = 0u;
@@ -695,14 +703,21 @@ __global__ void __launch_bounds__(64 * HW_UNITS) k_huffman_wave(const uint8_t *_
         }
         const uint32_t ts = k < r1 ? ts0 : (k < r2 ? ts1 : ts2);
         const int kend = k < r1 ? r1 : (k < r2 ? r2 : bv2);
-        uint32_t tl, wd;
-        hw_pair(s_lut, bits, pos + (uint32_t)lane, ts, tl, wd);
+        /* two speculative decodes per lane (offsets lane, 64 + lane; their
+         * latencies overlap): a round follows the chain over 128 bits */
+        uint32_t tl0, wd0, tl1, wd1;
+        hw_pair(s_lut, bits, pos + (uint32_t)lane, ts, tl0, wd0);
+        hw_pair(s_lut, bits, pos + 64u + (uint32_t)lane, ts, tl1, wd1);
         uint32_t o = 0;
         do {
-            out.emit((uint32_t)__builtin_amdgcn_readlane((int)wd, (int)o));
-            o += (uint32_t)__builtin_amdgcn_readlane((int)tl, (int)o);
+            const bool lo = o < 64u;
+            const int ol = (int)(o & 63u);
+            const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)(lo ? wd0 : wd1), ol);
+            const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)(lo ? tl0 : tl1), ol);
+            out.emit(w);
+            o += t;
             k += 2;
-        } while (k < kend && o < 64u && pos + o < end_bit);
+        } while (k < kend && o < 128u && pos + o < end_bit);
         pos += o;
     }
     const bool c1b = (side >> 5) & 1;
