@@ -56,6 +56,8 @@ VARS = {
     "MC3": [],
     "OV1": [],
     "HG4": [],
+    "LX": [],
+    "LA": [],
     "WL16": [("#define WALK_LANES 64", "#define WALK_LANES 16")],
     "WL32": [("#define WALK_LANES 64", "#define WALK_LANES 32")],
     "NOSLP": [],  # now the default for mp3d_synth.hip (_build.FILE_FLAGS)
