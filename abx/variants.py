@@ -56,8 +56,9 @@ VARS = {
     "MC3": [],
     "OV1": [],
     "HG4": [],
-    "LX": [],
-    "LA": [],
+    "HB": [("""                            const uint32_t i2 = (e1 & 0x8000u) ? sub : i1;
+                            const uint32_t e = s_lut[i2];""", """                            uint32_t e = e1;
+                            if (__ballot(e1 & 0x8000u)) e = s_lut[(e1 & 0x8000u) ? sub : i1];""")],
     "WL16": [("#define WALK_LANES 64", "#define WALK_LANES 16")],
     "WL32": [("#define WALK_LANES 64", "#define WALK_LANES 32")],
     "NOSLP": [],  # now the default for mp3d_synth.hip (_build.FILE_FLAGS)
