@@ -56,6 +56,7 @@ VARS = {
     "MC3": [],
     "OV1": [],
     "HG4": [],
+    "SF": [],
     "HB": [("""                            const uint32_t i2 = (e1 & 0x8000u) ? sub : i1;
                             const uint32_t e = s_lut[i2];""", """                            uint32_t e = e1;
                             if (__ballot(e1 & 0x8000u)) e = s_lut[(e1 & 0x8000u) ? sub : i1];""")],
