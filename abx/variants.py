@@ -8,7 +8,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mp3_amd import _build  # noqa: E402
 
-KERNELS = ["mp3d_demux.hip", "mp3d_huffman.hip", "mp3d_synth.hip"]
+KERNELS = ["mp3d_demux.hip", "mp3d_huffman.hip", "mp3d_synth.hip", "mp3d_demux_dev.h", "mp3d_huffman_dev.h"]
 
 
 def variant(name, reps):
@@ -20,7 +20,7 @@ def variant(name, reps):
         srcs = {k: s.replace(a, b) for k, s in srcs.items()}
     d = "/tmp/vars/" + name
     os.makedirs(d, exist_ok=True)
-    for h in ["mp3d_internal.h", "mp3d_tables.h", "mp3d_consts.h", "mp3d_device.h", "mp3d_hostparse.h"]:
+    for h in _build.HIP_HDRS:
         shutil.copy("mp3_amd/csrc/" + h, d)
     for k, s in srcs.items():
         open(d + "/" + k, "w").write(s)
@@ -57,6 +57,36 @@ VARS = {
     "OV1": [],
     "HG4": [],
     "SF": [],
+    "HT": [],
+    "FR": [],
+    "HTOLD": [("/* the block's LDS tables: the LUT (the whole array: past the last table it\n * holds the zero table of table_select 0, 4, 14), table_select -> LUT base |\n * bits1 << 16 | linbits << 24, long sfb start lines per sample-rate index,\n * MPEG-1 slen pairs.  Every load is independent (one memory latency).\n * Both Huffman kernels run 256-thread blocks. */\n__device__ __forceinline__ void huff_tables(const DevTables *tab, uint16_t *s_lut, uint32_t *s_tsel,\n                                            uint16_t (*s_lbnd)[24], uint8_t *s_slen) {\n    constexpr int LUT4 = MP3D_LUT_MAX / 8; /* uint4 chunks */\n    constexpr int PER = (LUT4 + 255) / 256;\n    const uint4 *src = (const uint4 *)tab->lut;\n    uint4 v[PER];\n#pragma unroll\n    for (int j = 0; j < PER; j++) {\n        const int i = (int)threadIdx.x + 256 * j;\n        if (i < LUT4) v[j] = src[i];\n    }\n    uint32_t ts = 0u, lb = 0u;\n    if (threadIdx.x < 32) ts = tab->tsel[threadIdx.x];\n    if (threadIdx.x < 9 * 24 / 2) lb = ((const uint32_t *)tab->lbnd)[threadIdx.x];\n#pragma unroll\n    for (int j = 0; j < PER; j++) {\n        const int i = (int)threadIdx.x + 256 * j;\n        if (i < LUT4) ((uint4 *)s_lut)[i] = v[j];\n    }\n    if (threadIdx.x < 32) s_tsel[threadIdx.x] = ts;\n    if (threadIdx.x < 9 * 24 / 2) ((uint32_t *)s_lbnd)[threadIdx.x] = lb;\n    if (threadIdx.x < 32) s_slen[threadIdx.x] = MP3D_SLEN[threadIdx.x >> 4][threadIdx.x & 15];\n}\n", "/* the block's LDS tables: the LUT (+ a 2-entry all-zero table for\n * table_select 0, 4, 14), table_select -> LUT base | bits1 << 16 | linbits\n * << 24, long sfb start lines per sample-rate index, MPEG-1 slen pairs */\n__device__ __forceinline__ void huff_tables(const DevTables *tab, uint16_t *s_lut, uint32_t *s_tsel,\n                                            uint16_t (*s_lbnd)[24], uint8_t *s_slen) {\n    const int lut_n = tab->lut_hdr.base[MP3D_LUT_TABLES - 1] + (1 << tab->lut_hdr.bits1[MP3D_LUT_TABLES - 1]);\n    const int zbase = (lut_n + 1) & ~1;\n    for (int i = threadIdx.x; i < (lut_n + 1) / 2; i += blockDim.x)\n        ((uint32_t *)s_lut)[i] = ((const uint32_t *)tab->lut)[i];\n    if (threadIdx.x == 0) ((uint32_t *)s_lut)[zbase / 2] = 0u;\n    if (threadIdx.x < 9) {\n        int acc = 0;\n        for (int i = 0; i < 22; i++) {\n            s_lbnd[threadIdx.x][i] = (uint16_t)acc;\n            acc += MP3D_SFB_LONG_WIDTH[threadIdx.x][i];\n        }\n        s_lbnd[threadIdx.x][22] = (uint16_t)acc;\n    }\n    if (threadIdx.x < 32) s_slen[threadIdx.x] = MP3D_SLEN[threadIdx.x >> 4][threadIdx.x & 15];\n    if (threadIdx.x < 32) {\n        const int t = MP3D_HTAB_OF_SELECT[threadIdx.x];\n        s_tsel[threadIdx.x] = t < 0 ? (uint32_t)zbase | (1u << 16)\n                                    : (uint32_t)tab->lut_hdr.base[t] | ((uint32_t)tab->lut_hdr.bits1[t] << 16) |\n                                          ((uint32_t)MP3D_LINBITS[threadIdx.x] << 24);\n    }\n}\n")],
+    "NOW": [],
+    "NOW2": [],
+    # r02 diagnostic (same output): k_frame phase timestamps (s_memtime) in g_fdbg, read by
+    # tools/dbg/frame_timing.py through mp3d_dbg_read
+    "FRT": [("#define PF_BYTES 4096 /* = MP3D_PF_BYTES (mp3d_host.cpp): the staged stream length */\n",
+             "#define PF_BYTES 4096 /* = MP3D_PF_BYTES (mp3d_host.cpp): the staged stream length */\n"
+             "__device__ unsigned long long g_fdbg[32];\n"
+             "#define FT(i) do { __asm__ volatile(\"s_waitcnt vmcnt(0) lgkmcnt(0)\" ::: \"memory\"); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (lane == 0) g_fdbg[(i)] = t_; } while (0)\n"),
+            ("    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);\n    if (wv == 0) {\n",
+             "    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);\n    const unsigned long long T0 = __builtin_amdgcn_s_memtime(), R0 = __builtin_amdgcn_s_memrealtime();\n"
+             "    if (tid == 0) { g_fdbg[0] = T0; g_fdbg[20] = R0; }\n    if (wv == 0) {\n"),
+            ("        wave_sync();\n        demux_stream((const uint8_t *)s_in, in_off, in_len, md, md_off, st, rec, sideu, infos, 1, opts, 0, lane);\n",
+             "        wave_sync();\n        FT(1);\n        demux_stream((const uint8_t *)s_in, in_off, in_len, md, md_off, st, rec, sideu, infos, 1, opts, 0, lane);\n        FT(2);\n"),
+            ("        synth_tables<F32, LSF, 192>(T, tab, tid - 64);\n",
+             "        synth_tables<F32, LSF, 192>(T, tab, tid - 64);\n        if (wv == 1) FT(3);\n"),
+            ("    __syncthreads(); /* rec, side words, md region and state visible to the workgroup */\n",
+             "    __syncthreads(); /* rec, side words, md region and state visible to the workgroup */\n    if (wv == 0) FT(5);\n"),
+            ("    __syncthreads(); /* is[] rows and UnitMeta visible to wave 0 */\n",
+             "    FT(6 + wv);\n    __syncthreads(); /* is[] rows and UnitMeta visible to wave 0 */\n    if (wv == 0) FT(10);\n"),
+            ("        __threadfence_system(); /* PCM, frame info and state before the completion word */\n",
+             "        FT(11);\n        __threadfence_system(); /* PCM, frame info and state before the completion word */\n        FT(12);\n"
+             "        if (lane == 0) g_fdbg[21] = __builtin_amdgcn_s_memrealtime();\n"),
+            ("""/* k_frame's copies of the demux constants (this translation unit's) */""",
+             """extern "C" __attribute__((visibility("default"))) int mp3d_dbg_read(unsigned long long *h) {
+    return (int)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_fdbg), sizeof(g_fdbg), 0, hipMemcpyDeviceToHost);
+}
+/* k_frame's copies of the demux constants (this translation unit's) */""")],
     "HB": [("""                            const uint32_t i2 = (e1 & 0x8000u) ? sub : i1;
                             const uint32_t e = s_lut[i2];""", """                            uint32_t e = e1;
                             if (__ballot(e1 & 0x8000u)) e = s_lut[(e1 & 0x8000u) ? sub : i1];""")],

@@ -27,7 +27,8 @@ def _stale(target, deps):
 # k_demux is 6.7 % faster WITH it (A/B NOSLP, profiles/r02_ab.txt).
 FILE_FLAGS = {"mp3d_synth.hip": ["-fno-slp-vectorize"]}
 HIP_SRCS = ["mp3d_demux.hip", "mp3d_huffman.hip", "mp3d_synth.hip", "mp3d_host.cpp"]
-HIP_HDRS = ["mp3d_internal.h", "mp3d_tables.h", "mp3d_consts.h", "mp3d_device.h", "mp3d_hostparse.h"]
+HIP_HDRS = ["mp3d_internal.h", "mp3d_tables.h", "mp3d_consts.h", "mp3d_device.h", "mp3d_hostparse.h",
+            "mp3d_demux_dev.h", "mp3d_huffman_dev.h"]
 
 
 def compile_hip(src_dir, out, obj_dir, extra=()):

@@ -36,6 +36,10 @@ void launch_synth_xr(const float *, const uint8_t *, const uint8_t *, const DevT
                      int, int, int, int, float *, hipStream_t);
 void launch_gather_frames(const void *, void *, const void *, void *, const int *, int, int, int, int, int,
                           hipStream_t);
+hipError_t upload_frame_constants(const uint16_t *);
+void launch_frame(const uint8_t *, uint32_t, const uint64_t *, const uint32_t *, uint8_t *, const uint64_t *,
+                  StreamState *, FrameRec *, uint64_t *, void *, int, const DevTables *, int16_t *, UnitMeta *, void *,
+                  bool, bool, uint32_t *, uint32_t, hipStream_t);
 } // namespace mp3d
 
 using namespace mp3d;
@@ -122,8 +126,30 @@ static void build_huffman_lut(DevTables &t) {
         abort();
     }
     for (size_t i = 0; i < lut.size(); i++) t.lut[i] = lut[i] == UNUSED ? (uint16_t)(1u << 8) : lut[i];
+    /* table_select 0, 4, 14: a 2-entry all-zero table (zero-length leaves)
+     * right after the last table (t.lut is zeroed past lut.size()) */
+    const size_t zbase = (lut.size() + 1) & ~(size_t)1;
+    if (zbase + 2 > MP3D_LUT_MAX) {
+        fprintf(stderr, "mp3d: LUT overflow %zu\n", zbase + 2);
+        abort();
+    }
+    for (int i = 0; i < 32; i++) {
+        const int ti = MP3D_HTAB_OF_SELECT[i];
+        t.tsel[i] = ti < 0 ? (uint32_t)zbase | (1u << 16) | (1u << 20)
+                           : (uint32_t)t.lut_hdr.base[ti] | ((uint32_t)t.lut_hdr.bits1[ti] << 16) |
+                                 ((uint32_t)MP3D_LINBITS[i] << 24);
+    }
+    for (int sr = 0; sr < 9; sr++) {
+        int acc = 0;
+        for (int b = 0; b < 22; b++) {
+            t.lbnd[sr][b] = (uint16_t)acc;
+            acc += MP3D_SFB_LONG_WIDTH[sr][b];
+        }
+        t.lbnd[sr][22] = (uint16_t)acc;
+    }
 }
 
+static_assert(offsetof(DevTables, lut) % 16 == 0, "k_huffman stages the LUT in 16-B loads");
 static void build_tables(DevTables &t) {
     memset(&t, 0, sizeof(t));
     for (int i = 0; i < 8208; i++) t.pow43[i] = (float)pow((double)i, 4.0 / 3.0);
@@ -243,6 +269,7 @@ static int upload_symbols() {
                                      (int)MP3D_SAMPLE_RATE[sr]);
     HIPCHK(upload_synth_constants(&win36[0][0], &isr[0][0], p2q, &isl[0][0][0]));
     HIPCHK(upload_demux_constants(&fbt[0][0]));
+    HIPCHK(upload_frame_constants(&fbt[0][0]));
     return MP3D_OK;
 }
 
@@ -874,6 +901,11 @@ struct mp3d_dec {
     uint8_t *m_in = nullptr;
     float *m_out = nullptr;
     mp3d_frame_info *m_info = nullptr;
+    /* one-launch path (k_frame): the kernel writes the call's sequence
+     * number into this mapped word after its PCM; the host polls it */
+    uint32_t *h_done = nullptr, *m_done = nullptr;
+    uint32_t seq = 0;
+    bool fused = false;
 };
 
 static void dec_free(mp3d_dec *d) {
@@ -881,6 +913,7 @@ static void dec_free(mp3d_dec *d) {
     if (d->h_in) (void)hipHostFree(d->h_in);
     if (d->h_out) (void)hipHostFree(d->h_out);
     if (d->h_info) (void)hipHostFree(d->h_info);
+    if (d->h_done) (void)hipHostFree(d->h_done);
     delete d;
 }
 
@@ -894,20 +927,31 @@ extern "C" int mp3d_dec_create_on(int device, mp3d_dec **out) {
         dec_free(d);
         return r;
     }
+    /* the buffers the device writes are coherent (not cached in the GPU's
+     * L2), so the completion word's fence orders them for the host */
+    const unsigned co = hipHostMallocMapped | hipHostMallocCoherent;
     if (hipHostMalloc((void **)&d->h_in, MP3D_PF_BYTES) != hipSuccess ||
-        hipHostMalloc((void **)&d->h_out, sizeof(float) * 2304) != hipSuccess ||
-        hipHostMalloc((void **)&d->h_info, sizeof(mp3d_frame_info)) != hipSuccess) {
+        hipHostMalloc((void **)&d->h_out, sizeof(float) * 2304, co) != hipSuccess ||
+        hipHostMalloc((void **)&d->h_info, sizeof(mp3d_frame_info), co) != hipSuccess ||
+        hipHostMalloc((void **)&d->h_done, 64, co) != hipSuccess) {
         dec_free(d);
         return MP3D_E_NOMEM;
     }
+    *d->h_done = 0u;
     if (!getenv("MP3D_PF_STAGED") && hipHostGetDevicePointer((void **)&d->m_in, d->h_in, 0) == hipSuccess &&
         hipHostGetDevicePointer((void **)&d->m_out, d->h_out, 0) == hipSuccess &&
-        hipHostGetDevicePointer((void **)&d->m_info, d->h_info, 0) == hipSuccess) {
+        hipHostGetDevicePointer((void **)&d->m_info, d->h_info, 0) == hipSuccess &&
+        hipHostGetDevicePointer((void **)&d->m_done, d->h_done, 0) == hipSuccess) {
+        /* MP3D_PF_FUSED=0: the three-kernel path with a stream sync (tests
+         * compare the two) */
+        const char *e = getenv("MP3D_PF_FUSED");
+        d->fused = !(e && !strcmp(e, "0"));
     } else {
         (void)hipGetLastError();
         d->m_in = nullptr;
         d->m_out = nullptr;
         d->m_info = nullptr;
+        d->m_done = nullptr;
     }
     *out = d;
     return MP3D_OK;
@@ -941,6 +985,36 @@ extern "C" int mp3d_dec_stream_info(mp3d_dec *d, mp3d_stream_info *out) {
     return mp3d_batch_stream_info(d->b, 1, out);
 }
 
+/* One frame through k_frame (one launch), then a poll of the mapped
+ * completion word instead of a stream sync (~5 us less per
+ * call).  The frame is in d->h_in[0, have).  A kernel that never completes
+ * is caught by a stream query every few thousand polls. */
+static int pf_fused(mp3d_dec *d, uint32_t have, bool f32, bool lsf) {
+    mp3d_batch *b = d->b;
+    hipStream_t s = b->own;
+    HIPCHK(hipSetDevice(b->device));
+    const uint64_t off = 0;
+    const uint32_t sz = MP3D_PF_BYTES;
+    int r = prepare_geometry(b, &off, &sz, 1, s); /* uploaded once, then cached */
+    if (r) return r;
+    b->last = s;
+    const uint32_t seq = ++d->seq ? d->seq : ++d->seq; /* never 0, the word's initial value */
+    launch_frame(d->m_in, have, b->d_in_off, b->d_in_len, b->md, b->d_md_off, b->st, b->rec, b->sideu, d->m_info,
+                 b->opts, g_dev[b->device].tables, b->is_buf, b->meta, d->m_out, f32, lsf, d->m_done, seq, s);
+    HIPCHK(hipGetLastError());
+    for (uint32_t n = 1;; n++) {
+        if (__atomic_load_n(d->h_done, __ATOMIC_ACQUIRE) == seq) return MP3D_OK;
+        if ((n & 4095u) == 0) {
+            const hipError_t e = hipStreamQuery(s);
+            if (e == hipErrorNotReady) continue;
+            HIPCHK(e);
+            /* the stream is idle: the word must be there now */
+            if (__atomic_load_n(d->h_done, __ATOMIC_ACQUIRE) == seq) return MP3D_OK;
+            return MP3D_E_HIP;
+        }
+    }
+}
+
 static int decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, void *pcm, bool f32, bool last,
                         mp3d_frame_info *info) {
     if (!d || !buf) return MP3D_E_ARG;
@@ -959,14 +1033,19 @@ static int decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, void *pcm
     uint64_t off = 0;
     uint32_t sz = MP3D_PF_BYTES;
     memcpy(d->h_in, buf + pos, have); /* have <= fb <= MP3D_MAX_FRAME_BYTES */
-    memset(d->h_in + have, 0, MP3D_PF_BYTES - have);
-    /* mapped pinned buffers: the kernels read the frame and write PCM + info
-     * in place (three launches + one sync); else staged copies */
-    const bool mapped = d->m_in != nullptr;
-    int r = mapped ? batch_decode(d->b, d->m_in, &off, &sz, 1, 1, d->m_out, f32, d->m_info, nullptr, true,
+    int r;
+    if (d->fused) {
+        r = pf_fused(d, (uint32_t)have, f32, host_frame_kind(buf + pos) == 2);
+    } else {
+        memset(d->h_in + have, 0, MP3D_PF_BYTES - have);
+        /* mapped pinned buffers: the kernels read the frame and write PCM +
+         * info in place (three launches + one sync); else staged copies */
+        const bool mapped = d->m_in != nullptr;
+        r = mapped ? batch_decode(d->b, d->m_in, &off, &sz, 1, 1, d->m_out, f32, d->m_info, nullptr, true,
                                   host_frame_kind(buf + pos), true)
                    : batch_decode(d->b, d->h_in, &off, &sz, 1, 1, d->h_out, f32, d->h_info, nullptr, true,
                                   host_frame_kind(buf + pos)); /* 1 MPEG-1, 2 LSF */
+    }
     if (r) return r;
     const mp3d_frame_info fi = *d->h_info;
     const float *out = d->h_out;

@@ -112,8 +112,16 @@ struct DevTables {
     uint32_t lpair[9][3][288];
     uint8_t win_a[32];         /* V[j] = sgn * X[a[j]]                   */
     uint8_t win_b[32];         /* V[32 + j] = sgn * X[b[j]]              */
-    uint16_t lut[MP3D_LUT_MAX];
+    uint16_t lut[MP3D_LUT_MAX];  /* entries past the last table are 0: the    */
+                                 /* zero table of table_select 0, 4, 14 at    */
+                                 /* tsel's base for those selects             */
     struct HuffLutHeader lut_hdr;
+    /* table_select -> LUT base | first-level bits << 16 | zero table << 20 |
+     * linbits << 24, and
+     * the long sfb start lines per sample-rate index (23 bounds): built on
+     * the host so k_huffman's table staging is one load deep              */
+    uint32_t tsel[32];
+    uint16_t lbnd[9][24];
 };
 
 #endif

@@ -2,11 +2,17 @@
  * mp3d_synth.hip -- k_synth (ISO 11172-3
  * 2.4.3.4 + Annex A, 13818-3 2.4.3.2): requantise, stereo, alias reduction,
  * IMDCT + overlap, polyphase synthesis (matrixing on the matrix cores) ->
- * int16 / float PCM; and k_gather_frames for the frame-parallel long-stream
- * decode (§8(f) row 2).  Pipeline overview: mp3d_device.h.
+ * int16 / float PCM; k_gather_frames for the frame-parallel long-stream
+ * decode (§8(f) row 2); k_frame, the per-frame decoder's one-launch call.
+ * Pipeline overview: mp3d_device.h.
  */
 #include "mp3d_device.h"
 #include "mp3d_consts.h" /* IMDCT-12 / short window / alias coefficients as literals */
+/* the per-frame k_frame below runs the demux and Huffman stages too: this
+ * translation unit's own copies of their device code and constants */
+#define MP3D_DEMUX_TU frame_tu
+#include "mp3d_demux_dev.h"
+#include "mp3d_huffman_dev.h"
 
 namespace mp3d {
 
@@ -175,70 +181,51 @@ __device__ __forceinline__ float lane_sel(uint64_t m, float f, float t) {
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 
-template <bool SRC_XR, bool F32, bool LSF>
-/* 3 waves / SIMD (168 VGPRs).  The synth-only entry would fit 4 waves /
- * SIMD without its spectra prefetch (-3.4 % k_synth on C2, A/B XW4), but the
- * one-granule-ahead prefetch at 3 waves is worth -13 % (A/B XPF3 vs XPF4,
- * profiles/r02_ab.txt): a wave's exposed load latency costs more than a
- * fourth wave hides. */
-__global__ void __launch_bounds__(64 * SYN_WAVES) __attribute__((amdgpu_waves_per_eu(3, 8)))
-k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, const UnitMeta *__restrict__ meta,
-        const float *__restrict__ xr_in, const uint8_t *__restrict__ xr_bt, const uint8_t *__restrict__ xr_mixed,
-        const DevTables *__restrict__ tab, StreamState *__restrict__ st, void *__restrict__ pcm, int n_streams,
-        int F, int xr_nch, int xr_sr, int seg_len, float *__restrict__ st_tail) {
-    __shared__ __attribute__((aligned(16))) SynShared<LSF> T;
-    __shared__ SynWave Wv[SYN_WAVES];
+/* the workgroup's read-only tables, staged by NT threads (tid = 0 .. NT - 1;
+ * the caller's barrier follows) */
+template <bool F32, bool LSF, int NT>
+__device__ __forceinline__ void synth_tables(SynShared<LSF> &T, const DevTables *__restrict__ tab, int tid) {
     constexpr int NRATE = LSF ? 6 : 3;
-    if (!SRC_XR) {
-        /* one variant per MPEG family (StreamState.kind, fixed by k_demux):
-         * MPEG-1 takes kinds 0 / 1, LSF kind 2.  A workgroup holding no
-         * stream of its variant leaves before staging any table (the same
-         * decision in every lane: no barrier is skipped by part of it). */
-        bool any = false;
-#pragma unroll
-        for (int k = 0; k < SYN_WAVES; k++) {
-            const int sk = blockIdx.x * SYN_WAVES + k;
-            if (sk < n_streams) any |= (st[sk].kind == 2) == LSF;
-        }
-        if (!any) return;
+    static_assert(NT >= 64, "synth_tables: the LSF intensity ratios take 64 threads");
+    for (int i = tid; i < NRATE * 3 * 288; i += NT)
+        (&T.lpair[0][0][0])[i] = (&tab->lpair[LSF ? 3 : 0][0][0])[i];
+    for (int i = tid; i < 256; i += NT) {
+        const int r = i >> 4, c = i & 15;
+        T.ce[r][c] = tab->dct_c[2 * r][c];
+        T.co[r][c] = tab->dct_c[2 * r + 1][c];
     }
-    {
-        const int tid = threadIdx.x;
-        for (int i = tid; i < NRATE * 3 * 288; i += 64 * SYN_WAVES)
-            (&T.lpair[0][0][0])[i] = (&tab->lpair[LSF ? 3 : 0][0][0])[i];
-        for (int i = tid; i < 256; i += 64 * SYN_WAVES) {
-            const int r = i >> 4, c = i & 15;
-            T.ce[r][c] = tab->dct_c[2 * r][c];
-            T.co[r][c] = tab->dct_c[2 * r + 1][c];
-        }
-        for (int i = tid; i < 512; i += 64 * SYN_WAVES)
-            T.p43s[i] = i >= 256 ? tab->pow43[i - 256] : -tab->pow43[256 - i];
-        /* int16 sinks: taps x 32768 (exact, a power of two), so the sums
-         * arrive in PCM units without a multiply per sample */
-        for (int i = tid; i < 32 * 16; i += 64 * SYN_WAVES)
-            (&T.dw[0][0])[i] = (&tab->dwin[0][0])[i] * (F32 ? 1.0f : 32768.0f);
-        for (int i = tid; i < 4 * 36; i += 64 * SYN_WAVES) (&T.w36[0][0])[i] = (&c_win36[0][0])[i];
-        if (LSF) {
-            if (tid < 64) (&T.isr[0][0])[tid] = (&c_is_lsf[0][0][0])[tid];
-        } else if (tid < 14) (&T.isr[0][0])[tid] = (&c_is_ratio[0][0])[tid];
-        __syncthreads();
-    }
-    const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); /* wave-uniform (SGPR) */
-    /* Frame-parallel segments (SRC_XR): wave vs decodes frames
-     * [f0, f1) of stream s after a one-frame warm-up from zero state.  The
-     * warm-up frame's granule 0 fixes the IMDCT overlap (the last 18 outputs
-     * of a granule's IMDCT do not depend on the state), its granule 1 then
-     * yields exact S, X and the 15 carried X slots, so [f0, f1) is
-     * bit-identical to the sequential decode.  One segment (seg_len >= F):
-     * the stream's state in and out, as before. */
-    const int nseg = (F + seg_len - 1) / seg_len;
-    const int vs = blockIdx.x * SYN_WAVES + wid;
-    if (vs >= n_streams * nseg) return; /* after the only workgroup barrier */
-    const int s = vs / nseg, seg = vs - s * nseg;
+    for (int i = tid; i < 512; i += NT)
+        T.p43s[i] = i >= 256 ? tab->pow43[i - 256] : -tab->pow43[256 - i];
+    /* int16 sinks: taps x 32768 (exact, a power of two), so the sums
+     * arrive in PCM units without a multiply per sample */
+    for (int i = tid; i < 32 * 16; i += NT)
+        (&T.dw[0][0])[i] = (&tab->dwin[0][0])[i] * (F32 ? 1.0f : 32768.0f);
+    for (int i = tid; i < 4 * 36; i += NT) (&T.w36[0][0])[i] = (&c_win36[0][0])[i];
+    if (LSF) {
+        if (tid < 64) (&T.isr[0][0])[tid] = (&c_is_lsf[0][0][0])[tid];
+    } else if (tid < 14) (&T.isr[0][0])[tid] = (&c_is_ratio[0][0])[tid];
+}
+
+/* One stream (or frame segment) of k_synth's work by one wave; also the
+ * last phase of the per-frame k_frame.  Frame-parallel segments (SRC_XR;
+ * DESIGN.md §4): segment seg of nseg decodes frames [f0, f1) of stream s
+ * after a one-frame warm-up from zero state.  The warm-up frame's granule 0
+ * fixes the IMDCT overlap (the last 18 outputs of a granule's IMDCT do not
+ * depend on the state), its granule 1 then yields exact S, X and the 15
+ * carried X slots, so [f0, f1) is bit-identical to the sequential decode.
+ * One segment (seg_len >= F): the stream's state in and out.  T = the
+ * workgroup's tables (synth_tables), Wd = the wave's LDS buffer.  No
+ * workgroup barrier inside. */
+template <bool SRC_XR, bool F32, bool LSF>
+__device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf,
+                                             const UnitMeta *__restrict__ meta, const float *__restrict__ xr_in,
+                                             const uint8_t *__restrict__ xr_bt, const uint8_t *__restrict__ xr_mixed,
+                                             const DevTables *__restrict__ tab, StreamState *__restrict__ st,
+                                             void *__restrict__ pcm, int F, int xr_nch, int xr_sr, int seg_len,
+                                             float *__restrict__ st_tail, SynShared<LSF> &T, SynWave &Wd, int s,
+                                             int seg, int nseg) {
     const int f0 = seg * seg_len, f1 = min(F, f0 + seg_len);
     const int fw = seg ? f0 - 1 : 0; /* first frame decoded (warm-up below f0) */
-    if (!SRC_XR && (st[s].kind == 2) != LSF) return; /* the other variant's stream */
-    SynWave &Wd = Wv[wid];
     float *const sBuf = Wd.buf;
     const int lane = threadIdx.x & 63;
     const int ch = lane >> 5;
@@ -907,6 +894,44 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
         for (int k = 0; k < 15; k++) ffo[(ch * MP3D_FIFO_SLOTS + k) * 32 + wb] = hb[k];
     }
 }
+
+template <bool SRC_XR, bool F32, bool LSF>
+/* 3 waves / SIMD (168 VGPRs).  The synth-only entry would fit 4 waves /
+ * SIMD without its spectra prefetch (-3.4 % k_synth on C2, A/B XW4), but the
+ * one-granule-ahead prefetch at 3 waves is worth -13 % (A/B XPF3 vs XPF4,
+ * profiles/r02_ab.txt): a wave's exposed load latency costs more than a
+ * fourth wave hides. */
+__global__ void __launch_bounds__(64 * SYN_WAVES) __attribute__((amdgpu_waves_per_eu(3, 8)))
+k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, const UnitMeta *__restrict__ meta,
+        const float *__restrict__ xr_in, const uint8_t *__restrict__ xr_bt, const uint8_t *__restrict__ xr_mixed,
+        const DevTables *__restrict__ tab, StreamState *__restrict__ st, void *__restrict__ pcm, int n_streams,
+        int F, int xr_nch, int xr_sr, int seg_len, float *__restrict__ st_tail) {
+    __shared__ __attribute__((aligned(16))) SynShared<LSF> T;
+    __shared__ SynWave Wv[SYN_WAVES];
+    if (!SRC_XR) {
+        /* one variant per MPEG family (StreamState.kind, fixed by k_demux):
+         * MPEG-1 takes kinds 0 / 1, LSF kind 2.  A workgroup holding no
+         * stream of its variant leaves before staging any table (the same
+         * decision in every lane: no barrier is skipped by part of it). */
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < SYN_WAVES; k++) {
+            const int sk = blockIdx.x * SYN_WAVES + k;
+            if (sk < n_streams) any |= (st[sk].kind == 2) == LSF;
+        }
+        if (!any) return;
+    }
+    synth_tables<F32, LSF, 64 * SYN_WAVES>(T, tab, threadIdx.x);
+    __syncthreads();
+    const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); /* wave-uniform (SGPR) */
+    const int nseg = (F + seg_len - 1) / seg_len;
+    const int vs = blockIdx.x * SYN_WAVES + wid;
+    if (vs >= n_streams * nseg) return; /* after the only workgroup barrier */
+    const int s = vs / nseg, seg = vs - s * nseg;
+    if (!SRC_XR && (st[s].kind == 2) != LSF) return; /* the other variant's stream */
+    synth_stream<SRC_XR, F32, LSF>(rec, is_buf, meta, xr_in, xr_bt, xr_mixed, tab, st, pcm, F, xr_nch, xr_sr, seg_len,
+                                   st_tail, T, Wv[wid], s, seg, nseg);
+}
 /* ------------------------------------------------------------------------ */
 /* k_gather_frames: segmented long-stream decode (mp3d_batch_decode_long).  */
 /* Output frame j of the long stream is frame (j - a[k]) of virtual stream  */
@@ -932,6 +957,91 @@ __global__ void __launch_bounds__(256) k_gather_frames(const uint4 *__restrict__
 
 
 /* ------------------------------------------------------------------------ */
+/* k_frame: the per-frame decoder's call (mp3d_decode_frame) in ONE launch  */
+/* of one 256-thread workgroup.  Wave 0 stages the frame from the caller's */
+/* mapped pinned buffer into LDS (one bus round trip) and demuxes it        */
+/* (demux_stream, input from LDS) while waves 1-3 stage the Huffman and     */
+/* synthesis tables; then the four waves decode the frame's granule         */
+/* channels (huffman_wave_unit), wave 0 synthesises the PCM straight into   */
+/* the mapped output (synth_stream) and, after a system-scope fence, writes */
+/* the call's sequence number into a mapped completion word the host polls  */
+/* (no stream synchronisation).  The hand-offs between the phases use the   */
+/* batch's device buffers exactly as the three-kernel path does, so the     */
+/* results are the same bit for bit (tests/test_gpu_per_frame.py).          */
+/* ------------------------------------------------------------------------ */
+#define PF_BYTES 4096 /* = MP3D_PF_BYTES (mp3d_host.cpp): the staged stream length */
+
+template <bool F32, bool LSF>
+__global__ void __launch_bounds__(256) k_frame(const uint8_t *__restrict__ in_host, uint32_t in_have,
+                                               const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ in_len,
+                                               uint8_t *__restrict__ md, const uint64_t *__restrict__ md_off,
+                                               StreamState *__restrict__ st, FrameRec *__restrict__ rec,
+                                               uint64_t *__restrict__ sideu, DevInfo *__restrict__ infos, int opts,
+                                               const DevTables *__restrict__ tab, int16_t *__restrict__ is_buf,
+                                               UnitMeta *__restrict__ meta, void *__restrict__ pcm,
+                                               uint32_t *__restrict__ done, uint32_t seq) {
+    __shared__ __attribute__((aligned(16))) SynShared<LSF> T;
+    __shared__ SynWave Wv[1];
+    __shared__ __attribute__((aligned(16))) uint16_t s_lut[MP3D_LUT_MAX];
+    __shared__ __attribute__((aligned(16))) uint32_t s_bits[HW_UNITS][HW_WORDS + 4];
+    __shared__ uint32_t s_tsel[32];
+    __shared__ uint16_t s_lbnd[9][24];
+    __shared__ uint8_t s_slen[32];
+    __shared__ __attribute__((aligned(16))) uint32_t s_in[PF_BYTES / 4];
+    static_assert(PF_BYTES == 256 * 16 && MP3D_MAX_FRAME_BYTES <= 128 * 16, "k_frame: frame staging by wave 0");
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (wv == 0) {
+        /* wave 0: the stream state's first lines into the cache (the demux
+         * reads them after the frame has arrived), then the frame's bytes
+         * [0, in_have) from the mapped buffer, 16 B per lane and chunk (one
+         * bus round trip), zeros after them (the host does not clear the
+         * pinned buffer's tail); then the demux, reading the frame from LDS
+         * (the wave's own stores: no barrier) */
+        const uint4 sp = ((const uint4 *)st)[lane];
+        __asm__ volatile("" ::"v"(sp.x), "v"(sp.y), "v"(sp.z), "v"(sp.w));
+        const uint32_t n16 = (in_have + 15u) / 16u; /* <= 91 (1441-B frame) */
+        uint4 v[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const uint32_t c = (uint32_t)lane + 64u * k;
+            v[k] = c < n16 ? ((const uint4 *)in_host)[c] : make_uint4(0u, 0u, 0u, 0u);
+            if (c + 1u == n16 && (in_have & 15u)) {
+                /* bytes past in_have inside the last chunk read as zeros */
+                const uint32_t keep = in_have & 15u;
+                uint32_t *w = (uint32_t *)&v[k];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int nb = (int)keep - 4 * q; /* bytes of word q kept */
+                    w[q] = nb >= 4 ? w[q] : nb <= 0 ? 0u : w[q] & (0xFFFFFFFFu >> (32 - 8 * nb));
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) ((uint4 *)s_in)[lane + 64 * k] = k < 2 ? v[k] : make_uint4(0u, 0u, 0u, 0u);
+        wave_sync();
+        demux_stream((const uint8_t *)s_in, in_off, in_len, md, md_off, st, rec, sideu, infos, 1, opts, 0, lane);
+    } else {
+        /* waves 1..3 meanwhile: the Huffman and synthesis tables */
+        huff_tables<192>(tab, s_lut, s_tsel, s_lbnd, s_slen, tid - 64);
+        synth_tables<F32, LSF, 192>(T, tab, tid - 64);
+    }
+    __syncthreads(); /* rec, side words, md region and state visible to the workgroup */
+    huffman_wave_unit(md, md_off, rec, sideu, tab, is_buf, meta, 1, wv, lane, s_bits[wv], s_lut, s_tsel, s_lbnd,
+                      s_slen);
+    __syncthreads(); /* is[] rows and UnitMeta visible to wave 0 */
+    if (wv == 0) {
+        /* a frame of the other MPEG family than the stream's was skipped as
+         * junk by the demux: no audio (as k_synth's variant check) */
+        if ((st[0].kind == 2) == LSF)
+            synth_stream<false, F32, LSF>(rec, is_buf, meta, nullptr, nullptr, nullptr, tab, st, pcm, 1, 2, 0, 1,
+                                          nullptr, T, Wv[0], 0, 0, 1);
+        __threadfence_system(); /* PCM, frame info and state before the completion word */
+        if (lane == 0) __hip_atomic_store(done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+/* ------------------------------------------------------------------------ */
 /* Host-side launchers                                                       */
 /* ------------------------------------------------------------------------ */
 hipError_t upload_synth_constants(const float *win36, const float *is_ratio, const float *pow2q, const float *is_lsf) {
@@ -940,6 +1050,26 @@ hipError_t upload_synth_constants(const float *win36, const float *is_ratio, con
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_is_ratio), is_ratio, sizeof(float) * 14))) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_pow2q), pow2q, sizeof(float) * 4))) return e;
     return hipMemcpyToSymbol(HIP_SYMBOL(c_is_lsf), is_lsf, sizeof(float) * 64);
+}
+
+/* k_frame's copies of the demux constants (this translation unit's) */
+hipError_t upload_frame_constants(const uint16_t *frame_bytes) { return upload_demux_tables(frame_bytes); }
+
+void launch_frame(const uint8_t *in_host, uint32_t in_have, const uint64_t *in_off, const uint32_t *in_len,
+                  uint8_t *md, const uint64_t *md_off, StreamState *st, FrameRec *rec, uint64_t *sideu, void *infos,
+                  int opts, const DevTables *tab, int16_t *is_buf, UnitMeta *meta, void *pcm, bool f32, bool lsf,
+                  uint32_t *done, uint32_t seq, hipStream_t strm) {
+#define MP3D_FRAME_LAUNCH(F32_, LSF_)                                                                              \
+    hipLaunchKernelGGL((k_frame<F32_, LSF_>), dim3(1), dim3(256), 0, strm, in_host, in_have, in_off, in_len, md,    \
+                       md_off, st, rec, sideu, (DevInfo *)infos, opts, tab, is_buf, meta, pcm, done, seq)
+    if (f32) {
+        if (lsf) MP3D_FRAME_LAUNCH(true, true);
+        else MP3D_FRAME_LAUNCH(true, false);
+    } else {
+        if (lsf) MP3D_FRAME_LAUNCH(false, true);
+        else MP3D_FRAME_LAUNCH(false, false);
+    }
+#undef MP3D_FRAME_LAUNCH
 }
 
 void launch_synth(const FrameRec *rec, const int16_t *is_buf, const UnitMeta *meta, const DevTables *tab,
