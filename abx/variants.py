@@ -82,9 +82,22 @@ VARS = {
             ("        __threadfence_system(); /* PCM, frame info and state before the completion word */\n",
              "        FT(11);\n        __threadfence_system(); /* PCM, frame info and state before the completion word */\n        FT(12);\n"
              "        if (lane == 0) g_fdbg[21] = __builtin_amdgcn_s_memrealtime();\n"),
+            ("#define HW_WORDS 520 /* staged md words per unit: four 4095-bit units + margin */\n",
+             "#define HW_WORDS 520 /* staged md words per unit: four 4095-bit units + margin */\n"
+             "static __device__ unsigned long long g_hdbg[32];\n"
+             "#define HT(i) do { __asm__ volatile(\"s_waitcnt vmcnt(0) lgkmcnt(0)\" ::: \"memory\"); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (lane == 0) g_hdbg[(u & 3) * 8 + (i)] = t_; } while (0)\n"),
+            ("    wave_sync();\n    const uint32_t seg = 0u - 32u * w0; /* md bit -> staged bit */\n",
+             "    wave_sync();\n    HT(0);\n    const uint32_t seg = 0u - 32u * w0; /* md bit -> staged bit */\n"),
+            ("    const int ws = (int)(side >> 30) & 1;\n    const int bv2 = 2 * ((int)(side >> 43) & 0x1FF);\n    int r1, r2;",
+             "    HT(1);\n    const int ws = (int)(side >> 30) & 1;\n    const int bv2 = 2 * ((int)(side >> 43) & 0x1FF);\n    int r1, r2;"),
+            ("    /* count1 quadruples until the part2_3 end (one per 2 words)",
+             "    HT(2);\n    /* count1 quadruples until the part2_3 end (one per 2 words)"),
+            ("\n    if (lane == 0) {\n        UnitMeta m;\n", "\n    HT(3);\n    if (lane == 0) {\n        UnitMeta m;\n"),
             ("""/* k_frame's copies of the demux constants (this translation unit's) */""",
              """extern "C" __attribute__((visibility("default"))) int mp3d_dbg_read(unsigned long long *h) {
-    return (int)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_fdbg), sizeof(g_fdbg), 0, hipMemcpyDeviceToHost);
+    hipError_t e = hipMemcpyFromSymbol(h, HIP_SYMBOL(g_fdbg), sizeof(g_fdbg), 0, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(h + 32, HIP_SYMBOL(g_hdbg), sizeof(g_hdbg), 0, hipMemcpyDeviceToHost);
+    return (int)e;
 }
 /* k_frame's copies of the demux constants (this translation unit's) */""")],
     "HB": [("""                            const uint32_t i2 = (e1 & 0x8000u) ? sub : i1;

@@ -4,17 +4,32 @@
  * on the GPU with mp3d_decode_frame, optionally applies the LAME gapless trim
  * (mp3d_dec_stream_info), and writes a 16-bit PCM WAV file.
  *
- *   mp3d_play in.mp3 out.wav [--gapless] [--crc]
+ *   mp3d_play in.mp3 out.wav [--gapless] [--crc] [--time]
+ *
+ * --time prints the median and p99 wall time of the mp3d_decode_frame calls
+ * (after 20 warm-up frames) to stderr: the per-frame latency as a C caller
+ * sees it.
  *
  * Build: make -C examples (gcc, links mp3_amd/libmp3d.so).  Exit status 0 on
  * success, 1 on a usage / file error, 2 when the library reports an error
  * (no GPU: MP3D_E_NO_DEVICE -- there is no CPU fallback). */
 #include <stdint.h>
 #include <stdio.h>
+#include <time.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "mp3d.h"
+
+static double now_us(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec * 1e6 + (double)t.tv_nsec * 1e-3;
+}
+static int cmp_d(const void *a, const void *b) {
+    const double x = *(const double *)a, y = *(const double *)b;
+    return (x > y) - (x < y);
+}
 
 static void put_u32(FILE *f, uint32_t v) {
     const uint8_t b[4] = {(uint8_t)v, (uint8_t)(v >> 8), (uint8_t)(v >> 16), (uint8_t)(v >> 24)};
@@ -46,14 +61,15 @@ static int write_wav(const char *path, const int16_t *pcm, long long frames, int
 }
 
 int main(int argc, char **argv) {
-    int gapless = 0, crc = 0;
+    int gapless = 0, crc = 0, timing = 0;
     if (argc < 3) {
-        fprintf(stderr, "usage: %s in.mp3 out.wav [--gapless] [--crc]\n", argv[0]);
+        fprintf(stderr, "usage: %s in.mp3 out.wav [--gapless] [--crc] [--time]\n", argv[0]);
         return 1;
     }
     for (int i = 3; i < argc; i++) {
         if (!strcmp(argv[i], "--gapless")) gapless = 1;
         else if (!strcmp(argv[i], "--crc")) crc = 1;
+        else if (!strcmp(argv[i], "--time")) timing = 1;
     }
     FILE *f = fopen(argv[1], "rb");
     if (!f) { perror(argv[1]); return 1; }
@@ -76,8 +92,12 @@ int main(int argc, char **argv) {
     int16_t frame[2304];
     mp3d_frame_info info;
     size_t pos = 0;
+    long n_lat = 0;
+    double *lat = (double *)malloc(sizeof(double) * ((size_t)len / 24 + 2)); /* >= frames in the file */
     while (pos < (size_t)len) {
+        const double t0 = timing ? now_us() : 0.0;
         const int got = mp3d_decode_frame(dec, buf + pos, (size_t)len - pos, frame, &info);
+        if (timing) lat[n_lat++] = now_us() - t0;
         if (got == MP3D_E_NEED_MORE) break; /* no complete frame left */
         if (got < 0) { fprintf(stderr, "mp3d_decode_frame: %s\n", mp3d_strerror(got)); return 2; }
         if (info.frame_bytes <= 0) break;
@@ -103,6 +123,13 @@ int main(int argc, char **argv) {
         }
     }
     mp3d_dec_destroy(dec);
+    if (timing && n_lat > 40) {
+        qsort(lat + 20, (size_t)(n_lat - 20), sizeof(double), cmp_d);
+        const long m = n_lat - 20;
+        fprintf(stderr, "mp3d_decode_frame: %ld calls, median %.2f us, p99 %.2f us\n", m, lat[20 + m / 2],
+                lat[20 + (m * 99) / 100]);
+    }
+    free(lat);
     if (!nch) nch = 2, hz = 44100; /* no audio: an empty WAV */
     rc = write_wav(argv[2], pcm + start * nch, stop - start, nch, hz);
     free(pcm);

@@ -115,8 +115,8 @@ __device__ __forceinline__ uint32_t read_sf(const uint32_t *bits, uint32_t pos, 
  * short bands from sf[8]).  LSF units only -- off the MPEG-1 path, so the
  * plain per-byte global stores are fine.  *preflag = scalefac_compress >= 500. */
 typedef const __attribute__((address_space(3))) uint32_t *lds_cu32;
-__device__ __attribute__((noinline)) uint32_t read_sf_lsf(lds_cu32 bits, uint32_t pos, uint64_t side, uint8_t *sf,
-                                                          int *preflag) {
+__device__ __forceinline__ uint32_t read_sf_lsf_i(lds_cu32 bits, uint32_t pos, uint64_t side, uint8_t *sf,
+                                                   int *preflag) {
     const int ws = (int)(side >> 30) & 1, bt = ws ? (int)(side >> 28) & 3 : 0;
     const int tindex = bt == 2 ? (((side >> 27) & 1) ? 2 : 1) : 0;
     const bool is_right = (side >> 7) & 1;
@@ -156,6 +156,13 @@ __device__ __attribute__((noinline)) uint32_t read_sf_lsf(lds_cu32 bits, uint32_
         }
     }
     return pos;
+}
+/* k_huffman's call: out of line, so its registers stay out of the kernel's
+ * allocation (the one-wave-per-unit decode inlines read_sf_lsf_i: no call,
+ * no stack) */
+__device__ __attribute__((noinline)) uint32_t read_sf_lsf(lds_cu32 bits, uint32_t pos, uint64_t side, uint8_t *sf,
+                                                          int *preflag) {
+    return read_sf_lsf_i(bits, pos, side, sf, preflag);
 }
 
 /* the block's LDS tables: the LUT (the whole array: past the last table it
@@ -235,6 +242,19 @@ __device__ __forceinline__ void hw_win64(const uint32_t *bits, uint32_t pos, uin
     const uint32_t w0 = bits[w], w1 = bits[w + 1], w2 = bits[w + 2];
     hi = (uint32_t)((((uint64_t)w0 << 32) | w1) >> sh);
     lo = (uint32_t)((((uint64_t)w1 << 32) | w2) >> sh);
+}
+
+/* m with bit i set (i < 64, wave-uniform): one scalar instruction */
+__device__ __forceinline__ uint64_t set_bit64(uint64_t m, uint32_t i) {
+    __asm__("s_bitset1_b64 %0, %1" : "+s"(m) : "s"(i));
+    return m;
+}
+
+/* position of the set bit of rank k (k < popcount(m)) of a wave-uniform mask */
+__device__ __forceinline__ uint32_t kth_bit(uint64_t m, int k, int lane) {
+    const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    const bool sel = ((m >> lane) & 1u) && r == (uint32_t)k;
+    return (uint32_t)__builtin_ctzll(__ballot(sel));
 }
 
 /* one big_values pair at bit p with table word ts (the k_huffman pair decode):
@@ -339,7 +359,7 @@ __device__ __forceinline__ void huffman_wave_unit(const uint8_t *__restrict__ md
     int lsf_pre = 0;
     if (r.lsf) {
         uint32_t p0 = 0;
-        if (lane == 0) p0 = read_sf_lsf((lds_cu32)bits, pos, side, (uint8_t *)&meta[u], &lsf_pre);
+        if (lane == 0) p0 = read_sf_lsf_i((lds_cu32)bits, pos, side, (uint8_t *)&meta[u], &lsf_pre);
         pos = (uint32_t)__builtin_amdgcn_readlane((int)p0, 0);
         lsf_pre = __builtin_amdgcn_readlane(lsf_pre, 0);
     } else {
@@ -416,20 +436,35 @@ __device__ __forceinline__ void huffman_wave_unit(const uint8_t *__restrict__ md
         hw_pair(s_lut, bits, pos + 64u + (uint32_t)lane, ts, tl1, wd1);
         /* a pair starts before the part2_3 end; at most 128 bits a round */
         const uint32_t lim = end_bit - pos < 128u ? end_bit - pos : 128u;
-        int left = (kend - k) / 2;
+        /* the hop loops test only the bit position (5 scalar-side
+         * instructions a codeword); a region ending inside the round is cut
+         * afterwards: its first `left` codewords stay, and the next one
+         * starts at the start mark of rank `left` */
+        const uint32_t lim0 = lim < 64u ? lim : 64u;
         uint64_t m0 = 0, m1 = 0;
         uint32_t o = 0;
         do {
-            m0 |= 1ull << o;
+            m0 = set_bit64(m0, o);
             o += (uint32_t)__builtin_amdgcn_readlane((int)tl0, (int)o);
-            left--;
-        } while (left > 0 && o < 64u && o < lim);
-        if (left > 0 && o < lim) {
+        } while (o < lim0);
+        if (o < lim) {
             do {
-                m1 |= 1ull << (o - 64u);
-                o += (uint32_t)__builtin_amdgcn_readlane((int)tl1, (int)(o - 64u));
-                left--;
-            } while (left > 0 && o < lim);
+                m1 = set_bit64(m1, o & 63u);
+                o += (uint32_t)__builtin_amdgcn_readlane((int)tl1, (int)(o & 63u));
+            } while (o < lim);
+        }
+        const int left = (kend - k) / 2;
+        if (__builtin_popcountll(m0) + __builtin_popcountll(m1) > left) {
+            const int c0 = __builtin_popcountll(m0);
+            if (left < c0) {
+                o = kth_bit(m0, left, lane);
+                m0 &= (1ull << o) - 1ull;
+                m1 = 0;
+            } else {
+                const uint32_t b = kth_bit(m1, left - c0, lane);
+                m1 &= (1ull << b) - 1ull;
+                o = 64u + b;
+            }
         }
         const uint32_t r0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
         const uint32_t rk1 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
@@ -470,7 +505,7 @@ __device__ __forceinline__ void huffman_wave_unit(const uint8_t *__restrict__ md
         const uint32_t wb = (uint32_t)(uint16_t)q2 | ((uint32_t)(uint16_t)q3 << 16);
         /* a quadruple ends at or before the part2_3 end */
         const uint32_t lim = end_bit - pos;
-        int left = (572 - k) / 4 + 1;
+        const uint32_t lim0 = lim < 64u ? lim : 64u;
         uint64_t m = 0;
         uint32_t o = 0;
         bool over = false;
@@ -480,10 +515,16 @@ __device__ __forceinline__ void huffman_wave_unit(const uint8_t *__restrict__ md
                 over = true;
                 break;
             }
-            m |= 1ull << o;
+            m = set_bit64(m, o);
             o += t;
-            left--;
-        } while (left > 0 && o < 64u && o < lim);
+        } while (o < lim0);
+        /* quadruples only up to line 575 (k <= 572): cut as above */
+        const int left = (572 - k) / 4 + 1;
+        if (__builtin_popcountll(m) > left) {
+            o = kth_bit(m, left, lane);
+            m &= (1ull << o) - 1ull;
+            over = false;
+        }
         const uint32_t rq = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         const int nq = __builtin_popcountll(m);
         if ((m >> lane) & 1u) *(uint2 *)(row + nw + 2 * (int)rq) = make_uint2(wa, wb);

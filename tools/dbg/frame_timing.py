@@ -29,7 +29,7 @@ def main():
     d = mp3_amd.Decoder()
     pcm = np.zeros(2304, np.int16)
     info = mp3_amd.FrameInfo()
-    dbg = np.zeros(32, np.uint64)
+    dbg = np.zeros(64, np.uint64)
     rows, lat = [], []
     pos = 0
     for f in range(len(offs)):
@@ -49,6 +49,10 @@ def main():
            "barrier1_us": us(2, 5), "huff_wave_us": [us(5, 6 + w) for w in range(4)], "barrier3_us": us(5, 10),
            "synth_us": us(10, 11), "fence_us": us(11, 12), "kernel_us": us(0, 12),
            "call_median_us": float(np.median(np.array(lat[20:]) * 1e6))}
+    h = a[:, 32:].reshape(len(a), 4, 8)  # per unit: staged, scalefactors, big_values, count1 stamps
+    hu = lambda x: [round(float(np.median(x[:, w])) / ghz / 1e3, 2) for w in range(4)]
+    out["huff_unit_us"] = {"until_staged": hu(h[:, :, 0] - a[:, 5:6]), "scalefactors": hu(h[:, :, 1] - h[:, :, 0]),
+                           "big_values": hu(h[:, :, 2] - h[:, :, 1]), "count1": hu(h[:, :, 3] - h[:, :, 2])}
     print(json.dumps(out))
 
 
