@@ -62,6 +62,7 @@ VARS = {
     "HTOLD": [("/* the block's LDS tables: the LUT (the whole array: past the last table it\n * holds the zero table of table_select 0, 4, 14), table_select -> LUT base |\n * bits1 << 16 | linbits << 24, long sfb start lines per sample-rate index,\n * MPEG-1 slen pairs.  Every load is independent (one memory latency).\n * Both Huffman kernels run 256-thread blocks. */\n__device__ __forceinline__ void huff_tables(const DevTables *tab, uint16_t *s_lut, uint32_t *s_tsel,\n                                            uint16_t (*s_lbnd)[24], uint8_t *s_slen) {\n    constexpr int LUT4 = MP3D_LUT_MAX / 8; /* uint4 chunks */\n    constexpr int PER = (LUT4 + 255) / 256;\n    const uint4 *src = (const uint4 *)tab->lut;\n    uint4 v[PER];\n#pragma unroll\n    for (int j = 0; j < PER; j++) {\n        const int i = (int)threadIdx.x + 256 * j;\n        if (i < LUT4) v[j] = src[i];\n    }\n    uint32_t ts = 0u, lb = 0u;\n    if (threadIdx.x < 32) ts = tab->tsel[threadIdx.x];\n    if (threadIdx.x < 9 * 24 / 2) lb = ((const uint32_t *)tab->lbnd)[threadIdx.x];\n#pragma unroll\n    for (int j = 0; j < PER; j++) {\n        const int i = (int)threadIdx.x + 256 * j;\n        if (i < LUT4) ((uint4 *)s_lut)[i] = v[j];\n    }\n    if (threadIdx.x < 32) s_tsel[threadIdx.x] = ts;\n    if (threadIdx.x < 9 * 24 / 2) ((uint32_t *)s_lbnd)[threadIdx.x] = lb;\n    if (threadIdx.x < 32) s_slen[threadIdx.x] = MP3D_SLEN[threadIdx.x >> 4][threadIdx.x & 15];\n}\n", "/* the block's LDS tables: the LUT (+ a 2-entry all-zero table for\n * table_select 0, 4, 14), table_select -> LUT base | bits1 << 16 | linbits\n * << 24, long sfb start lines per sample-rate index, MPEG-1 slen pairs */\n__device__ __forceinline__ void huff_tables(const DevTables *tab, uint16_t *s_lut, uint32_t *s_tsel,\n                                            uint16_t (*s_lbnd)[24], uint8_t *s_slen) {\n    const int lut_n = tab->lut_hdr.base[MP3D_LUT_TABLES - 1] + (1 << tab->lut_hdr.bits1[MP3D_LUT_TABLES - 1]);\n    const int zbase = (lut_n + 1) & ~1;\n    for (int i = threadIdx.x; i < (lut_n + 1) / 2; i += blockDim.x)\n        ((uint32_t *)s_lut)[i] = ((const uint32_t *)tab->lut)[i];\n    if (threadIdx.x == 0) ((uint32_t *)s_lut)[zbase / 2] = 0u;\n    if (threadIdx.x < 9) {\n        int acc = 0;\n        for (int i = 0; i < 22; i++) {\n            s_lbnd[threadIdx.x][i] = (uint16_t)acc;\n            acc += MP3D_SFB_LONG_WIDTH[threadIdx.x][i];\n        }\n        s_lbnd[threadIdx.x][22] = (uint16_t)acc;\n    }\n    if (threadIdx.x < 32) s_slen[threadIdx.x] = MP3D_SLEN[threadIdx.x >> 4][threadIdx.x & 15];\n    if (threadIdx.x < 32) {\n        const int t = MP3D_HTAB_OF_SELECT[threadIdx.x];\n        s_tsel[threadIdx.x] = t < 0 ? (uint32_t)zbase | (1u << 16)\n                                    : (uint32_t)tab->lut_hdr.base[t] | ((uint32_t)tab->lut_hdr.bits1[t] << 16) |\n                                          ((uint32_t)MP3D_LINBITS[threadIdx.x] << 24);\n    }\n}\n")],
     "NOW": [],
     "NOW2": [],
+    "NOW3": [],
     # r02 diagnostic (same output): k_frame phase timestamps (s_memtime) in g_fdbg, read by
     # tools/dbg/frame_timing.py through mp3d_dbg_read
     "FRT": [("#define PF_BYTES 4096 /* = MP3D_PF_BYTES (mp3d_host.cpp): the staged stream length */\n",
@@ -100,6 +101,7 @@ VARS = {
     return (int)e;
 }
 /* k_frame's copies of the demux constants (this translation unit's) */""")],
+    "WP": [('                    for (; __ballot(k < bv2); k += 8) {\n                        uint32_t wv[4];\n#pragma unroll\n                        for (int j = 0; j < 4; j++) {\n                            const int kk = k + 2 * j;\n                            const uint32_t ts = kk < r1 ? ts0 : (kk < r2 ? ts1 : ts2);\n                            const uint32_t tb = ts & 0xFFFFu, b1 = (ts >> 16) & 15u, lin = ts >> 24;\n                            uint32_t hi, lo;\n                            win64(bits, pos, hi, lo);\n', '                    uint32_t W = min(pos >> 5, (uint32_t)(HUFF_CAPW - 2));\n                    uint32_t q0 = bits[W], q1 = bits[W + 1], q2 = bits[W + 2], q3 = bits[W + 3], q4 = bits[W + 4];\n                    for (; __ballot(k < bv2); k += 8) {\n                        uint32_t wv[4];\n#pragma unroll\n                        for (int j = 0; j < 4; j++) {\n                            const int kk = k + 2 * j;\n                            const uint32_t ts = kk < r1 ? ts0 : (kk < r2 ? ts1 : ts2);\n                            const uint32_t tb = ts & 0xFFFFu, b1 = (ts >> 16) & 15u, lin = ts >> 24;\n                            const uint32_t d = (pos >> 5) - W;\n                            const uint32_t w0 = d == 0u ? q0 : (d == 1u ? q1 : q2);\n                            const uint32_t w1 = d == 0u ? q1 : (d == 1u ? q2 : q3);\n                            const uint32_t w2 = d == 0u ? q2 : (d == 1u ? q3 : q4);\n                            W = min(pos >> 5, (uint32_t)(HUFF_CAPW - 2));\n                            q0 = bits[W]; q1 = bits[W + 1]; q2 = bits[W + 2]; q3 = bits[W + 3]; q4 = bits[W + 4];\n                            const uint32_t shw = 32u - (pos & 31u);\n                            const uint32_t hi = (uint32_t)((((uint64_t)w0 << 32) | w1) >> shw);\n                            const uint32_t lo = (uint32_t)((((uint64_t)w1 << 32) | w2) >> shw);\n')],
     "HB": [("""                            const uint32_t i2 = (e1 & 0x8000u) ? sub : i1;
                             const uint32_t e = s_lut[i2];""", """                            uint32_t e = e1;
                             if (__ballot(e1 & 0x8000u)) e = s_lut[(e1 & 0x8000u) ? sub : i1];""")],
