@@ -129,7 +129,7 @@ static void build_huffman_lut(DevTables &t) {
     /* table_select 0, 4, 14: a 2-entry all-zero table (zero-length leaves)
      * right after the last table (t.lut is zeroed past lut.size()) */
     const size_t zbase = (lut.size() + 1) & ~(size_t)1;
-    if (zbase + 2 > MP3D_LUT_MAX) {
+    if (zbase + 2 + 16 > MP3D_LUT_MAX) { /* + count1 table B in k_huffman's LDS copy */
         fprintf(stderr, "mp3d: LUT overflow %zu\n", zbase + 2);
         abort();
     }

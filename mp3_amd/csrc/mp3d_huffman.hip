@@ -15,16 +15,20 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                                                         const DevTables *__restrict__ tab, int16_t *__restrict__ is_buf,
                                                         UnitMeta *__restrict__ meta, int n_units, int F) {
     __shared__ __attribute__((aligned(16))) uint16_t s_lut[MP3D_LUT_MAX];
-    __shared__ __attribute__((aligned(16))) uint32_t s_bits[HUFF_WAVES][HUFF_CAPW + 4];
-    __shared__ uint32_t s_tsel[32]; /* table_select -> LUT base | bits1 << 16 | linbits << 24 */
+    /* per-wave staging areas after a 4-word guard: win64g / win32g read the
+     * word below a window that starts on a word boundary */
+    __shared__ __attribute__((aligned(16))) uint32_t s_bits[4 + HUFF_WAVES * (HUFF_CAPW + 4)];
+    __shared__ uint32_t s_tsel[32]; /* table_select -> LUT base | (32 - bits1) << 16 | linbits << 24 */
     __shared__ uint16_t s_lbnd[9][24]; /* long sfb start line per sample-rate index (23 bounds) */
     __shared__ uint8_t s_slen[32];     /* MPEG-1 slen1 | slen2 per scalefac_compress          */
     huff_tables_lane(tab, s_lut, s_tsel, s_lbnd, s_slen);
     __syncthreads();
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint32_t *bits = s_bits[wv];
+    uint32_t *bits = s_bits + 4 + wv * (HUFF_CAPW + 4);
     const uint32_t qbase = tab->lut_hdr.base[MP3D_LUT_TABLES - 1];
     const int qb1 = tab->lut_hdr.bits1[MP3D_LUT_TABLES - 1];
+    /* count1 table B: after the zero table (huff_tables_lane) */
+    const uint32_t c1b_base = ((qbase + (1u << qb1) + 1u) & ~1u) + MP3D_C1B_OFF;
     const int n_super = (n_units + HUFF_SUPER - 1) / HUFF_SUPER;
 
     for (int sc = blockIdx.x * HUFF_WAVES + wv; sc < n_super; sc += gridDim.x * HUFF_WAVES) {
@@ -210,15 +214,16 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                         for (int j = 0; j < 4; j++) {
                             const int kk = k + 2 * j;
                             const uint32_t ts = kk < r1 ? ts0 : (kk < r2 ? ts1 : ts2);
-                            const uint32_t tb = ts & 0xFFFFu, b1 = (ts >> 16) & 15u, lin = ts >> 24;
+                            const uint32_t tb = ts & 0xFFFFu, s1 = (ts >> 16) & 63u, lin = ts >> 24;
                             uint32_t hi, lo;
-                            win64(bits, pos, hi, lo);
-                            const uint32_t i1 = tb + (hi >> (32 - b1));
+                            win64g(bits, pos, hi, lo);
+                            const uint32_t i1 = tb + (hi >> s1);
                             const uint32_t e1 = s_lut[i1];
                             /* second level, branch-free: i2 = i1 for a leaf */
                             const uint32_t nb = (e1 >> 11) & 15u;
-                            const uint32_t sub =
-                                ((e1 & 0x7FFu) << 2) + (uint32_t)((((uint64_t)hi << b1) & 0xFFFFFFFFull) >> (32u - nb));
+                            /* the nb bits after the first level's b1 = 32 - s1: (hi << b1) >> (32 - nb); a
+                             * zero-width field (leaf, nb = 0) extracts 0 */
+                            const uint32_t sub = ((e1 & 0x7FFu) << 2) + __builtin_amdgcn_ubfe(hi, s1 - nb, nb);
                             const uint32_t i2 = (e1 & 0x8000u) ? sub : i1;
                             const uint32_t e = s_lut[i2];
                             const uint32_t x = (e >> 4) & 15u, y = e & 15u, len_c = (e >> 8) & 31u;
@@ -226,21 +231,21 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                             /* after the code: [x linbits][x sign][y linbits][y sign],
                              * <= 28 bits, all in the window (code <= 19 bits); a
                              * zero-width field extracts 0 (v_bfe_u32) */
-                            const uint32_t rb = shl64hi(hi, lo, len_c);
+                            /* len_c = 0 only for table 0, whose x = y = 0 need no bits */
+                            const uint32_t rb = shl64hi_a(hi, lo, len_c);
                             const uint32_t nx = x == 15u ? lin : 0u, ny = y == 15u ? lin : 0u;
-                            const uint32_t ex = __builtin_amdgcn_ubfe(rb, 32u - nx, nx);
-                            const uint32_t q1 = nx + sx;
-                            const uint32_t sgx = __builtin_amdgcn_ubfe(rb, 32u - q1, 1u);
-                            const uint32_t ey = __builtin_amdgcn_ubfe(rb, 32u - q1 - ny, ny);
-                            const uint32_t q2 = q1 + ny + sy;
-                            const uint32_t sgy = __builtin_amdgcn_ubfe(rb, 32u - q2, 1u);
+                            /* field offsets counted down from the top of rb */
+                            const uint32_t t0 = 32u - nx, t1 = t0 - sx, t2 = t1 - ny, t3 = t2 - sy;
+                            const uint32_t ex = __builtin_amdgcn_ubfe(rb, t0, nx);
+                            const uint32_t ey = __builtin_amdgcn_ubfe(rb, t2, ny);
+                            /* sign bits as 0 / -1 masks (signed 1-bit fields): v = (v ^ m) - m */
+                            const int mx = __builtin_amdgcn_sbfe((int)rb, t1, 1u), my = __builtin_amdgcn_sbfe((int)rb, t3, 1u);
                             const bool live = kk < bv2 && pos < end_bit;
-                            pos += live ? len_c + q2 : 0u;
+                            pos += live ? len_c + (32u - t3) : 0u;
                             /* x = 0 gives X = 0 whatever the (absent) sign bit */
-                            int X = (int)(x + ex), Y = (int)(y + ey);
-                            X = sgx ? -X : X;
-                            Y = sgy ? -Y : Y;
-                            wv[j] = live ? (uint32_t)(uint16_t)X | ((uint32_t)(uint16_t)Y << 16) : 0u;
+                            const int X = ((int)(x + ex) ^ mx) - mx, Y = ((int)(y + ey) ^ my) - my;
+                            /* low halves of X and Y -> one word (v_perm_b32) */
+                            wv[j] = live ? __builtin_amdgcn_perm((uint32_t)Y, (uint32_t)X, 0x05040100u) : 0u;
                         }
                         *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
                     }
@@ -248,30 +253,30 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                     /* count1 quadruples until the part2_3 end; a quadruple that
                      * overreads it is discarded (FFmpeg); one
                      * 8-B store each (lines k .. k + 3) */
+                    /* table A or B (count1table_select) as one LUT read, no branch */
                     const bool c1b = (side >> 5) & 1;
+                    const uint32_t c1base = c1b ? c1b_base : qbase, c1sh = c1b ? 28u : 32u - (uint32_t)qb1;
                     while (k <= 572 && pos < end_bit) {
-                        const uint32_t hw = win32(bits, pos);
-                        uint32_t v, lq;
-                        if (c1b) {
-                            v = 15u - (hw >> 28);
-                            lq = 4u;
-                        } else {
-                            const uint32_t e = s_lut[qbase + (hw >> (32 - qb1))];
-                            v = e & 15u;
-                            lq = (e >> 8) & 31u;
-                        }
+                        const uint32_t hw = win32g(bits, pos);
+                        const uint32_t e = s_lut[c1base + (hw >> c1sh)];
+                        const uint32_t v = e & 15u, lq = (e >> 8) & 31u;
                         const uint32_t ns = __builtin_popcount(v);
                         if (pos + lq + ns > end_bit) break;
-                        const uint32_t sbits = (hw << lq) >> (32 - (ns ? ns : 1));
-                        int bit = (int)ns;
-                        int q0 = (v >> 3) & 1, q1 = (v >> 2) & 1, q2 = (v >> 1) & 1, q3 = v & 1;
-                        if (q0) { bit--; if ((sbits >> bit) & 1) q0 = -1; }
-                        if (q1) { bit--; if ((sbits >> bit) & 1) q1 = -1; }
-                        if (q2) { bit--; if ((sbits >> bit) & 1) q2 = -1; }
-                        if (q3) { bit--; if ((sbits >> bit) & 1) q3 = -1; }
+                        /* value i's sign bit follows the signs of the nonzero
+                         * values before it: offsets from the top of rb by
+                         * prefix counts of v (bit 3 = value 0); masks 0 / -1 */
+                        const uint32_t rb = hw << lq;
+                        const uint32_t p1 = v >> 3, p2 = __builtin_popcount(v >> 2), p3 = __builtin_popcount(v >> 1);
+                        const int m0 = __builtin_amdgcn_sbfe((int)rb, 31u, 1u);
+                        const int m1 = __builtin_amdgcn_sbfe((int)rb, 31u - p1, 1u);
+                        const int m2 = __builtin_amdgcn_sbfe((int)rb, 31u - p2, 1u);
+                        const int m3 = __builtin_amdgcn_sbfe((int)rb, 31u - p3, 1u);
+                        /* a zero value stays 0 whatever mask it meets */
+                        const int q0 = ((int)p1 ^ m0) - m0, q1 = ((int)((v >> 2) & 1u) ^ m1) - m1;
+                        const int q2 = ((int)((v >> 1) & 1u) ^ m2) - m2, q3 = ((int)(v & 1u) ^ m3) - m3;
                         pos += lq + ns;
-                        *(uint2 *)(row + k) = make_uint2((uint32_t)(uint16_t)q0 | ((uint32_t)(uint16_t)q1 << 16),
-                                                         (uint32_t)(uint16_t)q2 | ((uint32_t)(uint16_t)q3 << 16));
+                        *(uint2 *)(row + k) = make_uint2(__builtin_amdgcn_perm((uint32_t)q1, (uint32_t)q0, 0x05040100u),
+                                                         __builtin_amdgcn_perm((uint32_t)q3, (uint32_t)q2, 0x05040100u));
                         k += 4;
                     }
                     const int nz_end = k;

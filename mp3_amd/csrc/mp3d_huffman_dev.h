@@ -24,6 +24,7 @@ namespace mp3d {
 /* Side info arrives pre-extracted by k_demux (one u64 per unit).           */
 /* ------------------------------------------------------------------------ */
 #define HUFF_WAVES 4
+#define MP3D_C1B_OFF 2 /* count1 table B after the zero table (huff_tables_lane) */
 #define HUFF_ROUNDS 4                    /* 64-unit rounds per super-chunk          */
 #define HUFF_SUPER (64 * HUFF_ROUNDS)    /* units ranked together by big_values     */
 #define HUFF_BLOCK (64 * HUFF_WAVES)
@@ -45,6 +46,27 @@ __device__ __forceinline__ uint32_t win32(const uint32_t *bits, uint32_t pos) {
     w = w < HUFF_CAPW ? w : HUFF_CAPW;
     const uint32_t w0 = bits[w], w1 = bits[w + 1];
     return (uint32_t)((((uint64_t)w0 << 32) | w1) >> (32u - (pos & 31u)));
+}
+/* win64 / win32 by 32-bit funnel shifts (v_alignbit_b32, shift = -pos mod
+ * 32): the word pair is picked from pos + 31, so a shift of 0 (pos a
+ * multiple of 32) selects the pair's second word.  Reads one word BELOW
+ * pos / 32 in that case (its value is not used): bits[-1] must be
+ * readable LDS (k_huffman's staging areas have a guard word). */
+/* No index clamp: k_huffman reads only while pos is inside the lane's staged
+ * segment (pos <= the unit end + 47 bits < its 2-word margin). */
+__device__ __forceinline__ void win64g(const uint32_t *bits, uint32_t pos, uint32_t &hi, uint32_t &lo) {
+    const uint32_t w = (pos + 31u) >> 5;
+    const uint32_t w0 = bits[(int)w - 1], w1 = bits[w], w2 = bits[w + 1];
+    hi = __builtin_amdgcn_alignbit(w0, w1, 0u - pos);
+    lo = __builtin_amdgcn_alignbit(w1, w2, 0u - pos);
+}
+__device__ __forceinline__ uint32_t win32g(const uint32_t *bits, uint32_t pos) {
+    const uint32_t w = (pos + 31u) >> 5;
+    return __builtin_amdgcn_alignbit(bits[(int)w - 1], bits[w], 0u - pos);
+}
+/* top 32 bits of (hi:lo) << n for 1 <= n <= 32 (n = 0 gives lo, not hi) */
+__device__ __forceinline__ uint32_t shl64hi_a(uint32_t hi, uint32_t lo, uint32_t n) {
+    return __builtin_amdgcn_alignbit(hi, lo, 32u - n);
 }
 /* top 32 bits of (hi:lo) << n, 0 <= n <= 32 */
 __device__ __forceinline__ uint32_t shl64hi(uint32_t hi, uint32_t lo, uint32_t n) {
@@ -202,6 +224,9 @@ __device__ __forceinline__ void huff_tables_lane(const DevTables *tab, uint16_t 
     for (int i = threadIdx.x; i < (lut_n + 1) / 2; i += blockDim.x)
         ((uint32_t *)s_lut)[i] = ((const uint32_t *)tab->lut)[i];
     if (threadIdx.x == 0) ((uint32_t *)s_lut)[zbase / 2] = 0u;
+    /* count1 table B (4-bit codes, value = 15 - code) as a 16-entry table at
+     * zbase + 2 (MP3D_C1B_OFF), so both count1 tables are one LUT read */
+    if (threadIdx.x < 16) s_lut[zbase + MP3D_C1B_OFF + threadIdx.x] = (uint16_t)((4u << 8) | (15u - threadIdx.x));
     if (threadIdx.x < 9) {
         int acc = 0;
         for (int i = 0; i < 22; i++) {
@@ -213,8 +238,9 @@ __device__ __forceinline__ void huff_tables_lane(const DevTables *tab, uint16_t 
     if (threadIdx.x < 32) s_slen[threadIdx.x] = MP3D_SLEN[threadIdx.x >> 4][threadIdx.x & 15];
     if (threadIdx.x < 32) {
         const int t = MP3D_HTAB_OF_SELECT[threadIdx.x];
-        s_tsel[threadIdx.x] = t < 0 ? (uint32_t)zbase | (1u << 16)
-                                    : (uint32_t)tab->lut_hdr.base[t] | ((uint32_t)tab->lut_hdr.bits1[t] << 16) |
+        /* k_huffman's encoding: 32 - bits1 (the first level's shift) in bits 16..21 */
+        s_tsel[threadIdx.x] = t < 0 ? (uint32_t)zbase | (31u << 16)
+                                    : (uint32_t)tab->lut_hdr.base[t] | ((32u - tab->lut_hdr.bits1[t]) << 16) |
                                           ((uint32_t)MP3D_LINBITS[threadIdx.x] << 24);
     }
 }
