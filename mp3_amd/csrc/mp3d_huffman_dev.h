@@ -293,23 +293,20 @@ __device__ __forceinline__ void hw_pair(const uint16_t *s_lut, const uint32_t *b
     const uint32_t i1 = tb + (hi >> (32 - b1));
     const uint32_t e1 = s_lut[i1];
     const uint32_t nb = (e1 >> 11) & 15u;
-    const uint32_t sub = ((e1 & 0x7FFu) << 2) + (uint32_t)((((uint64_t)hi << b1) & 0xFFFFFFFFull) >> (32u - nb));
+    /* (hi << b1) >> (32 - nb) as one field extract (nb = 0 for a leaf: 0) */
+    const uint32_t sub = ((e1 & 0x7FFu) << 2) + __builtin_amdgcn_ubfe(hi, 32u - b1 - nb, nb);
     const uint32_t e = s_lut[(e1 & 0x8000u) ? sub : i1];
     const uint32_t x = (e >> 4) & 15u, y = e & 15u, len_c = (e >> 8) & 31u;
     const uint32_t sx = (e >> 13) & 1u, sy = (e >> 14) & 1u;
-    const uint32_t rb = shl64hi(hi, lo, len_c);
+    const uint32_t rb = shl64hi_a(hi, lo, len_c); /* len_c = 0: table 0, no bits read */
     const uint32_t nx = x == 15u ? lin : 0u, ny = y == 15u ? lin : 0u;
-    const uint32_t ex = __builtin_amdgcn_ubfe(rb, 32u - nx, nx);
-    const uint32_t q1 = nx + sx;
-    const uint32_t sgx = __builtin_amdgcn_ubfe(rb, 32u - q1, 1u);
-    const uint32_t ey = __builtin_amdgcn_ubfe(rb, 32u - q1 - ny, ny);
-    const uint32_t q2 = q1 + ny + sy;
-    const uint32_t sgy = __builtin_amdgcn_ubfe(rb, 32u - q2, 1u);
-    int X = (int)(x + ex), Y = (int)(y + ey);
-    X = sgx ? -X : X;
-    Y = sgy ? -Y : Y;
-    tl = len_c + q2;
-    word = (uint32_t)(uint16_t)X | ((uint32_t)(uint16_t)Y << 16);
+    /* fields counted down from the top of rb; signs as 0 / -1 masks */
+    const uint32_t t0 = 32u - nx, t1 = t0 - sx, t2 = t1 - ny, t3 = t2 - sy;
+    const uint32_t ex = __builtin_amdgcn_ubfe(rb, t0, nx), ey = __builtin_amdgcn_ubfe(rb, t2, ny);
+    const int mx = __builtin_amdgcn_sbfe((int)rb, t1, 1u), my = __builtin_amdgcn_sbfe((int)rb, t3, 1u);
+    const int X = ((int)(x + ex) ^ mx) - mx, Y = ((int)(y + ey) ^ my) - my;
+    tl = len_c + (32u - t3);
+    word = __builtin_amdgcn_perm((uint32_t)Y, (uint32_t)X, 0x05040100u);
 }
 
 
@@ -519,16 +516,16 @@ __device__ __forceinline__ void huffman_wave_unit(const uint8_t *__restrict__ md
             lq = (e >> 8) & 31u;
         }
         const uint32_t ns = __builtin_popcount(v);
-        const uint32_t sbits = (hw << lq) >> (32 - (ns ? ns : 1));
-        int bit = (int)ns;
-        int q0 = (v >> 3) & 1, q1 = (v >> 2) & 1, q2 = (v >> 1) & 1, q3 = v & 1;
-        if (q0) { bit--; if ((sbits >> bit) & 1) q0 = -1; }
-        if (q1) { bit--; if ((sbits >> bit) & 1) q1 = -1; }
-        if (q2) { bit--; if ((sbits >> bit) & 1) q2 = -1; }
-        if (q3) { bit--; if ((sbits >> bit) & 1) q3 = -1; }
+        /* sign bits by prefix counts of v (k_huffman's count1 decode) */
+        const uint32_t rb = hw << lq;
+        const uint32_t p1 = v >> 3, p2 = __builtin_popcount(v >> 2), p3 = __builtin_popcount(v >> 1);
+        const int m0 = __builtin_amdgcn_sbfe((int)rb, 31u, 1u), m1 = __builtin_amdgcn_sbfe((int)rb, 31u - p1, 1u);
+        const int m2 = __builtin_amdgcn_sbfe((int)rb, 31u - p2, 1u), m3 = __builtin_amdgcn_sbfe((int)rb, 31u - p3, 1u);
+        const int q0 = ((int)p1 ^ m0) - m0, q1 = ((int)((v >> 2) & 1u) ^ m1) - m1;
+        const int q2 = ((int)((v >> 1) & 1u) ^ m2) - m2, q3 = ((int)(v & 1u) ^ m3) - m3;
         const uint32_t tq = lq + ns;
-        const uint32_t wa = (uint32_t)(uint16_t)q0 | ((uint32_t)(uint16_t)q1 << 16);
-        const uint32_t wb = (uint32_t)(uint16_t)q2 | ((uint32_t)(uint16_t)q3 << 16);
+        const uint32_t wa = __builtin_amdgcn_perm((uint32_t)q1, (uint32_t)q0, 0x05040100u);
+        const uint32_t wb = __builtin_amdgcn_perm((uint32_t)q3, (uint32_t)q2, 0x05040100u);
         /* a quadruple ends at or before the part2_3 end */
         const uint32_t lim = end_bit - pos;
         const uint32_t lim0 = lim < 64u ? lim : 64u;
