@@ -259,15 +259,15 @@ __global__ void __launch_bounds__(64) k_walk(const uint8_t *__restrict__ in, con
  * are in flight together), then the next carry.  Each lane first loads the
  * copy descriptor of one frame (lane f: frame f of a 64-frame chunk), so the
  * frame loop reads no record from memory.  Payload words: the destination
- * is written in aligned words, each from one 8-B source load funnel-shifted
- * by the source misalignment (the k_demux copy; edge bytes and a cut-short
- * tail as there).  All loads of an iteration are straight-line and
+ * is written in aligned words, each funnel-shifted from two source words by
+ * the source misalignment (the k_demux copy; edge bytes and a cut-short
+ * tail as there), four per lane and store.  All loads of an iteration are straight-line and
  * unconditional (lanes without work re-read a valid word): a load under a
  * branch makes the compiler's waitcnt pass drain vmcnt(0) at the join.  An
  * aligned source loads words (k - 1, k) instead of (k, k + 1), so no load
  * passes the payload's last word (word -1 is side info or header). */
 #define MDC_WAVES 4
-#define MDC_ROUNDS 8 /* 16-lane rounds per frame in the unrolled part: 512 B */
+#define MDC_QROUNDS 2 /* 16-lane rounds of word quadruples per frame, unrolled: 512 B */
 __global__ void __launch_bounds__(64 * MDC_WAVES) k_mdcopy(const uint8_t *__restrict__ in, uint8_t *__restrict__ md,
                                                          const uint64_t *__restrict__ md_off,
                                                          StreamState *__restrict__ st,
@@ -326,21 +326,40 @@ __global__ void __launch_bounds__(64 * MDC_WAVES) k_mdcopy(const uint8_t *__rest
                                          : (const uint32_t *)(hb0 - ((uintptr_t)hb0 & 3u));
                 const uint8_t hbv = *((uint32_t)ql < h ? src + ql : hb0);
                 const uint8_t tbv = *((uint32_t)ql < L - t0 ? src + t0 + ql : hb0);
-                uint32_t v[MDC_ROUNDS];
+                /* whole quadruples of words: lane ql builds words 4 q .. 4 q + 3
+                 * (q = 16 j + ql) from source words 4 q .. 4 q + 4 (one 16-B and
+                 * one 4-B load, dword-aligned) and stores them with one 16-B
+                 * store: a quarter of the stores and half the loads of one word
+                 * per lane.  A quadruple reads up to word 4 q + 4 <= nwd, so only
+                 * whole ones (q < nq) are copied here; the others load from the
+                 * stream's own md region (>= 20 readable bytes, unlike a cut-short
+                 * final frame's source) and their stores are masked by an
+                 * out-of-range offset (not a branch: the compiler would sink each
+                 * load into its store's branch). */
+                const uint32_t nq = nwd >> 2;
+                uint4 v[MDC_QROUNDS];
 #pragma unroll
-                for (int j = 0; j < MDC_ROUNDS; j++) {
-                    const uint32_t k = 16u * j + (uint32_t)ql;
-                    const uint2 x = *(const uint2 *)(lp + (k < nwd ? k : 0u));
-                    v[j] = __builtin_amdgcn_alignbit(x.y, sh ? x.x : x.y, sh);
+                for (int j = 0; j < MDC_QROUNDS; j++) {
+                    const uint32_t q = 16u * j + (uint32_t)ql;
+                    const uint32_t *L = q < nq ? lp + 4u * q : (const uint32_t *)dst;
+                    uint4 a;
+                    __builtin_memcpy(&a, L, 16);
+                    const uint32_t e = L[4];
+                    v[j] = make_uint4(__builtin_amdgcn_alignbit(a.y, sh ? a.x : a.y, sh),
+                                      __builtin_amdgcn_alignbit(a.z, sh ? a.y : a.z, sh),
+                                      __builtin_amdgcn_alignbit(a.w, sh ? a.z : a.w, sh),
+                                      __builtin_amdgcn_alignbit(e, sh ? a.w : e, sh));
                 }
-                /* stores masked by an out-of-range offset, not a branch (the
-                 * compiler would sink each load into its store's branch) */
 #pragma unroll
-                for (int j = 0; j < MDC_ROUNDS; j++) {
-                    const uint32_t k = 16u * j + (uint32_t)ql;
-                    __builtin_amdgcn_raw_buffer_store_b32(v[j], r_md, k < nwd ? 4u * (wb + k) : 0x80000000u, 0, 0);
+                for (int j = 0; j < MDC_QROUNDS; j++) {
+                    const uint32_t q = 16u * j + (uint32_t)ql;
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v[j]), r_md,
+                        q < nq ? 4u * (wb + 4u * q) : 0x80000000u, 0, 0);
                 }
-                for (uint32_t k = 16u * MDC_ROUNDS + (uint32_t)ql; k < nwd; k += 16) {
+                /* the rest one word per lane: the last partial quadruple and
+                 * payloads past the unrolled 16 MDC_QROUNDS quadruples */
+                for (uint32_t k = 4u * min(nq, 16u * MDC_QROUNDS) + (uint32_t)ql; k < nwd; k += 16) {
                     const uint2 x = *(const uint2 *)(lp + k);
                     ((uint32_t *)dst)[wb + k] = __builtin_amdgcn_alignbit(x.y, sh ? x.x : x.y, sh);
                 }
