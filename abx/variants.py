@@ -34,6 +34,12 @@ W4H = ("__global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(",
        "__global__ void __launch_bounds__(HUFF_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 8))) k_huffman(")
 LID = "__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u))"
 VARS = {
+    # ranking key: part2_3_length / 16 (total bits: big_values + count1 work) instead of big_values
+    "RK1": [("            bvk[j] = u < n_units ? (uint32_t)(sideu[u] >> 43) & 0x1FFu : 0u;",
+             "            bvk[j] = u < n_units ? (uint32_t)(sideu[u] >> 56) & 0xFFu : 0u;")],
+    # ranking key: big_values / 2 + part2_3_length / 32
+    "RK2": [("            bvk[j] = u < n_units ? (uint32_t)(sideu[u] >> 43) & 0x1FFu : 0u;",
+             "            bvk[j] = u < n_units ? (((uint32_t)(sideu[u] >> 43) & 0x1FFu) >> 1) + ((uint32_t)(sideu[u] >> 57) & 0x7Fu) : 0u;")],
     # r02 timing-only probes (wrong output): k_huffman with conflict-free window / LUT reads
     "HW0": [("    const uint32_t w0 = bits[w], w1 = bits[w + 1], w2 = bits[w + 2];",
              "    const uint32_t ln = " + LID + "; (void)w;\n    const uint32_t w0 = bits[ln], w1 = bits[ln + 64], w2 = bits[ln + 128];"),

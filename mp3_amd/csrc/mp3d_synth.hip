@@ -216,14 +216,21 @@ __device__ __forceinline__ void synth_tables(SynShared<LSF> &T, const DevTables 
  * One segment (seg_len >= F): the stream's state in and out.  T = the
  * workgroup's tables (synth_tables), Wd = the wave's LDS buffer.  No
  * workgroup barrier inside. */
-template <bool SRC_XR, bool F32, bool LSF>
+/* PF (k_frame's two-wave synthesis of one MPEG-1 frame): 0 =
+ * the normal path; 1 = granule 0 only, publishing its IMDCT overlap (after
+ * phase I) and its synthesis history (after phase W) in xch, no state out;
+ * 2 = granule 1 only, taking them from xch, state out.  The two waves meet
+ * at two workgroup barriers (every other wave of the workgroup runs two
+ * as well). */
+template <bool SRC_XR, bool F32, bool LSF, int PF = 0>
 __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf,
                                              const UnitMeta *__restrict__ meta, const float *__restrict__ xr_in,
                                              const uint8_t *__restrict__ xr_bt, const uint8_t *__restrict__ xr_mixed,
                                              const DevTables *__restrict__ tab, StreamState *__restrict__ st,
                                              void *__restrict__ pcm, int F, int xr_nch, int xr_sr, int seg_len,
                                              float *__restrict__ st_tail, SynShared<LSF> &T, SynWave &Wd, int s,
-                                             int seg, int nseg) {
+                                             int seg, int nseg, float *xch = nullptr) {
+    static_assert(PF == 0 || (!SRC_XR && !LSF), "PF: k_frame's MPEG-1 decode path only");
     const int f0 = seg * seg_len, f1 = min(F, f0 + seg_len);
     const int fw = seg ? f0 - 1 : 0; /* first frame decoded (warm-up below f0) */
     float *const sBuf = Wd.buf;
@@ -348,7 +355,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
     };
     if (SRC_XR) load_xr(2 * fw);
     if (!SRC_XR) {
-        prefetch_full(2 * fw);
+        prefetch_full(2 * fw + (PF == 2 ? 1 : 0));
         /* explicit drain on the entry path, so the compiler's wait before
          * each prefetch use is set by the loop path (stores after it) */
         WAIT_VMCNT0();
@@ -381,7 +388,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
         const bool active = ch < nch;
         const uint64_t amask = __ballot(active); /* lanes of coded channels */
         const uint32_t(*lpair)[288] = T.lpair[sr];
-        for (int gr = 0; gr < (LSF ? 1 : 2); gr++) { /* LSF: one granule per frame */
+        for (int gr = PF == 2 ? 1 : 0; gr < (LSF || PF == 1 ? 1 : 2); gr++) { /* LSF: one granule per frame */
             /* lane-derived indices are re-derived from an opaque copy each
              * granule so they are not hoisted and held live across the loop */
             const int lane = opaque((int)(threadIdx.x & 63));
@@ -595,7 +602,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                 }
                 /* the next granule's loads fly during phases I, M, W (issued
                  * after cis is consumed: fewer live registers in phase Q) */
-                if (LSF ? f + 1 < f1 : (gr == 0 || f + 1 < f1)) prefetch(LSF ? 2 * f + 2 : 2 * f + gr + 1);
+                if (PF == 0 && (LSF ? f + 1 < f1 : (gr == 0 || f + 1 < f1))) prefetch(LSF ? 2 * f + 2 : 2 * f + gr + 1);
                 /* scatter in (short-block reordered) position */
 #pragma unroll
                 for (int i = 0; i < 5; i++) {
@@ -619,6 +626,11 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
             wave_sync();
 #undef XV
             /* ---------------- phase I: alias + IMDCT + overlap ------------ */
+            if (PF == 2) { /* granule 0's overlap from the other wave */
+                __syncthreads();
+#pragma unroll
+                for (int i = 0; i < 18; i++) ov[i] = xch[i * 64 + lane];
+            }
             const int bt = ch ? bt1 : bt0, mixed = ch ? mx1 : mx0;
             float o18[18];
             {
@@ -701,6 +713,11 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                     }
                 }
             }
+            if (PF == 1) { /* granule 0's overlap for the other wave */
+#pragma unroll
+                for (int i = 0; i < 18; i++) xch[i * 64 + lane] = ov[i];
+                __syncthreads();
+            }
             wave_sync(); /* every lane has read its xr before S overwrites it */
             {
                 const int sw = opaque(18 * ch * SROW + sb);
@@ -766,6 +783,13 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
              * waitcnt pass treats loads and stores pending together as out of
              * order and would otherwise emit vmcnt(0) right after them.) */
             if (!SRC_XR) WAIT_VMCNT0();
+            if (PF == 2) { /* granule 0's synthesis history from the other wave */
+                __syncthreads();
+#pragma unroll
+                for (int k = 0; k < 14; k++) ha[k] = xch[(18 + k) * 64 + lane];
+#pragma unroll
+                for (int k = 0; k < 15; k++) hb[k] = xch[(32 + k) * 64 + lane];
+            }
             {
                 float Dw[16];
 #pragma unroll
@@ -875,6 +899,13 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                 for (int k = 0; k < 14; k++) ha[k] = lane_sel(amask, ha[k], xa[k + 4]);
 #pragma unroll
                 for (int k = 0; k < 15; k++) hb[k] = lane_sel(amask, hb[k], xb[k + 3]);
+                if (PF == 1) {
+#pragma unroll
+                    for (int k = 0; k < 14; k++) xch[(18 + k) * 64 + lane] = ha[k];
+#pragma unroll
+                    for (int k = 0; k < 15; k++) xch[(32 + k) * 64 + lane] = hb[k];
+                    __syncthreads();
+                }
             }
             wave_sync(); /* X reads done before the next granule's xr */
         }
@@ -883,7 +914,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
      * first one may still be reading S, so the state goes to st_tail (the
      * overlap + fifo tail of StreamState, copied in by the host after the
      * launch). */
-    if (f1 == F) {
+    if (f1 == F && PF != 1) {
         float *ovo = nseg > 1 ? st_tail + (size_t)s * (sizeof(S.overlap) + sizeof(S.fifo)) / 4 : &S.overlap[0][0][0];
         float *ffo = ovo + sizeof(S.overlap) / 4;
 #pragma unroll
@@ -981,7 +1012,8 @@ __global__ void __launch_bounds__(256) k_frame(const uint8_t *__restrict__ in_ho
                                                UnitMeta *__restrict__ meta, void *__restrict__ pcm,
                                                uint32_t *__restrict__ done, uint32_t seq) {
     __shared__ __attribute__((aligned(16))) SynShared<LSF> T;
-    __shared__ SynWave Wv[1];
+    __shared__ SynWave Wv[2];
+    __shared__ float s_xch[47 * 64]; /* granule 0 -> 1 hand-off: overlap (18), history (14 + 15) per lane */
     __shared__ __attribute__((aligned(16))) uint16_t s_lut[MP3D_LUT_MAX];
     __shared__ __attribute__((aligned(16))) uint32_t s_bits[HW_UNITS][HW_WORDS + 4];
     __shared__ uint32_t s_tsel[32];
@@ -1029,13 +1061,39 @@ __global__ void __launch_bounds__(256) k_frame(const uint8_t *__restrict__ in_ho
     __syncthreads(); /* rec, side words, md region and state visible to the workgroup */
     huffman_wave_unit(md, md_off, rec, sideu, tab, is_buf, meta, 1, wv, lane, s_bits[wv], s_lut, s_tsel, s_lbnd,
                       s_slen);
-    __syncthreads(); /* is[] rows and UnitMeta visible to wave 0 */
+    __syncthreads(); /* is[] rows and UnitMeta visible to the synthesis waves */
+    /* a frame of the other MPEG family than the stream's was skipped as
+     * junk by the demux: no audio (as k_synth's variant check) */
+    const bool fam = (st[0].kind == 2) == LSF;
+    const FrameRec r0 = rec[0];
+    /* MPEG-1 frame with audio: wave 0 synthesises granule 0 and wave 1
+     * granule 1 side by side (synth_stream PF = 1, 2): wave 1 requantises
+     * its granule while wave 0 runs granule 0's phases Q and I, takes
+     * granule 0's IMDCT overlap at the first barrier and its synthesis
+     * history at the second.  Same operations in the same order per value
+     * as one wave doing both granules, so bit-identical.  The condition is
+     * the one under which synth_stream decodes the frame (so every wave
+     * meets the same two barriers). */
+    const bool split = !LSF && fam && r0.frame_bytes && !(r0.first_gr & (REC_TAG | REC_DROP));
+    if constexpr (!LSF) if (split) {
+        if (wv == 0)
+            synth_stream<false, F32, LSF, 1>(rec, is_buf, meta, nullptr, nullptr, nullptr, tab, st, pcm, 1, 2, 0, 1,
+                                             nullptr, T, Wv[0], 0, 0, 1, s_xch);
+        else if (wv == 1)
+            synth_stream<false, F32, LSF, 2>(rec, is_buf, meta, nullptr, nullptr, nullptr, tab, st, pcm, 1, 2, 0, 1,
+                                             nullptr, T, Wv[1], 0, 0, 1, s_xch);
+        else {
+            __syncthreads();
+            __syncthreads();
+        }
+        if (wv == 1) __threadfence_system(); /* granule 1's PCM and the state, before the barrier */
+        __syncthreads();
+    }
+    if (!split && wv == 0 && fam) {
+        synth_stream<false, F32, LSF>(rec, is_buf, meta, nullptr, nullptr, nullptr, tab, st, pcm, 1, 2, 0, 1, nullptr,
+                                      T, Wv[0], 0, 0, 1);
+    }
     if (wv == 0) {
-        /* a frame of the other MPEG family than the stream's was skipped as
-         * junk by the demux: no audio (as k_synth's variant check) */
-        if ((st[0].kind == 2) == LSF)
-            synth_stream<false, F32, LSF>(rec, is_buf, meta, nullptr, nullptr, nullptr, tab, st, pcm, 1, 2, 0, 1,
-                                          nullptr, T, Wv[0], 0, 0, 1);
         __threadfence_system(); /* PCM, frame info and state before the completion word */
         if (lane == 0) __hip_atomic_store(done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
