@@ -252,7 +252,7 @@ def setup_decode(c, cfg_name):
     import mp3_amd
     from mp3_amd import shard
     cfg = _gen.C3 if cfg_name == "c3" else _gen.C5
-    base = shard.BASE_SEED_C3 if cfg_name == "c3" else 5_000_011
+    base = c.seed if c.seed is not None else shard.BASE_SEED_C3 if cfg_name == "c3" else 5_000_011
     t0 = time.time()
     buf, offs, sizes = _gen.batch(cfg, shard.shard_seed_base(c.rank, c.n, base), c.n, c.F,
                                   threads=min(16, host_threads()))
@@ -275,7 +275,8 @@ def setup_synth(c):
     import _gen
     import mp3_amd
     from mp3_amd import shard
-    xr, bt, mx = _gen.c2_spectra(c.n, c.F, 2, seed=shard.shard_seed_base(c.rank, c.n, 1_000_003 * 2))
+    xr, bt, mx = _gen.c2_spectra(c.n, c.F, 2, seed=shard.shard_seed_base(c.rank, c.n,
+                                                                           c.seed if c.seed is not None else 1_000_003 * 2))
     c.xr, c.bt, c.mx = xr, bt, mx
     c.d_xr, c.d_bt, c.d_mx = (torch.from_numpy(a).to(c.dev) for a in (xr, bt, mx))
     c.pcm = [torch.empty((c.n, c.F, 2304), dtype=torch.int16, device=c.dev) for _ in range(2 if c.gather else 1)]
@@ -347,6 +348,8 @@ def main():
                     help="BASELINE.json configs[k-1]; 4 = 3 at --gpus 8 (65,536 streams per GPU)")
     ap.add_argument("--streams", type=int, default=None, help="streams per GPU (default: the config's)")
     ap.add_argument("--frames", type=int, default=None, help="frames per stream per step (default: the config's)")
+    ap.add_argument("--seed", type=int, default=None,
+                    help="generator seed of global stream 0 (stream g uses seed + g; default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true",
                     help="also time an RCCL PCM gather to rank 0 overlapped with the next step (reported apart)")
@@ -376,7 +379,7 @@ def main():
     if world != args.gpus:
         raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     c = Ctx()
-    c.rank, c.world, c.gather = rank, world, args.gather
+    c.rank, c.world, c.gather, c.seed = rank, world, args.gather, args.seed
     backend = "gloo" if args.plumbing else args.dist_backend
     if args.plumbing:
         c.dev = torch.device("cpu")
@@ -566,6 +569,7 @@ def report_decode(c, args, cfg, value, kt, frames_per_step):
         "data": data,
         "config": {"workload": wl, "streams_per_gpu": n, "frames_per_stream": F, "bitrate_kbps": 128 if cfg == "c3"
                    else "32-320 VBR", "hz": 44100 if cfg == "c3" else "32000/44100/48000",
+                   "seed": c.seed if c.seed is not None else "default",
                    "parallelism": "streams sharded, 1 process per GPU, no data-path collective"},
         "roofline": {
             "kernel": "k_synth", "bound": "mfma", "unit": "TFLOP/s",
@@ -613,6 +617,7 @@ def report_c2(c, args, value, kt):
         "config": {"workload": "C2: IMDCT + polyphase synthesis only (mp3d_batch_synth_only), %d streams x %d "
                                "frames per GPU per step" % (n, F),
                    "streams_per_gpu": n, "frames_per_stream": F, "hz": 44100,
+                   "seed": c.seed if c.seed is not None else "default",
                    "parallelism": "streams sharded, 1 process per GPU, no data-path collective"},
         "roofline": {
             "kernel": "k_synth<xr>", "bound": "mfma", "unit": "TFLOP/s", "achieved": achieved_tf,

@@ -552,7 +552,12 @@ static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *of
     if (!b || !pcm) return MP3D_E_ARG;
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : b->own;
     bool sync_needed = mapped;
-    int r = run_front(b, frames, offsets, sizes, n, F, s, &sync_needed, mapped, mapped ? infos : nullptr);
+    /* frame infos: written in place when the caller's array is device memory
+     * (or the per-frame decoder's mapped buffer), else into d_infos and
+     * copied to the host after the call */
+    const bool inf_host = infos && !mapped && !is_device_ptr(infos);
+    mp3d_frame_info *dinf = infos && !inf_host ? infos : b->d_infos;
+    int r = run_front(b, frames, offsets, sizes, n, F, s, &sync_needed, mapped, dinf);
     if (r) return r;
     const size_t PB = f32 ? sizeof(float) : sizeof(int16_t), row = 2304 * PB;
     const size_t pcm_bytes = (size_t)n * F * row;
@@ -568,8 +573,6 @@ static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *of
     if (b->timing) HIPCHK(hipEventRecord(b->ev[3], s));
     HIPCHK(hipGetLastError());
     const size_t ib = sizeof(mp3d_frame_info) * (size_t)n * F;
-    const bool inf_host = infos && !mapped && !is_device_ptr(infos);
-    if (infos && !inf_host && !mapped) HIPCHK(hipMemcpyAsync(infos, b->d_infos, ib, hipMemcpyDeviceToDevice, s));
     if (pcm_host && !overwrite) {
         /* A host sink is read back whole, but each row keeps the caller's
          * bytes the kernel did not write (rows without audio, the second
@@ -582,7 +585,7 @@ static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *of
             tmp.resize((size_t)n * F);
             hi = tmp.data();
         }
-        HIPCHK(hipMemcpyAsync(hi, b->d_infos, ib, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(hi, dinf, ib, hipMemcpyDefault, s));
         HIPCHK(hipStreamSynchronize(s));
         std::vector<size_t> at;
         std::vector<uint8_t> kept;
