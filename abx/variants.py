@@ -34,6 +34,16 @@ W4H = ("__global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(",
        "__global__ void __launch_bounds__(HUFF_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 8))) k_huffman(")
 LID = "__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u))"
 VARS = {
+    # k_synth wave priority: raised through phase M (the MFMA chains issue ahead of other waves' VALU)
+    "SP1": [("            /* ---------------- phase M: matrixing on the matrix cores ------- */",
+             "            __builtin_amdgcn_s_setprio(2);\n            /* ---------------- phase M: matrixing on the matrix cores ------- */"),
+            ("            /* ---------------- phase W: 512-tap window -> PCM --------------- */",
+             "            __builtin_amdgcn_s_setprio(0);\n            /* ---------------- phase W: 512-tap window -> PCM --------------- */")],
+    # k_synth wave priority: raised through phase Q (its loads and LDS table reads issue early)
+    "SP2": [("            /* ---------------- phase Q: requantise + stereo -> LDS ---------- */",
+             "            __builtin_amdgcn_s_setprio(1);\n            /* ---------------- phase Q: requantise + stereo -> LDS ---------- */"),
+            ("            /* ---------------- phase I: alias + IMDCT + overlap ------------ */",
+             "            __builtin_amdgcn_s_setprio(0);\n            /* ---------------- phase I: alias + IMDCT + overlap ------------ */")],
     # ranking key: part2_3_length / 16 (total bits: big_values + count1 work) instead of big_values
     "RK1": [("            bvk[j] = u < n_units ? (uint32_t)(sideu[u] >> 43) & 0x1FFu : 0u;",
              "            bvk[j] = u < n_units ? (uint32_t)(sideu[u] >> 56) & 0xFFu : 0u;")],
