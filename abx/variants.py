@@ -32,8 +32,46 @@ def variant(name, reps):
 
 W4H = ("__global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(",
        "__global__ void __launch_bounds__(HUFF_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 8))) k_huffman(")
+_QS = "            /* ---------------- phase Q: requantise + stereo -> LDS ---------- */"
+_IS = "            /* ---------------- phase I: alias + IMDCT + overlap ------------ */"
+_MS = "            /* ---------------- phase M: matrixing on the matrix cores ------- */"
+_WS = "            /* ---------------- phase W: 512-tap window -> PCM --------------- */"
+
+
+def _pr(n, marker):
+    """s_setprio(n) just before a k_synth phase marker"""
+    return (marker, "            __builtin_amdgcn_s_setprio(%d);\n%s" % (n, marker))
+
+
 LID = "__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u))"
 VARS = {
+    # k_synth phase Q: channel 1 reuses channel 0's line-pair table word when both have the same block variant
+    "LP1": [("""                for (int i = 0; i < 5; i++) {
+                    const int l0 = 2 * lane + 128 * i;
+                    const bool ok = i < 4 || lane < 32;
+#pragma unroll
+                    for (int c = 0; c < 2; c++) {
+                        const uint32_t tv2 = ok ? lpair[var[c]][l0 >> 1] : 0u;""",
+             """                for (int i = 0; i < 5; i++) {
+                    const int l0 = 2 * lane + 128 * i;
+                    const bool ok = i < 4 || lane < 32;
+                    uint32_t tvp[2];
+                    tvp[0] = ok ? lpair[var[0]][l0 >> 1] : 0u;
+                    if (var[1] == var[0]) tvp[1] = tvp[0];
+                    else tvp[1] = ok ? lpair[var[1]][l0 >> 1] : 0u;
+#pragma unroll
+                    for (int c = 0; c < 2; c++) {
+                        const uint32_t tv2 = tvp[c];""")],
+    # priority through phase Q = 2 (SP4), Q = 3 (SP6); Q 1 + M 2 (SP3); Q and I at 1 (SP5)
+    "SP4": [_pr(2, _QS), _pr(0, _IS)],
+    "SP6": [_pr(3, _QS), _pr(0, _IS)],
+    "SP3": [_pr(1, _QS), _pr(0, _IS), _pr(2, _MS), _pr(0, _WS)],
+    "SP5": [_pr(1, _QS), _pr(0, _MS)],
+    # k_huffman: priority 1 while a round's segments stage into LDS, 0 for the decode (HP1)
+    "HP1": [("                /* stage: each lane copies its own segment, 4 x 16 B in flight */",
+             "                __builtin_amdgcn_s_setprio(1);\n                /* stage: each lane copies its own segment, 4 x 16 B in flight */"),
+            ("                    /* big_values: region boundaries (ISO 2.4.2.7; FFmpeg clamp) */",
+             "                    __builtin_amdgcn_s_setprio(0);\n                    /* big_values: region boundaries (ISO 2.4.2.7; FFmpeg clamp) */")],
     # k_synth wave priority: raised through phase M (the MFMA chains issue ahead of other waves' VALU)
     "SP1": [("            /* ---------------- phase M: matrixing on the matrix cores ------- */",
              "            __builtin_amdgcn_s_setprio(2);\n            /* ---------------- phase M: matrixing on the matrix cores ------- */"),

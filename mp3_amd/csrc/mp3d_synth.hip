@@ -395,6 +395,11 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
             const int ch = lane >> 5, sb = lane & 31;
             /* block structure of both channels (uniform) */
             int bt0, mx0, bt1 = 0, mx1 = 0;
+            /* decode path: the wave issues at raised priority through phase Q
+             * (its next-granule prefetch and LDS table reads go out ahead of
+             * the other waves' VALU phases; A/B SP2: -2 % k_synth on C3; the
+             * synth-only entry measured within noise, so it stays at 0) */
+            if (!SRC_XR) __builtin_amdgcn_s_setprio(1);
             /* ---------------- phase Q: requantise + stereo -> LDS ---------- */
             if (SRC_XR) {
                 (void)fr;
@@ -625,6 +630,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
             }
             wave_sync();
 #undef XV
+            if (!SRC_XR) __builtin_amdgcn_s_setprio(0);
             /* ---------------- phase I: alias + IMDCT + overlap ------------ */
             if (PF == 2) { /* granule 0's overlap from the other wave */
                 __syncthreads();
