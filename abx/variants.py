@@ -72,6 +72,14 @@ VARS = {
              "                __builtin_amdgcn_s_setprio(1);\n                /* stage: each lane copies its own segment, 4 x 16 B in flight */"),
             ("                    /* big_values: region boundaries (ISO 2.4.2.7; FFmpeg clamp) */",
              "                    __builtin_amdgcn_s_setprio(0);\n                    /* big_values: region boundaries (ISO 2.4.2.7; FFmpeg clamp) */")],
+    # k_huffman: priority 1 through the count1 loop (HP2) / through the big_values loop (HP3)
+    "HP2": [("                    /* count1 quadruples until the part2_3 end; a quadruple that",
+             "                    __builtin_amdgcn_s_setprio(1);\n                    /* count1 quadruples until the part2_3 end; a quadruple that"),
+            ("                    const int nz_end = k;", "                    __builtin_amdgcn_s_setprio(0);\n                    const int nz_end = k;")],
+    "HP3": [("                    for (; __ballot(k < bv2); k += 8) {",
+             "                    __builtin_amdgcn_s_setprio(1);\n                    for (; __ballot(k < bv2); k += 8) {"),
+            ("                    /* count1 quadruples until the part2_3 end; a quadruple that",
+             "                    __builtin_amdgcn_s_setprio(0);\n                    /* count1 quadruples until the part2_3 end; a quadruple that")],
     # k_synth wave priority: raised through phase M (the MFMA chains issue ahead of other waves' VALU)
     "SP1": [("            /* ---------------- phase M: matrixing on the matrix cores ------- */",
              "            __builtin_amdgcn_s_setprio(2);\n            /* ---------------- phase M: matrixing on the matrix cores ------- */"),
