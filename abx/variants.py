@@ -80,6 +80,20 @@ VARS = {
              "                    __builtin_amdgcn_s_setprio(1);\n                    for (; __ballot(k < bv2); k += 8) {"),
             ("                    /* count1 quadruples until the part2_3 end; a quadruple that",
              "                    __builtin_amdgcn_s_setprio(0);\n                    /* count1 quadruples until the part2_3 end; a quadruple that")],
+    # k_synth: priority 1 while a phase issues its LDS reads, 0 for its arithmetic (on top of phase Q at 1):
+    # phase W's X reads (SW1), phase I's spectrum reads (SI1), phase M's S reads (SM1)
+    "SW1": [("                float xa[18], xb[18];",
+             "                __builtin_amdgcn_s_setprio(1);\n                float xa[18], xb[18];"),
+            ("                /* output slots in pairs (t0, t1): lanes 0-31 hold L, lanes",
+             "                __builtin_amdgcn_s_setprio(0);\n                /* output slots in pairs (t0, t1): lanes 0-31 hold L, lanes")],
+    "SI1": [("                float x[18], up[8], dn[8];",
+             "                __builtin_amdgcn_s_setprio(1);\n                float x[18], up[8], dn[8];"),
+            ("                /* alias reduction (ISO 2.4.3.4): all 31 boundaries (long),",
+             "                __builtin_amdgcn_s_setprio(0);\n                /* alias reduction (ISO 2.4.3.4): all 31 boundaries (long),")],
+    "SM1": [("                float Be[3][4], Bo[3][4];",
+             "                __builtin_amdgcn_s_setprio(1);\n                float Be[3][4], Bo[3][4];"),
+            ("                f32x4 ce[3], co[3];",
+             "                __builtin_amdgcn_s_setprio(0);\n                f32x4 ce[3], co[3];")],
     # k_synth wave priority: raised through phase M (the MFMA chains issue ahead of other waves' VALU)
     "SP1": [("            /* ---------------- phase M: matrixing on the matrix cores ------- */",
              "            __builtin_amdgcn_s_setprio(2);\n            /* ---------------- phase M: matrixing on the matrix cores ------- */"),
