@@ -94,6 +94,22 @@ VARS = {
              "                __builtin_amdgcn_s_setprio(1);\n                float Be[3][4], Bo[3][4];"),
             ("                f32x4 ce[3], co[3];",
              "                __builtin_amdgcn_s_setprio(0);\n                f32x4 ce[3], co[3];")],
+    # k_synth: the next granule's prefetch issued at the start of phase Q (right after the current is[] words
+    # are copied), phase Q reading the current meta words from a copy (PF1)
+    "PF1": [("                    for (int i = 0; i < 5; i++) cis[c][i] = nis[c][i];",
+             "                    for (int i = 0; i < 5; i++) cis[c][i] = nis[c][i];\n"
+             "                const uint32_t cmeta = nmeta;\n"
+             "                if (PF == 0 && (LSF ? f + 1 < f1 : (gr == 0 || f + 1 < f1))) prefetch(LSF ? 2 * f + 2 : 2 * f + gr + 1);"),
+            ("                if (PF == 0 && (LSF ? f + 1 < f1 : (gr == 0 || f + 1 < f1))) prefetch(LSF ? 2 * f + 2 : 2 * f + gr + 1);\n                /* scatter",
+             "                /* scatter"),
+            ("((uint32_t *)&Wd.m[0])[lane] = nmeta;", "((uint32_t *)&Wd.m[0])[lane] = cmeta;"),
+            ("readlane((int)nmeta, 10)", "readlane((int)cmeta, 10)"),
+            ("readlane((int)nmeta, 11)", "readlane((int)cmeta, 11)"),
+            ("readlane((int)nmeta, 12)", "readlane((int)cmeta, 12)"),
+            ("readlane((int)nmeta, MW + 10)", "readlane((int)cmeta, MW + 10)"),
+            ("readlane((int)nmeta, MW + 11)", "readlane((int)cmeta, MW + 11)"),
+            ("readlane((int)nmeta, MW + 12)", "readlane((int)cmeta, MW + 12)"),
+            ("__shfl((int)nmeta, cbase", "__shfl((int)cmeta, cbase")],
     # k_synth wave priority: raised through phase M (the MFMA chains issue ahead of other waves' VALU)
     "SP1": [("            /* ---------------- phase M: matrixing on the matrix cores ------- */",
              "            __builtin_amdgcn_s_setprio(2);\n            /* ---------------- phase M: matrixing on the matrix cores ------- */"),
