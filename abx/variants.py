@@ -170,8 +170,8 @@ VARS = {
              "        synth_tables<F32, LSF, 192>(T, tab, tid - 64);\n        if (wv == 1) FT(3);\n"),
             ("    __syncthreads(); /* rec, side words, md region and state visible to the workgroup */\n",
              "    __syncthreads(); /* rec, side words, md region and state visible to the workgroup */\n    if (wv == 0) FT(5);\n"),
-            ("    __syncthreads(); /* is[] rows and UnitMeta visible to wave 0 */\n",
-             "    FT(6 + wv);\n    __syncthreads(); /* is[] rows and UnitMeta visible to wave 0 */\n    if (wv == 0) FT(10);\n"),
+            ("    __syncthreads(); /* is[] rows and UnitMeta visible to the synthesis waves */\n",
+             "    FT(6 + wv);\n    __syncthreads(); /* is[] rows and UnitMeta visible to the synthesis waves */\n    if (wv == 0) FT(10);\n"),
             ("        __threadfence_system(); /* PCM, frame info and state before the completion word */\n",
              "        FT(11);\n        __threadfence_system(); /* PCM, frame info and state before the completion word */\n        FT(12);\n"
              "        if (lane == 0) g_fdbg[21] = __builtin_amdgcn_s_memrealtime();\n"),
