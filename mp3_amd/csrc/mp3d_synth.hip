@@ -999,8 +999,9 @@ __global__ void __launch_bounds__(256) k_gather_frames(const uint4 *__restrict__
 /* mapped pinned buffer into LDS (one bus round trip) and demuxes it        */
 /* (demux_stream, input from LDS) while waves 1-3 stage the Huffman and     */
 /* synthesis tables; then the four waves decode the frame's granule         */
-/* channels (huffman_wave_unit), wave 0 synthesises the PCM straight into   */
-/* the mapped output (synth_stream) and, after a system-scope fence, writes */
+/* channels (huffman_wave_unit), waves 0 and 1 synthesise the PCM of one   */
+/* granule each (MPEG-1; one wave for LSF) straight into the mapped output */
+/* (synth_stream PF = 1, 2) and wave 0, after a system-scope fence, writes  */
 /* the call's sequence number into a mapped completion word the host polls  */
 /* (no stream synchronisation).  The hand-offs between the phases use the   */
 /* batch's device buffers exactly as the three-kernel path does, so the     */
