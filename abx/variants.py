@@ -110,6 +110,12 @@ VARS = {
             ("readlane((int)nmeta, MW + 11)", "readlane((int)cmeta, MW + 11)"),
             ("readlane((int)nmeta, MW + 12)", "readlane((int)cmeta, MW + 12)"),
             ("__shfl((int)nmeta, cbase", "__shfl((int)cmeta, cbase")],
+    # compiler scheduling knobs (all kernels): max-ILP / max-memory-clause strategies, latency-leaning metric
+    # bias, LLVM's automatic wave-priority pass
+    "SC1": [("FLAGS", "-mllvm"), ("FLAGS", "-amdgpu-sched-strategy=max-ilp")],
+    "SC2": [("FLAGS", "-mllvm"), ("FLAGS", "-amdgpu-sched-strategy=max-memory-clause")],
+    "SC3": [("FLAGS", "-mllvm"), ("FLAGS", "-amdgpu-schedule-metric-bias=0")],
+    "SC4": [("FLAGS", "-mllvm"), ("FLAGS", "-amdgpu-set-wave-priority")],
     # k_synth wave priority: raised through phase M (the MFMA chains issue ahead of other waves' VALU)
     "SP1": [("            /* ---------------- phase M: matrixing on the matrix cores ------- */",
              "            __builtin_amdgcn_s_setprio(2);\n            /* ---------------- phase M: matrixing on the matrix cores ------- */"),
