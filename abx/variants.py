@@ -116,6 +116,8 @@ VARS = {
     "SC2": [("FLAGS", "-mllvm"), ("FLAGS", "-amdgpu-sched-strategy=max-memory-clause")],
     "SC3": [("FLAGS", "-mllvm"), ("FLAGS", "-amdgpu-schedule-metric-bias=0")],
     "SC4": [("FLAGS", "-mllvm"), ("FLAGS", "-amdgpu-set-wave-priority")],
+    # k_synth streams per workgroup: 6 (two 6-wave workgroups per CU at 3 waves/SIMD; tables staged once per 6)
+    "SW6": [("#define SYN_WAVES 4", "#define SYN_WAVES 6")],
     # k_synth wave priority: raised through phase M (the MFMA chains issue ahead of other waves' VALU)
     "SP1": [("            /* ---------------- phase M: matrixing on the matrix cores ------- */",
              "            __builtin_amdgcn_s_setprio(2);\n            /* ---------------- phase M: matrixing on the matrix cores ------- */"),
