@@ -31,16 +31,8 @@ namespace mp3d {
 #define HUFF_CAPW 2400 /* LDS words per wave (9.6 KB): staging + round order    */
 #define HUFF_STAGEW (HUFF_CAPW - HUFF_SUPER / 2) /* staging words; the u16 order follows */
 
-/* 64 bits of a staged (big-endian word) bitstream starting at bit pos;
- * 64-bit funnel shifts keep it branch-free (sh = 0 included) */
-__device__ __forceinline__ void win64(const uint32_t *bits, uint32_t pos, uint32_t &hi, uint32_t &lo) {
-    uint32_t w = pos >> 5;
-    w = w < HUFF_CAPW ? w : HUFF_CAPW;
-    const uint32_t sh = 32u - (pos & 31u);
-    const uint32_t w0 = bits[w], w1 = bits[w + 1], w2 = bits[w + 2];
-    hi = (uint32_t)((((uint64_t)w0 << 32) | w1) >> sh);
-    lo = (uint32_t)((((uint64_t)w1 << 32) | w2) >> sh);
-}
+/* 32 bits of a staged (big-endian word) bitstream starting at bit pos (the
+ * scalefactor readers; a 64-bit funnel shift, so sh = 0 needs no case) */
 __device__ __forceinline__ uint32_t win32(const uint32_t *bits, uint32_t pos) {
     uint32_t w = pos >> 5;
     w = w < HUFF_CAPW ? w : HUFF_CAPW;
@@ -67,10 +59,6 @@ __device__ __forceinline__ uint32_t win32g(const uint32_t *bits, uint32_t pos) {
 /* top 32 bits of (hi:lo) << n for 1 <= n <= 32 (n = 0 gives lo, not hi) */
 __device__ __forceinline__ uint32_t shl64hi_a(uint32_t hi, uint32_t lo, uint32_t n) {
     return __builtin_amdgcn_alignbit(hi, lo, 32u - n);
-}
-/* top 32 bits of (hi:lo) << n, 0 <= n <= 32 */
-__device__ __forceinline__ uint32_t shl64hi(uint32_t hi, uint32_t lo, uint32_t n) {
-    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (32u - n));
 }
 
 /* Scalefactors are built in 10 packed registers (byte j of UnitMeta.sf in
