@@ -118,6 +118,9 @@ VARS = {
     "SC4": [("FLAGS", "-mllvm"), ("FLAGS", "-amdgpu-set-wave-priority")],
     # k_synth streams per workgroup: 6 (two 6-wave workgroups per CU at 3 waves/SIMD; tables staged once per 6)
     "SW6": [("#define SYN_WAVES 4", "#define SYN_WAVES 6")],
+    # phase-Q priority also on the synth-only (C2) entry (SPX)
+    "SPX": [("            if (!SRC_XR) __builtin_amdgcn_s_setprio(1);", "            __builtin_amdgcn_s_setprio(1);"),
+            ("            if (!SRC_XR) __builtin_amdgcn_s_setprio(0);", "            __builtin_amdgcn_s_setprio(0);")],
     # k_synth wave priority: raised through phase M (the MFMA chains issue ahead of other waves' VALU)
     "SP1": [("            /* ---------------- phase M: matrixing on the matrix cores ------- */",
              "            __builtin_amdgcn_s_setprio(2);\n            /* ---------------- phase M: matrixing on the matrix cores ------- */"),
