@@ -228,8 +228,9 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                                              const uint8_t *__restrict__ xr_bt, const uint8_t *__restrict__ xr_mixed,
                                              const DevTables *__restrict__ tab, StreamState *__restrict__ st,
                                              void *__restrict__ pcm, int F, int xr_nch, int xr_sr, int seg_len,
-                                             float *__restrict__ st_tail, SynShared<LSF> &T, SynWave &Wd, int s,
-                                             int seg, int nseg, float *xch = nullptr) {
+                                             float *__restrict__ st_tail, const float *__restrict__ st_tail_in,
+                                             SynShared<LSF> &T, SynWave &Wd, int s, int seg, int nseg,
+                                             float *xch = nullptr) {
     static_assert(PF == 0 || (!SRC_XR && !LSF), "PF: k_frame's MPEG-1 decode path only");
     const int f0 = seg * seg_len, f1 = min(F, f0 + seg_len);
     const int fw = seg ? f0 - 1 : 0; /* first frame decoded (warm-up below f0) */
@@ -245,13 +246,18 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
     /* synthesis history: ha[k] = X_{k-14}[wa], hb[k] = X_{k-15}[wb] (slot
      * index relative to the granule's first slot; fifo[t] = slot t - 15)  */
     float ha[14], hb[15];
+    constexpr int TAIL = (int)(sizeof(S.overlap) + sizeof(S.fifo)) / 4; /* floats per stream tail */
     if (seg == 0) {
+        /* state in: StreamState, or the previous synth-only call's tail
+         * (the same overlap + fifo layout, packed per stream) */
+        const float *ovi = st_tail_in ? st_tail_in + (size_t)s * TAIL : &S.overlap[0][0][0];
+        const float *ffi = ovi + sizeof(S.overlap) / 4;
 #pragma unroll
-        for (int i = 0; i < 18; i++) ov[i] = S.overlap[ch][sb][i];
+        for (int i = 0; i < 18; i++) ov[i] = ovi[(ch * 32 + sb) * 18 + i];
 #pragma unroll
-        for (int k = 0; k < 14; k++) ha[k] = S.fifo[ch][k + 1][wa];
+        for (int k = 0; k < 14; k++) ha[k] = ffi[(ch * MP3D_FIFO_SLOTS + k + 1) * 32 + wa];
 #pragma unroll
-        for (int k = 0; k < 15; k++) hb[k] = S.fifo[ch][k][wb];
+        for (int k = 0; k < 15; k++) hb[k] = ffi[(ch * MP3D_FIFO_SLOTS + k) * 32 + wb];
     } else {
 #pragma unroll
         for (int i = 0; i < 18; i++) ov[i] = 0.f;
@@ -546,12 +552,18 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                      * nzR bit = right-channel band idx holding a nonzero line. */
                     /* no intensity for is_pos >= 7 (MPEG-1), >= 16 (LSF, FFmpeg) */
                     constexpr int IS_ILLEGAL = LSF ? 16 : 7;
+                    /* a line counts as nonzero from FFmpeg's fixed-point
+                     * resolution up: its requantiser rounds |xr| below
+                     * 0.5 * 1.759 * 2^-28 to 0 (oracle ORC_FFMPEG_FLUSH,
+                     * pinned by the probe_flush_* fixtures) */
+                    constexpr float FLUSH = 0.5f * 1.759f / 268435456.0f;
                     uint64_t nzR = 0;
 #pragma unroll
                     for (int i = 0; i < 5; i++) {
                         const int l0 = 2 * lane + 128 * i;
                         const uint32_t tv2 = (i < 4 || lane < 32) ? lpair[var[1]][l0 >> 1] : 0u;
-                        if (XV(1, 2 * i) != 0.f || XV(1, 2 * i + 1) != 0.f) nzR |= 1ull << ((tv2 >> 2) & 63u);
+                        if (fmaxf(fabsf(XV(1, 2 * i)), fabsf(XV(1, 2 * i + 1))) >= FLUSH)
+                            nzR |= 1ull << ((tv2 >> 2) & 63u);
                     }
 #pragma unroll
                     for (int o = 1; o < 64; o <<= 1) nzR |= __shfl_xor(nzR, o);
@@ -917,11 +929,12 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
         }
     }
     /* state out: the stream's last segment.  With several segments the
-     * first one may still be reading S, so the state goes to st_tail (the
-     * overlap + fifo tail of StreamState, copied in by the host after the
-     * launch). */
+     * first one may still be reading the state, so it goes to st_tail (the
+     * overlap + fifo tail of StreamState, packed per stream): the next
+     * synth-only call reads it from there (st_tail_in), any other use of the
+     * handle first copies it into StreamState (mp3d_host.cpp flush_tail). */
     if (f1 == F && PF != 1) {
-        float *ovo = nseg > 1 ? st_tail + (size_t)s * (sizeof(S.overlap) + sizeof(S.fifo)) / 4 : &S.overlap[0][0][0];
+        float *ovo = st_tail ? st_tail + (size_t)s * TAIL : &S.overlap[0][0][0];
         float *ffo = ovo + sizeof(S.overlap) / 4;
 #pragma unroll
         for (int i = 0; i < 18; i++) ovo[(ch * 32 + sb) * 18 + i] = ov[i];
@@ -942,7 +955,8 @@ __global__ void __launch_bounds__(64 * SYN_WAVES) __attribute__((amdgpu_waves_pe
 k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, const UnitMeta *__restrict__ meta,
         const float *__restrict__ xr_in, const uint8_t *__restrict__ xr_bt, const uint8_t *__restrict__ xr_mixed,
         const DevTables *__restrict__ tab, StreamState *__restrict__ st, void *__restrict__ pcm, int n_streams,
-        int F, int xr_nch, int xr_sr, int seg_len, float *__restrict__ st_tail) {
+        int F, int xr_nch, int xr_sr, int seg_len, float *__restrict__ st_tail,
+        const float *__restrict__ st_tail_in) {
     __shared__ __attribute__((aligned(16))) SynShared<LSF> T;
     __shared__ SynWave Wv[SYN_WAVES];
     if (!SRC_XR) {
@@ -967,7 +981,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
     const int s = vs / nseg, seg = vs - s * nseg;
     if (!SRC_XR && (st[s].kind == 2) != LSF) return; /* the other variant's stream */
     synth_stream<SRC_XR, F32, LSF>(rec, is_buf, meta, xr_in, xr_bt, xr_mixed, tab, st, pcm, F, xr_nch, xr_sr, seg_len,
-                                   st_tail, T, Wv[wid], s, seg, nseg);
+                                   st_tail, st_tail_in, T, Wv[wid], s, seg, nseg);
 }
 /* ------------------------------------------------------------------------ */
 /* k_gather_frames: segmented long-stream decode (mp3d_batch_decode_long).  */
@@ -1085,10 +1099,10 @@ __global__ void __launch_bounds__(256) k_frame(const uint8_t *__restrict__ in_ho
     if constexpr (!LSF) if (split) {
         if (wv == 0)
             synth_stream<false, F32, LSF, 1>(rec, is_buf, meta, nullptr, nullptr, nullptr, tab, st, pcm, 1, 2, 0, 1,
-                                             nullptr, T, Wv[0], 0, 0, 1, s_xch);
+                                             nullptr, nullptr, T, Wv[0], 0, 0, 1, s_xch);
         else if (wv == 1)
             synth_stream<false, F32, LSF, 2>(rec, is_buf, meta, nullptr, nullptr, nullptr, tab, st, pcm, 1, 2, 0, 1,
-                                             nullptr, T, Wv[1], 0, 0, 1, s_xch);
+                                             nullptr, nullptr, T, Wv[1], 0, 0, 1, s_xch);
         else {
             __syncthreads();
             __syncthreads();
@@ -1098,7 +1112,7 @@ __global__ void __launch_bounds__(256) k_frame(const uint8_t *__restrict__ in_ho
     }
     if (!split && wv == 0 && fam) {
         synth_stream<false, F32, LSF>(rec, is_buf, meta, nullptr, nullptr, nullptr, tab, st, pcm, 1, 2, 0, 1, nullptr,
-                                      T, Wv[0], 0, 0, 1);
+                                      nullptr, T, Wv[0], 0, 0, 1);
     }
     if (wv == 0) {
         __threadfence_system(); /* PCM, frame info and state before the completion word */
@@ -1147,7 +1161,7 @@ void launch_synth(const FrameRec *rec, const int16_t *is_buf, const UnitMeta *me
 #define MP3D_SYNTH_LAUNCH(F32_, LSF_)                                                                            \
     hipLaunchKernelGGL((k_synth<false, F32_, LSF_>), grid, block, 0, strm, rec, is_buf, meta, (const float *)nullptr, \
                        (const uint8_t *)nullptr, (const uint8_t *)nullptr, tab, st, pcm, n_streams, F, 2, 0, F,     \
-                       (float *)nullptr)
+                       (float *)nullptr, (const float *)nullptr)
     if (f32) {
         if (kinds & 1) MP3D_SYNTH_LAUNCH(true, false);
         if (kinds & 2) MP3D_SYNTH_LAUNCH(true, true);
@@ -1162,11 +1176,11 @@ void launch_synth(const FrameRec *rec, const int16_t *is_buf, const UnitMeta *me
  * streams' final overlap + fifo, which the caller copies into st */
 void launch_synth_xr(const float *xr, const uint8_t *bt, const uint8_t *mixed, const DevTables *tab, StreamState *st,
                      int16_t *pcm, int n_streams, int F, int nch, int sr, int seg_len, float *st_tail,
-                     hipStream_t strm) {
+                     const float *st_tail_in, hipStream_t strm) {
     const int waves = n_streams * ((F + seg_len - 1) / seg_len);
     hipLaunchKernelGGL((k_synth<true, false, false>), dim3((waves + SYN_WAVES - 1) / SYN_WAVES), dim3(64 * SYN_WAVES), 0,
                        strm, (const FrameRec *)nullptr, (const int16_t *)nullptr, (const UnitMeta *)nullptr, xr, bt,
-                       mixed, tab, st, (void *)pcm, n_streams, F, nch, sr, seg_len, st_tail);
+                       mixed, tab, st, (void *)pcm, n_streams, F, nch, sr, seg_len, st_tail, st_tail_in);
 }
 
 void launch_gather_frames(const void *src, void *dst, const void *isrc, void *idst, const int *a, int L, int F, int k0,

@@ -416,6 +416,19 @@ static long orc_huffman(orc_bits *b, const orc_gr *g, int sr_idx, long end_bit, 
 
 /* Requantise, ISO 2.4.3.4: xr = sgn(is)|is|^(4/3) 2^(q/4) with quarter
  * exponent q per line (FFmpeg exponents_from_scale_factors layout). */
+/* FFmpeg's golden decoder is the fixed-point one: a requantised line whose
+ * fixed-point value rounds to 0 IS zero there, and compute_stereo's "band of
+ * the right channel holds a nonzero line" test (the intensity boundary) sees
+ * it as zero.  Its line value is llrint(|is|^(4/3) 2^(q/4) 2^28 / 1.759)
+ * (expval / table_4_3 scale: 2^(FRAC_BITS + 5) over IMDCT_SCALAR), so a line
+ * is zero below |xr| = 0.5 * 1.759 * 2^-28.  Pinned by the FFmpeg fixtures
+ * scale_msis_mixed_32k and probe_flush_* to (1.395, 2.0] * 2^-29
+ * (tests/test_oracle.py::test_flush_threshold_pinned); below 2^-28 of full
+ * scale the flush itself changes no PCM sample. */
+#define ORC_FFMPEG_FLUSH (0.5 * 1.759 / 268435456.0)
+static double g_orc_flush = ORC_FFMPEG_FLUSH;
+/* test hook: move the threshold (0 = float decoder, no flush) */
+ORC_API void orc_set_flush(double t) { g_orc_flush = t < 0 ? ORC_FFMPEG_FLUSH : t; }
 static void orc_requant(const orc_gr *g, int sr_idx, const uint8_t *sf, const int16_t *is, orc_real *xr,
                         int gain_adj) {
     int gain = g->global_gain - 210 + gain_adj;
@@ -436,6 +449,7 @@ static void orc_requant(const orc_gr *g, int sr_idx, const uint8_t *sf, const in
         for (int n = 0; n < MP3D_SFB_LONG_WIDTH[sr_idx][i]; n++, line++) {
             int v = is[line];
             xr[line] = v == 0 ? 0.0 : (v < 0 ? -g_pow43[-v] : g_pow43[v]) * s;
+            if (fabs(xr[line]) < g_orc_flush) xr[line] = 0.0;
         }
     }
     if (g->mixed && long_end < 22) j = 8; /* canonical layout: short bands from sf[8] */
@@ -446,6 +460,7 @@ static void orc_requant(const orc_gr *g, int sr_idx, const uint8_t *sf, const in
             for (int n = 0; n < MP3D_SFB_SHORT_WIDTH[sr_idx][i]; n++, line++) {
                 int v = is[line];
                 xr[line] = v == 0 ? 0.0 : (v < 0 ? -g_pow43[-v] : g_pow43[v]) * s;
+                if (fabs(xr[line]) < g_orc_flush) xr[line] = 0.0;
             }
         }
     }

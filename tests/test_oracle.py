@@ -146,3 +146,32 @@ def test_oracle_crc_option_drops_bad_frames():
     assert np.array_equal(chk[:, :3 * 1152], ref[:, :3 * 1152])
     clean, _ = _oracle.decode_stream(data, opts=_oracle.OPT_CRC_CHECK)
     assert np.array_equal(clean, ref)
+
+
+def test_flush_threshold_pinned():
+    """FFmpeg's fixed-point requantiser rounds |xr| < 0.5 * 1.759 * 2^-28 to 0,
+    and its intensity-stereo boundary then sees the right channel's band as
+    empty (oracle/mp3_oracle.c ORC_FFMPEG_FLUSH).  The probe fixtures pin that
+    threshold from both sides: no flush (the float decoder's rule) or a
+    threshold of 1.30 * 2^-29 misses the FFmpeg output on a probe, 2.05 *
+    2^-29 over-flushes on another, and the derived 1.759 * 2^-29 matches all."""
+    import ctypes
+    L = _oracle.lib()
+    L.orc_set_flush.argtypes = [ctypes.c_double]
+    probes = [n for n in _golden.names() if n.startswith("probe_flush_")] + ["scale_msis_mixed_32k"]
+
+    def worst_over_probes():
+        out = {}
+        for n in probes:
+            data, ref = _golden.case(n)
+            out[n] = _golden.compare(n, _golden.to_int16(_oracle.decode_stream(data)[0]), ref)[0]
+        return out
+
+    try:
+        for t in (0.0, 1.30 * 2.0 ** -29, 2.05 * 2.0 ** -29):
+            L.orc_set_flush(t)
+            assert max(worst_over_probes().values()) > 1, t
+        L.orc_set_flush(-1.0)  # back to the FFmpeg threshold
+        assert max(worst_over_probes().values()) <= 1
+    finally:
+        L.orc_set_flush(-1.0)
