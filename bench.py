@@ -254,10 +254,12 @@ def setup_decode(c, cfg_name):
     cfg = _gen.C3 if cfg_name == "c3" else _gen.C5
     base = c.seed if c.seed is not None else shard.BASE_SEED_C3 if cfg_name == "c3" else 5_000_011
     t0 = time.time()
-    buf, offs, sizes = _gen.batch(cfg, shard.shard_seed_base(c.rank, c.n, base), c.n, c.F,
-                                  threads=min(16, host_threads()))
-    log("rank %d: generated %d streams x %d frames (%.1f MB) in %.1fs" % (c.rank, c.n, c.F, buf.size / 1e6,
-                                                                        time.time() - t0))
+    # the ranks share the host: each generates with its share of the threads
+    c.gen_threads = max(1, min(16, host_threads() // c.world))
+    buf, offs, sizes = _gen.batch(cfg, shard.shard_seed_base(c.rank, c.n, base), c.n, c.F, threads=c.gen_threads)
+    c.setup_s = time.time() - t0
+    log("rank %d: generated %d streams x %d frames (%.1f MB) on %d threads in %.1fs"
+        % (c.rank, c.n, c.F, buf.size / 1e6, c.gen_threads, c.setup_s))
     c.buf, c.offs, c.sizes = buf, offs, sizes
     c.d_in = torch.from_numpy(buf).to(c.dev)
     c.pcm = [torch.empty((c.n, c.F, 2304), dtype=torch.int16, device=c.dev) for _ in range(2 if c.gather else 1)]
@@ -268,6 +270,46 @@ def setup_decode(c, cfg_name):
         c.dec.decode(c.d_in, offs, sizes, c.F, pcm=c.pcm[k % len(c.pcm)], infos=c.infos, stream=c.strm)
     c.step = step
     c.in_bytes = int(sizes.astype(np.int64).sum())
+    c.cfg_gen, c.seed_base = cfg, base
+
+
+def setup_streaming(c, segments):
+    """The streaming loop of a server or player: streams
+    of segments x F frames, and step k decodes frames [F (k mod segments),
+    F (k mod segments) + F) of every stream, so the stream geometry (offsets
+    and sizes) handed to mp3d_batch_decode changes on EVERY call; the
+    decoder state carries on in HBM (after the last segment the streams run
+    on from their first frame, like concatenated files).  Each segment's
+    offsets come from the previous call's frame infos in an untimed setup
+    pass, exactly as a streaming caller advances them."""
+    import torch
+    import _gen
+    import mp3_amd
+    from mp3_amd import shard
+    t0 = time.time()
+    FF = segments * c.F
+    buf, offs, sizes = _gen.batch(c.cfg_gen, shard.shard_seed_base(c.rank, c.n, c.seed_base), c.n, FF,
+                                  threads=c.gen_threads)
+    d_in = torch.from_numpy(buf).to(c.dev)
+    dec = mp3_amd.BatchDecoder(c.n, c.F, device=c.gpu)
+    infos = torch.zeros((c.n, c.F, 6), dtype=torch.int32, device=c.dev)
+    geo, pos = [], offs.astype(np.uint64).copy()
+    end = offs.astype(np.uint64) + sizes.astype(np.uint64)
+    for j in range(segments):
+        sz = (end - pos).astype(np.uint32)  # the rest of each stream, as a streaming caller hands it over
+        dec.decode(d_in, pos, sz, c.F, pcm=c.pcm[0], infos=infos, stream=c.strm)
+        used = infos[..., 0].sum(1).cpu().numpy().astype(np.uint64)
+        geo.append((pos.copy(), sz))
+        pos = pos + used
+    dec.reset()
+    log("rank %d: streaming set-up (%d streams x %d frames, %d segments) in %.1fs"
+        % (c.rank, c.n, FF, segments, time.time() - t0))
+    c.stream_buf = (buf, d_in, dec, infos, geo)
+
+    def step(k=0):
+        o, z = geo[k % segments]
+        dec.decode(d_in, o, z, c.F, pcm=c.pcm[k % len(c.pcm)], infos=infos, stream=c.strm)
+    return step
 
 
 def setup_synth(c):
@@ -356,6 +398,9 @@ def main():
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse the "
                          "multi-rank path, e.g. several ranks on one GPU)")
+    ap.add_argument("--streaming", type=int, default=None, metavar="SEGMENTS",
+                    help="also time the streaming loop: streams of SEGMENTS x frames, each step decoding the next "
+                         "frames (new offsets every call); reported as `streaming` (default 4 at N = 1, 0 = off)")
     ap.add_argument("--plumbing", action="store_true",
                     help="no GPU: exercise the launcher, rendezvous, sharding, barriers, max-over-ranks timing and "
                          "the gather on CPU tensors (gloo); value is null (tests/test_bench_launch.py)")
@@ -397,13 +442,29 @@ def main():
             if c.gpu is not None:
                 torch.cuda.set_device(c.gpu)
             dist.init_process_group(backend)
+        # what the initialised group reports, not the environment
+        world, backend = dist.get_world_size(), dist.get_backend()
+        c.world = world
     cfg = {2: "c2", 3: "c3", 4: "c3", 5: "c5"}[args.config]
     c.n = args.streams or (1024 if cfg == "c2" else 65536)
     c.F = args.frames or (64 if cfg == "c2" else 32)
+    c.gen_threads = max(1, min(16, host_threads() // world))
+    c.setup_s = 0.0
+    if args.gather and world > 1:
+        # rank 0's receive lists (one per gather in flight) must fit beside
+        # the batch buffers; checked at the FULL per-rank size even when
+        # --plumbing shrinks the data
+        plan = shard.gather_plan(c.n, c.F, world, decoder_bytes=decoder_bytes(c.n, c.F))
+        if not plan["fits"]:
+            raise SystemExit("bench.py: the --gather receive lists need %.1f GB on rank 0, more than %.1f GB"
+                             % (plan["need_bytes"] / 1e9, plan["device_bytes"] / 1e9))
+        c.gather_plan = plan
     if args.plumbing:
         import _gen
         c.n, c.F = min(c.n, 8), min(c.F, 4)
-        buf, offs, sizes = _gen.batch(_gen.C3, shard.shard_seed_base(rank, c.n), c.n, c.F, threads=1)
+        t0 = time.time()
+        buf, offs, sizes = _gen.batch(_gen.C3, shard.shard_seed_base(rank, c.n), c.n, c.F, threads=c.gen_threads)
+        c.setup_s = time.time() - t0
         c.pcm = [torch.full((c.n, c.F, 2304), rank, dtype=torch.int16) for _ in range(2 if c.gather else 1)]
         c.step = lambda k=0: None
         sync = lambda: None  # noqa: E731
@@ -455,11 +516,37 @@ def main():
         c.dec.set_timing(False)
         sync()
 
+    # --- streaming loop: new stream geometry on every call ----------------
+    streaming = None
+    segs = args.streaming if args.streaming is not None else (4 if world == 1 else 0)
+    if segs > 0 and cfg != "c2" and not args.plumbing:
+        sstep = setup_streaming(c, segs)
+        for k in range(args.warmup):
+            sstep(k)
+        if world > 1:
+            dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            sstep(k)
+        sync()
+        if world > 1:
+            dist.barrier()
+        sdt = shard.max_over_ranks(time.perf_counter() - t0, c.dev)
+        sval = sum(per_rank_frames) * args.steps / sdt
+        streaming = {"value": sval, "ms_per_step": sdt / args.steps * 1e3, "segments": segs,
+                     "vs_fixed_offsets": sval / value,
+                     "note": "streams of %d x %d frames; step k decodes frames [%d (k mod %d), +%d) of every stream, "
+                             "so offsets and sizes change on every mp3d_batch_decode call (async geometry staging)"
+                             % (segs, c.F, c.F, segs, c.F)}
+        c.stream_buf = None
+
     # --- optional RCCL PCM gather, overlapped with the next step ----------
     gather = None
     if args.gather and world > 1:
         gather = time_gather(c, args, dist, shard, torch, sync)
 
+    setup_all = shard.all_ranks(c.setup_s, c.dev)  # collective: every rank takes part
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -468,7 +555,8 @@ def main():
            "ranks": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
            "per_rank_frames_per_s": [f * args.steps / t for f, t in zip(per_rank_frames, per_rank_dt)],
-           "dist_backend": backend if world > 1 else None}
+           "dist_backend": backend if world > 1 else None,
+           "setup_s_per_rank": setup_all, "gen_threads_per_rank": c.gen_threads}
     if args.plumbing:
         res.update(plumbing_only=True, data="synthetic C3 shard per rank (generated, not decoded)",
                    config={"workload": "plumbing rehearsal: %d ranks x %d streams x %d frames" % (world, c.n, c.F),
@@ -480,6 +568,8 @@ def main():
         res.update(report_decode(c, args, cfg, value, kt, frames_per_step))
     if gather:
         res["gather"] = gather
+    if streaming:
+        res["streaming"] = streaming
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -491,14 +581,17 @@ def time_gather(c, args, dist, shard, torch, sync):
     of step k+2 waits for the gather that read its PCM buffer).  gloo gathers
     host tensors synchronously, so that rehearsal shows no overlap."""
     nbytes = c.pcm[0].numel() * c.pcm[0].element_size()
-    recv = None
+    # one receive list per gather in flight: the two overlapped gathers never
+    # write the same buffers (a real pipelined consumer reads slot b while
+    # the other fills)
+    recv = [None, None]
     if c.rank == 0 and dist.get_backend() != "gloo":
-        recv = [torch.empty_like(c.pcm[0]) for _ in range(c.world)]
+        recv = [[torch.empty_like(c.pcm[0]) for _ in range(c.world)] for _ in range(2)]
     # gather alone (no decode beside it)
     dist.barrier()
     sync()
     tg = time.perf_counter()
-    shard.gather_to_root(c.pcm[0], out=recv)
+    shard.gather_to_root(c.pcm[0], out=recv[0])
     sync()
     alone = shard.max_over_ranks(time.perf_counter() - tg, c.dev)
     pending = [None, None]
@@ -515,7 +608,7 @@ def time_gather(c, args, dist, shard, torch, sync):
             sync()
             shard.gather_to_root(c.pcm[b])
         else:
-            _, pending[b] = shard.gather_to_root(c.pcm[b], async_op=True, out=recv)
+            _, pending[b] = shard.gather_to_root(c.pcm[b], async_op=True, out=recv[b])
     for w in pending:
         if w is not None:
             w.wait()
@@ -526,8 +619,17 @@ def time_gather(c, args, dist, shard, torch, sync):
             "ms_per_step_decode_plus_gather": dt / args.steps * 1e3,
             "frames_per_s_with_gather": c.n * c.F * c.world * args.steps / dt,
             "overlapped": dist.get_backend() != "gloo",
+            "rank0_memory_plan": getattr(c, "gather_plan", None),
             "note": "PCM of step k gathered to rank 0 over RCCL (xGMI) on the process group's stream while step "
                     "k+1 decodes; reported apart from `value`"}
+
+
+def decoder_bytes(n, F):
+    """Device bytes of one BatchDecoder(n, F) plus its resident input (C3
+    sizes): state, frame records, side words, is[] rows, unit meta, infos,
+    md region and the input frames."""
+    units = n * F * 4
+    return int(n * 8832 + n * F * (32 + 24 + 418 + 400) + units * (8 + 1152 + 224))
 
 
 def load_pmc(key, n, F):
@@ -572,7 +674,7 @@ def report_decode(c, args, cfg, value, kt, frames_per_step):
                    "seed": c.seed if c.seed is not None else "default",
                    "parallelism": "streams sharded, 1 process per GPU, no data-path collective"},
         "roofline": {
-            "kernel": "k_synth", "bound": "mfma", "unit": "TFLOP/s",
+            "kernel": "k_synth", "bound": "valu-issue/latency", "roofline_class": "FP32 compute", "unit": "TFLOP/s",
             "achieved": achieved_tf, "peak": FP32_PEAK_TFLOPS, "frac": achieved_tf / FP32_PEAK_TFLOPS,
             "traffic": pmc.get("k_synth_hbm_bytes_per_launch"),
             "limiter": "FP32 compute roofline (vector rate = matrix rate, 157.3 TF); the PMC counters "
@@ -620,7 +722,8 @@ def report_c2(c, args, value, kt):
                    "seed": c.seed if c.seed is not None else "default",
                    "parallelism": "streams sharded, 1 process per GPU, no data-path collective"},
         "roofline": {
-            "kernel": "k_synth<xr>", "bound": "mfma", "unit": "TFLOP/s", "achieved": achieved_tf,
+            "kernel": "k_synth<xr>", "bound": "valu-issue/latency", "roofline_class": "FP32 compute",
+            "unit": "TFLOP/s", "achieved": achieved_tf,
             "peak": FP32_PEAK_TFLOPS, "frac": achieved_tf / FP32_PEAK_TFLOPS,
             "traffic": pmc.get("k_synth_hbm_bytes_per_launch"),
             "flop_per_frame": C2_FLOP_PER_FRAME, "frames_per_launch": fpl, "launch_us": kt["synth"],

@@ -274,25 +274,51 @@ class BatchDecoder:
         _check(fn(self._h, fp, off.ctypes.data, sz.ctypes.data, n, F, pp, ip, ctypes.c_void_p(stream) if stream else None))
         return pcm, infos
 
+    @staticmethod
+    def _nbytes(x):
+        """Byte size of a contiguous host array / device tensor (its element
+        count times element size, whatever the dtype)."""
+        if hasattr(x, "numel"):
+            if not x.is_contiguous():
+                raise ValueError("state tensor must be contiguous")
+            return x.numel() * x.element_size()
+        if not isinstance(x, np.ndarray) or not x.flags.c_contiguous:
+            raise ValueError("state buffer must be a C-contiguous numpy array or tensor")
+        return x.nbytes
+
+    def _state_range(self, first, n):
+        first, n = int(first), int(n)
+        if first < 0 or n <= 0 or first + n > self.max_streams:
+            raise ValueError("streams [%d, %d) outside the handle's %d" % (first, first + n, self.max_streams))
+        return first, n
+
     def get_state(self, first=0, n=None, out=None):
         """State blobs of streams [first, first + n): np.uint8 [n, state_bytes()]
-        (or into `out`, a host array or device tensor of that size)."""
-        n = self.max_streams - first if n is None else int(n)
+        (or into `out`, a host array or device tensor of exactly that many
+        bytes)."""
+        first, n = self._state_range(first, self.max_streams - int(first) if n is None else n)
         if out is None:
             out = np.zeros((n, state_bytes()), np.uint8)
+        if self._nbytes(out) != n * state_bytes():
+            raise ValueError("out holds %d bytes, %d streams need %d" % (self._nbytes(out), n, n * state_bytes()))
         op, k = _ptr(out)
-        _check(lib().mp3d_batch_get_state(self._h, int(first), n, op))
+        _check(lib().mp3d_batch_get_state(self._h, first, n, op))
         return out
 
     def set_state(self, buf, first=0):
-        """Restore state blobs [n, state_bytes()] into streams [first, first + n)."""
-        n = (buf.numel() if hasattr(buf, "numel") else np.asarray(buf).size) // state_bytes()
-        if hasattr(buf, "numel"):
-            bp, k = _ptr(buf)
-        else:
-            buf = np.ascontiguousarray(buf, np.uint8)
-            bp, k = buf.ctypes.data, buf
-        _check(lib().mp3d_batch_set_state(self._h, int(first), int(n), bp))
+        """Restore state blobs [n, state_bytes()] into streams [first, first + n);
+        buf is a contiguous host array or device tensor of n * state_bytes()
+        bytes (any dtype: the byte count decides n)."""
+        if not hasattr(buf, "numel"):
+            buf = np.asarray(buf)
+            if not buf.flags.c_contiguous:
+                raise ValueError("state buffer must be C-contiguous")
+        nb = self._nbytes(buf)
+        if nb == 0 or nb % state_bytes():
+            raise ValueError("state buffer of %d bytes is not a whole number of %d-byte blobs" % (nb, state_bytes()))
+        first, n = self._state_range(first, nb // state_bytes())
+        bp, k = _ptr(buf)
+        _check(lib().mp3d_batch_set_state(self._h, first, n, bp))
 
     def stream_info(self, n_streams):
         """[StreamInfo] of the first n_streams streams (after a decode call)."""

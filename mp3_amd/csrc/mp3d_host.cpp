@@ -33,7 +33,7 @@ void launch_huffman(const uint8_t *, const uint64_t *, const FrameRec *, const u
 void launch_synth(const FrameRec *, const int16_t *, const UnitMeta *, const DevTables *, StreamState *, void *, bool, int,
                   int, int, hipStream_t);
 void launch_synth_xr(const float *, const uint8_t *, const uint8_t *, const DevTables *, StreamState *, int16_t *, int,
-                     int, int, int, int, float *, hipStream_t);
+                     int, int, int, int, float *, const float *, hipStream_t);
 void launch_gather_frames(const void *, void *, const void *, void *, const int *, int, int, int, int, int,
                           hipStream_t);
 hipError_t upload_frame_constants(const uint16_t *);
@@ -316,8 +316,26 @@ struct mp3d_batch {
     uint64_t *sideu = nullptr; /* per-unit side info (k_demux -> k_huffman) */
     int16_t *is_buf = nullptr;
     UnitMeta *meta = nullptr;
-    uint64_t *d_in_off = nullptr, *d_md_off = nullptr;
-    uint32_t *d_in_len = nullptr;
+    /* Stream geometry of a call (input offsets, sizes, md-region offsets) in
+     * two device slots, each filled from its own pinned host buffer by an
+     * async copy on the handle's copy stream: a call with new geometry (a
+     * streaming loop's offsets advance every call) stages it and returns
+     * without waiting; the copy overlaps the previous call's kernels.
+     * Layout per slot for a call of n streams: in_off[n] u64, md_off[n] u64,
+     * in_len[n] u32. */
+    struct Geo {
+        uint64_t *d = nullptr;
+        uint64_t *h = nullptr;       /* pinned */
+        hipEvent_t staged = nullptr; /* the copy h -> d is complete        */
+        hipEvent_t freed = nullptr;  /* the last kernel reading d is done */
+        bool fresh = false;          /* freed recorded by the slot's last reader */
+        int n = -1;
+        uint64_t *in_off() const { return d; }
+        uint64_t *md_off() const { return d + n; }
+        uint32_t *in_len() const { return (uint32_t *)(d + 2 * (size_t)n); }
+    } geo[2];
+    int geo_i = 0;
+    hipStream_t copy = nullptr;
     mp3d_frame_info *d_infos = nullptr;
     uint8_t *md = nullptr;
     size_t md_cap = 0;
@@ -328,15 +346,66 @@ struct mp3d_batch {
     float *d_xr = nullptr;
     uint8_t *d_bt = nullptr, *d_mx = nullptr;
     size_t xr_cap = 0;
-    float *st_tail = nullptr; /* segmented synth: final overlap + fifo per stream */
-    size_t tail_cap = 0;
-    std::vector<uint64_t> last_off, md_off_host;
-    std::vector<uint32_t> last_len;
-    int last_n = -1;
+    /* segmented synth-only calls: the final overlap + fifo per stream go to
+     * a packed tail (the first segment may still be reading the state), and
+     * the next synth-only call reads them from there: two tails used in
+     * turn, so steady config-2 calls never copy state.  tail_live = the tail
+     * holding streams [0, tail_n)'s current overlap + fifo (-1: StreamState
+     * does); any other use of the handle first copies it back (flush_tail). */
+    float *st_tail[2] = {};
+    size_t tail_cap[2] = {};
+    int tail_live = -1, tail_n = 0;
     bool timing = false;
     int opts = 0; /* MP3D_OPT_* */
-    hipStream_t last = nullptr; /* stream of the last call (caller's or own) */
+    /* End of the handle's last call when it ran on a caller's stream,
+     * recorded on that stream: sync, reset and state copies wait on this
+     * event, never on the caller's stream handle (which the caller may have
+     * destroyed since), and a call on another stream is ordered after it.
+     * Calls on the handle's own stream (the per-frame decoder) record
+     * nothing: own-stream order covers them. */
+    hipEvent_t ev_done = nullptr;
+    hipStream_t last_s = nullptr; /* compared with the next call's, never used */
     hipEvent_t ev[4] = {};
+};
+
+/* an event after all of the handle's work issued so far */
+static hipEvent_t end_event(mp3d_batch *b) {
+    if (!b->last_s || b->last_s == b->own) (void)hipEventRecord(b->ev_done, b->own);
+    return b->ev_done;
+}
+
+static constexpr size_t STATE_TAIL = sizeof(((StreamState *)0)->overlap) + sizeof(((StreamState *)0)->fifo);
+
+/* the live synth-only tail back into StreamState (on stream s) */
+static int flush_tail(mp3d_batch *b, hipStream_t s) {
+    if (b->tail_live < 0) return MP3D_OK;
+    HIPCHK(hipMemcpy2DAsync(&b->st[0].overlap[0][0][0], sizeof(StreamState), b->st_tail[b->tail_live], STATE_TAIL,
+                            STATE_TAIL, b->tail_n, hipMemcpyDeviceToDevice, s));
+    b->tail_live = -1;
+    return MP3D_OK;
+}
+
+/* a call on stream s: order it after the handle's previous call when that
+ * one ran on another stream (the handle's buffers are shared) */
+static int call_begin(mp3d_batch *b, hipStream_t s) {
+    HIPCHK(hipSetDevice(b->device));
+    if (b->last_s && b->last_s != s) HIPCHK(hipStreamWaitEvent(s, end_event(b), 0));
+    return MP3D_OK;
+}
+
+/* the own stream (sync, reset, state copies) after the handle's last call */
+static int own_after_last(mp3d_batch *b) {
+    if (b->last_s && b->last_s != b->own) HIPCHK(hipStreamWaitEvent(b->own, b->ev_done, 0));
+    return MP3D_OK;
+}
+
+/* when a public call returns: ev_done on a caller's stream */
+struct CallEnd {
+    mp3d_batch *b;
+    hipStream_t s;
+    ~CallEnd() {
+        if (s == b->own || hipEventRecord(b->ev_done, s) == hipSuccess) b->last_s = s;
+    }
 };
 
 static bool is_device_ptr(const void *p) {
@@ -384,12 +453,17 @@ extern "C" int mp3d_batch_create(int device, int max_streams, int max_frames, mp
     BALLOC(b->sideu, sizeof(uint64_t) * units);
     BALLOC(b->is_buf, sizeof(int16_t) * 576 * units);
     BALLOC(b->meta, sizeof(UnitMeta) * units);
-    BALLOC(b->d_in_off, sizeof(uint64_t) * max_streams);
-    BALLOC(b->d_md_off, sizeof(uint64_t) * max_streams);
-    BALLOC(b->d_in_len, sizeof(uint32_t) * max_streams);
+    for (auto &g : b->geo) BALLOC(g.d, 20 * (size_t)max_streams);
     BALLOC(b->d_infos, sizeof(mp3d_frame_info) * (size_t)max_streams * max_frames);
 #undef BALLOC
-    if (hipStreamCreateWithFlags(&b->own, hipStreamNonBlocking) != hipSuccess) {
+    bool ok = hipStreamCreateWithFlags(&b->own, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&b->copy, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&b->ev_done, hipEventDisableTiming) == hipSuccess;
+    for (auto &g : b->geo)
+        ok = ok && hipHostMalloc((void **)&g.h, 20 * (size_t)max_streams) == hipSuccess &&
+             hipEventCreateWithFlags(&g.staged, hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&g.freed, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
         mp3d_batch_destroy(b);
         return MP3D_E_HIP;
     }
@@ -405,20 +479,32 @@ extern "C" int mp3d_batch_create(int device, int max_streams, int max_frames, mp
 extern "C" void mp3d_batch_destroy(mp3d_batch *b) {
     if (!b) return;
     (void)hipSetDevice(b->device);
+    if (b->ev_done) (void)hipEventSynchronize(b->ev_done);
     if (b->own) (void)hipStreamSynchronize(b->own);
-    void *ptrs[] = {b->st, b->rec, b->sideu, b->is_buf, b->meta, b->d_in_off, b->d_md_off, b->d_in_len,
-                    b->d_infos, b->md, b->d_in, b->d_pcm, b->d_xr, b->d_bt, b->d_mx, b->st_tail};
+    if (b->copy) (void)hipStreamSynchronize(b->copy);
+    void *ptrs[] = {b->st, b->rec, b->sideu, b->is_buf, b->meta, b->geo[0].d, b->geo[1].d,
+                    b->d_infos, b->md, b->d_in, b->d_pcm, b->d_xr, b->d_bt, b->d_mx, b->st_tail[0], b->st_tail[1]};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
+    for (auto &g : b->geo) {
+        if (g.h) (void)hipHostFree(g.h);
+        if (g.staged) (void)hipEventDestroy(g.staged);
+        if (g.freed) (void)hipEventDestroy(g.freed);
+    }
     for (hipEvent_t e : b->ev)
         if (e) (void)hipEventDestroy(e);
+    if (b->ev_done) (void)hipEventDestroy(b->ev_done);
     if (b->own) (void)hipStreamDestroy(b->own);
+    if (b->copy) (void)hipStreamDestroy(b->copy);
     delete b;
 }
 
 extern "C" int mp3d_batch_reset(mp3d_batch *b) {
     if (!b) return MP3D_E_ARG;
     HIPCHK(hipSetDevice(b->device));
+    int r = own_after_last(b);
+    if (r) return r;
+    b->tail_live = -1; /* the state is zeroed whole */
     HIPCHK(hipMemsetAsync(b->st, 0, sizeof(StreamState) * b->max_streams, b->own));
     HIPCHK(hipStreamSynchronize(b->own));
     return MP3D_OK;
@@ -430,13 +516,13 @@ extern "C" int mp3d_batch_set_options(mp3d_batch *b, int flags) {
     return MP3D_OK;
 }
 
-/* waits for this handle's work only: its own stream and the stream of its
- * last call (a caller's hip_stream), never the whole device */
+/* waits for this handle's work only: its last call (through ev_done, on
+ * whatever stream it ran) and its own stream, never the whole device */
 extern "C" int mp3d_batch_sync(mp3d_batch *b) {
     if (!b) return MP3D_E_ARG;
     HIPCHK(hipSetDevice(b->device));
+    if (b->last_s && b->last_s != b->own) HIPCHK(hipEventSynchronize(b->ev_done));
     HIPCHK(hipStreamSynchronize(b->own));
-    if (b->last && b->last != b->own) HIPCHK(hipStreamSynchronize(b->last));
     return MP3D_OK;
 }
 
@@ -478,28 +564,46 @@ static bool huffman_wave(int n_units) {
     return n_units <= MP3D_WAVE_HUFF_UNITS;
 }
 
-/* Upload stream geometry (cached when unchanged) and size the md region. */
+/* small batches (the per-frame decoder, small servers) compare the new
+ * geometry with the current slot's and skip the copy when it is unchanged;
+ * big ones always stage (a memcmp of up to 1.3 MB would cost more) */
+#define MP3D_GEO_CACHE_STREAMS 1024
+
+/* Stage the call's stream geometry (input offsets and sizes, md-region
+ * offsets) into the next device slot, asynchronously (struct Geo), size the
+ * md region, and make stream s wait for the copy.  Never blocks the host
+ * except on the copy of two calls ago. */
 static int prepare_geometry(mp3d_batch *b, const uint64_t *offsets, const uint32_t *sizes, int n, hipStream_t s) {
-    bool same = b->last_n == n && !memcmp(b->last_off.data(), offsets, sizeof(uint64_t) * n) &&
-                !memcmp(b->last_len.data(), sizes, sizeof(uint32_t) * n);
-    if (same) return MP3D_OK;
-    b->last_off.assign(offsets, offsets + n);
-    b->last_len.assign(sizes, sizes + n);
-    b->md_off_host.resize(n);
+    {
+        mp3d_batch::Geo &g = b->geo[b->geo_i];
+        if (n <= MP3D_GEO_CACHE_STREAMS && g.n == n && !memcmp(g.h, offsets, sizeof(uint64_t) * n) &&
+            !memcmp(g.h + 2 * (size_t)n, sizes, sizeof(uint32_t) * n)) {
+            HIPCHK(hipStreamWaitEvent(s, g.staged, 0)); /* a no-op once the copy is done */
+            return MP3D_OK;
+        }
+    }
+    b->geo_i ^= 1;
+    mp3d_batch::Geo &g = b->geo[b->geo_i];
+    HIPCHK(hipEventSynchronize(g.staged)); /* this slot's last copy has read g.h */
+    g.n = n;
+    uint64_t *h_md = g.h + n;
     size_t o = 0;
     for (int i = 0; i < n; i++) {
-        b->md_off_host[i] = o;
+        h_md[i] = o;
         /* carry-in + payloads; a cut-short final frame is completed with
          * zeros, so allow one maximal frame beyond the stream's bytes */
         o += ((size_t)sizes[i] + MP3D_RES_BYTES + MP3D_MAX_FRAME_BYTES + 16 + 15) & ~(size_t)15;
     }
+    memcpy(g.h, offsets, sizeof(uint64_t) * n);
+    memcpy(g.h + 2 * (size_t)n, sizes, sizeof(uint32_t) * n);
+    /* growing md frees the old region: hipFree waits for the device */
     int r = grow((void **)&b->md, &b->md_cap, o + 8192);
     if (r) return r;
-    HIPCHK(hipMemcpyAsync(b->d_in_off, offsets, sizeof(uint64_t) * n, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(b->d_in_len, sizes, sizeof(uint32_t) * n, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(b->d_md_off, b->md_off_host.data(), sizeof(uint64_t) * n, hipMemcpyHostToDevice, s));
-    HIPCHK(hipStreamSynchronize(s)); /* host vectors must outlive the copies */
-    b->last_n = n;
+    /* after the call that last read this slot */
+    HIPCHK(hipStreamWaitEvent(b->copy, g.fresh ? g.freed : end_event(b), 0));
+    HIPCHK(hipMemcpyAsync(g.d, g.h, 20 * (size_t)n, hipMemcpyHostToDevice, b->copy));
+    HIPCHK(hipEventRecord(g.staged, b->copy));
+    HIPCHK(hipStreamWaitEvent(s, g.staged, 0));
     return MP3D_OK;
 }
 
@@ -512,29 +616,34 @@ static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offse
                      mp3d_frame_info *dev_infos = nullptr) {
     if (!b || !frames || !offsets || !sizes || n <= 0 || F <= 0) return MP3D_E_ARG;
     if (n > b->max_streams || F > b->max_frames) return MP3D_E_CAPACITY;
-    HIPCHK(hipSetDevice(b->device));
-    b->last = s;
+    int r = call_begin(b, s);
+    if (r) return r;
+    r = flush_tail(b, s);
+    if (r) return r;
     uint64_t total = 0;
     for (int i = 0; i < n; i++) total = std::max<uint64_t>(total, offsets[i] + sizes[i]);
     const uint8_t *din = frames;
     if (!mapped && !is_device_ptr(frames)) {
-        int r = grow((void **)&b->d_in, &b->in_cap, total + 64);
+        r = grow((void **)&b->d_in, &b->in_cap, total + 64);
         if (r) return r;
         HIPCHK(hipMemcpyAsync(b->d_in, frames, total, hipMemcpyHostToDevice, s));
         din = b->d_in;
         *sync_needed = true;
     }
-    int r = prepare_geometry(b, offsets, sizes, n, s);
+    r = prepare_geometry(b, offsets, sizes, n, s);
     if (r) return r;
+    const mp3d_batch::Geo &g = b->geo[b->geo_i];
     DeviceCtx &dc = g_dev[b->device];
     if (b->timing) HIPCHK(hipEventRecord(b->ev[0], s));
     /* demux + main-data gather: lane-per-stream walk + payload copy for wide
      * batches, one wave per stream below MP3D_WIDE_STREAMS (fewer launches) */
-    launch_demux(din, b->d_in_off, b->d_in_len, b->md, b->d_md_off, b->st, b->rec, b->sideu,
+    launch_demux(din, g.in_off(), g.in_len(), b->md, g.md_off(), b->st, b->rec, b->sideu,
                  dev_infos ? (void *)dev_infos : b->d_infos, n, F, b->opts, demux_wide(n), s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[1], s));
-    launch_huffman(b->md, b->d_md_off, b->rec, b->sideu, dc.tables, b->is_buf, b->meta, n, F, dc.n_cu,
+    launch_huffman(b->md, g.md_off(), b->rec, b->sideu, dc.tables, b->is_buf, b->meta, n, F, dc.n_cu,
                    huffman_wave(n * F * 4), s);
+    HIPCHK(hipEventRecord(g.freed, s)); /* the slot's last reader */
+    b->geo[b->geo_i].fresh = true;
     if (b->timing) HIPCHK(hipEventRecord(b->ev[2], s));
     HIPCHK(hipGetLastError());
     return MP3D_OK;
@@ -551,6 +660,7 @@ static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *of
                         int kinds = 3, bool mapped = false) {
     if (!b || !pcm) return MP3D_E_ARG;
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : b->own;
+    CallEnd done{b, s};
     bool sync_needed = mapped;
     /* frame infos: written in place when the caller's array is device memory
      * (or the per-frame decoder's mapped buffer), else into d_infos and
@@ -633,12 +743,14 @@ extern "C" int mp3d_batch_huffman_only(mp3d_batch *b, const uint8_t *frames, con
                                        void *hip_stream) {
     if (!b) return MP3D_E_ARG;
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : b->own;
+    CallEnd done{b, s};
     bool sync_needed = false;
     size_t units = (size_t)n * F * 4;
     if (n > 0 && F > 0 && n <= b->max_streams && F <= b->max_frames) {
         /* k_huffman stores only each row's nonzero prefix (nz_end); the tap
          * returns whole rows, so clear them first */
-        HIPCHK(hipSetDevice(b->device));
+        int r = call_begin(b, s);
+        if (r) return r;
         HIPCHK(hipMemsetAsync(b->is_buf, 0, units * 576 * sizeof(int16_t), s));
     }
     int r = run_front(b, frames, offsets, sizes, n, F, s, &sync_needed);
@@ -664,9 +776,12 @@ extern "C" int mp3d_batch_synth_only(mp3d_batch *b, const float *xr, const uint8
     if (n > b->max_streams || F > b->max_frames) return MP3D_E_CAPACITY;
     int sr = hz == 44100 ? 0 : hz == 48000 ? 1 : hz == 32000 ? 2 : -1;
     if (sr < 0) return MP3D_E_ARG;
-    HIPCHK(hipSetDevice(b->device));
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : b->own;
-    b->last = s;
+    {
+        int r = call_begin(b, s);
+        if (r) return r;
+    }
+    CallEnd done{b, s};
     bool sync_needed = false;
     size_t nx = (size_t)n * F * 2 * nch;
     const float *dxr = xr;
@@ -711,17 +826,28 @@ extern "C" int mp3d_batch_synth_only(mp3d_batch *b, const float *xr, const uint8
         const char *e = getenv("MP3D_SEG_FRAMES");
         if (e && atoi(e) > 0) seg_len = std::min(F, atoi(e));
     }
-    const size_t tail = sizeof(((StreamState *)0)->overlap) + sizeof(((StreamState *)0)->fifo);
-    if (seg_len < F) {
-        int r = grow((void **)&b->st_tail, &b->tail_cap, tail * (size_t)n);
+    /* state in: the live tail when it holds these n streams, else
+     * StreamState (after copying back a tail of another shape); state out:
+     * the other tail (segments), or StreamState (one segment per stream) */
+    if (b->tail_live >= 0 && (seg_len >= F || b->tail_n != n)) {
+        int r = flush_tail(b, s);
         if (r) return r;
     }
-    launch_synth_xr(dxr, dbt, dmx, dc.tables, b->st, dpcm, n, F, nch, sr, seg_len, b->st_tail, s);
+    const float *tail_in = b->tail_live >= 0 ? b->st_tail[b->tail_live] : nullptr;
+    float *tail_out = nullptr;
+    const int t_out = b->tail_live >= 0 ? b->tail_live ^ 1 : 0;
+    if (seg_len < F) {
+        int r = grow((void **)&b->st_tail[t_out], &b->tail_cap[t_out], STATE_TAIL * (size_t)n);
+        if (r) return r;
+        tail_out = b->st_tail[t_out];
+    }
+    launch_synth_xr(dxr, dbt, dmx, dc.tables, b->st, dpcm, n, F, nch, sr, seg_len, tail_out, tail_in, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[3], s));
     HIPCHK(hipGetLastError());
-    if (seg_len < F) /* the last segments' state into StreamState (overlap, fifo are its tail) */
-        HIPCHK(hipMemcpy2DAsync(&b->st[0].overlap[0][0][0], sizeof(StreamState), b->st_tail, tail, tail, n,
-                                hipMemcpyDeviceToDevice, s));
+    if (seg_len < F) {
+        b->tail_live = t_out;
+        b->tail_n = n;
+    }
     if (pcm_host) {
         HIPCHK(hipMemcpyAsync(pcm, dpcm, pcm_bytes, hipMemcpyDeviceToHost, s));
         sync_needed = true;
@@ -750,9 +876,11 @@ extern "C" int mp3d_batch_stream_info(mp3d_batch *b, int n, mp3d_stream_info *ou
     HIPCHK(hipSetDevice(b->device));
     /* StreamState tag_info, tag_frames, kind: three consecutive words */
     std::vector<uint32_t> tag((size_t)n * 3);
+    int r = own_after_last(b); /* after the handle's last call, on any stream */
+    if (r) return r;
+    HIPCHK(hipMemcpy2DAsync(tag.data(), 3 * sizeof(uint32_t), &b->st[0].tag_info, sizeof(StreamState),
+                            3 * sizeof(uint32_t), n, hipMemcpyDeviceToHost, b->own));
     HIPCHK(hipStreamSynchronize(b->own));
-    HIPCHK(hipMemcpy2D(tag.data(), 3 * sizeof(uint32_t), &b->st[0].tag_info, sizeof(StreamState),
-                       3 * sizeof(uint32_t), n, hipMemcpyDeviceToHost));
     for (int i = 0; i < n; i++) tag_to_info(tag[3 * i], tag[3 * i + 1], (int)tag[3 * i + 2], &out[i]);
     return MP3D_OK;
 }
@@ -809,6 +937,11 @@ extern "C" int mp3d_batch_decode_long(mp3d_batch *b, const uint8_t *data, size_t
     const int F = L + wmax;
     if (F > b->max_frames) return MP3D_E_CAPACITY;
     hipStream_t s = b->own;
+    {
+        int r = own_after_last(b);
+        if (!r) r = flush_tail(b, s); /* before b->st points at the scratch states */
+        if (r) return r;
+    }
     const uint8_t *din = data;
     if (!dev_in) {
         int r = grow((void **)&b->d_in, &b->in_cap, bytes + 64);
@@ -880,7 +1013,6 @@ done:
     if (d_a) (void)hipFree(d_a);
     if (!pcm_dev && out_pcm) (void)hipFree(out_pcm);
     if (infos && !inf_dev && out_inf) (void)hipFree(out_inf);
-    b->last_n = -1; /* geometry cache: the virtual streams are not the caller's */
     return rc;
 }
 
@@ -995,16 +1127,19 @@ extern "C" int mp3d_dec_stream_info(mp3d_dec *d, mp3d_stream_info *out) {
 static int pf_fused(mp3d_dec *d, uint32_t have, bool f32, bool lsf) {
     mp3d_batch *b = d->b;
     hipStream_t s = b->own;
-    HIPCHK(hipSetDevice(b->device));
+    int r = call_begin(b, s);
+    if (r) return r;
+    CallEnd done{b, s};
     const uint64_t off = 0;
     const uint32_t sz = MP3D_PF_BYTES;
-    int r = prepare_geometry(b, &off, &sz, 1, s); /* uploaded once, then cached */
+    r = prepare_geometry(b, &off, &sz, 1, s); /* uploaded once, then cached */
     if (r) return r;
-    b->last = s;
+    const mp3d_batch::Geo &g = b->geo[b->geo_i];
     const uint32_t seq = ++d->seq ? d->seq : ++d->seq; /* never 0, the word's initial value */
-    launch_frame(d->m_in, have, b->d_in_off, b->d_in_len, b->md, b->d_md_off, b->st, b->rec, b->sideu, d->m_info,
+    launch_frame(d->m_in, have, g.in_off(), g.in_len(), b->md, g.md_off(), b->st, b->rec, b->sideu, d->m_info,
                  b->opts, g_dev[b->device].tables, b->is_buf, b->meta, d->m_out, f32, lsf, d->m_done, seq, s);
     HIPCHK(hipGetLastError());
+    b->geo[b->geo_i].fresh = false; /* no event per call here: end_event covers it */
     for (uint32_t n = 1;; n++) {
         if (__atomic_load_n(d->h_done, __ATOMIC_ACQUIRE) == seq) return MP3D_OK;
         if ((n & 4095u) == 0) {
@@ -1084,7 +1219,11 @@ static int state_copy(mp3d_batch *b, int first, int n, void *dst, const void *sr
     if (!b || !(out ? dst : src) || first < 0 || n <= 0) return MP3D_E_ARG;
     if ((long long)first + n > b->max_streams) return MP3D_E_CAPACITY;
     HIPCHK(hipSetDevice(b->device));
-    hipStream_t s = b->last ? b->last : b->own;
+    hipStream_t s = b->own;
+    int r = own_after_last(b); /* after the handle's last call, on any stream */
+    if (r) return r;
+    r = flush_tail(b, s);
+    if (r) return r;
     StreamState *at = b->st + first;
     HIPCHK(hipMemcpyAsync(out ? dst : (void *)at, out ? (const void *)at : src, sizeof(StreamState) * (size_t)n,
                           hipMemcpyDefault, s));

@@ -70,3 +70,22 @@ def gather_to_root(t: torch.Tensor, root: int = 0, async_op: bool = False, out=N
     if out is not None:
         out = [o.view(t.dtype) for o in out]
     return (out, work) if async_op else out
+
+
+PCM_ROW_BYTES = 2304 * 2  # one int16 stereo frame
+
+
+def gather_plan(n_per_rank: int, frames: int, world: int, in_flight: int = 2, device_bytes: int = 288 << 30,
+                decoder_bytes: int = 0):
+    """Device memory rank 0 needs for the overlapped PCM gather (bench.py
+    --gather): `in_flight` receive lists of `world` PCM shards each (one list
+    per gather in flight, so two overlapped gathers never write the same
+    buffers), next to its own double-buffered PCM and the decoder's buffers.
+    Returns a dict with the byte counts and whether it fits; at C4 (65 536 x
+    32 per rank, 8 ranks) the receive lists are 2 x 8 x 9.66 GB."""
+    shard_bytes = n_per_rank * frames * PCM_ROW_BYTES
+    recv = in_flight * world * shard_bytes
+    own = 2 * shard_bytes
+    need = recv + own + decoder_bytes
+    return {"shard_bytes": shard_bytes, "recv_bytes": recv, "own_pcm_bytes": own, "decoder_bytes": decoder_bytes,
+            "need_bytes": need, "device_bytes": device_bytes, "fits": need <= device_bytes}

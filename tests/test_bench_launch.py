@@ -48,3 +48,26 @@ def test_bench_rank_failure_propagates():
     p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--plumbing", "--gpus", "2"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert p.returncode != 0 and "WORLD_SIZE" in p.stderr
+
+
+def test_bench_eight_ranks_gather_plan():
+    """C4's launch shape (8 ranks) through the launcher with the gather:
+    the line carries the rank count and backend the initialised process
+    group reports, per-rank setup times and generator threads (the host's
+    threads split over the ranks), and rank 0's receive-list plan, checked
+    at the FULL C4 shard size: one receive list per gather in flight, 2 x 8 x
+    9.66 GB, beside rank 0's own PCM and decoder buffers within 288 GB."""
+    r = _run("--gpus", "8", "--gather", "--dist-backend", "gloo")
+    assert r["n_gpus"] == 8 and r["ranks"] == 8 and r["dist_backend"] == "gloo"
+    assert len(r["per_rank_frames_per_s"]) == 8 and len(r["setup_s_per_rank"]) == 8
+    assert r["gen_threads_per_rank"] >= 1
+    plan = r["gather"]["rank0_memory_plan"]
+    shard_bytes = 65536 * 32 * 2304 * 2
+    assert plan["shard_bytes"] == shard_bytes and plan["recv_bytes"] == 2 * 8 * shard_bytes
+    assert plan["fits"] and plan["need_bytes"] <= 288 << 30
+    assert plan["decoder_bytes"] > 5e9  # the batch buffers are counted
+
+
+def test_gather_plan_rejects_oversize():
+    p = shard.gather_plan(65536 * 4, 32, 8)
+    assert not p["fits"]

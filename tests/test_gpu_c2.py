@@ -33,23 +33,27 @@ def _oracle_pcm(xr, bt, mx, s, frames):
     return ref
 
 
-def _run(xr, bt, mx, seg=None, calls=1):
-    """decode F frames per call, `calls` calls, device buffers; PCM [N, calls*F, 2304]"""
-    if seg is None:
-        os.environ.pop("MP3D_SEG_FRAMES", None)
-    else:
-        os.environ["MP3D_SEG_FRAMES"] = str(seg)
+def _run(xr, bt, mx, seg=None, calls=1, state=False):
+    """decode F frames per call, `calls` calls, device buffers; PCM [N, calls*F, 2304]
+    (and the final per-stream state blobs with state=True); seg: segment
+    length for every call, or a list with one per call"""
+    segs = seg if isinstance(seg, list) else [seg] * calls
     try:
         dec = mp3_amd.BatchDecoder(N, F)
         out = []
         for c in range(calls):
+            if segs[c] is None:
+                os.environ.pop("MP3D_SEG_FRAMES", None)
+            else:
+                os.environ["MP3D_SEG_FRAMES"] = str(segs[c])
             sl = slice(c * F, (c + 1) * F)
             d_xr, d_bt, d_mx = (torch.from_numpy(np.ascontiguousarray(a[:, sl])).cuda() for a in (xr, bt, mx))
             pcm = torch.zeros((N, F, 2304), dtype=torch.int16, device="cuda")
             dec.synth_only(d_xr, d_bt, d_mx, NCH, 44100, pcm=pcm)
             torch.cuda.synchronize()
             out.append(pcm.cpu().numpy())
-        return np.concatenate(out, axis=1)
+        pcm = np.concatenate(out, axis=1)
+        return (pcm, dec.get_state(0, N)) if state else pcm
     finally:
         os.environ.pop("MP3D_SEG_FRAMES", None)
 
@@ -74,6 +78,20 @@ def test_c2_segments_bit_identical_across_calls():
         ref = _oracle_pcm(xr, bt, mx, s, 2 * F)
         g = seq[s, :, :1152 * NCH].reshape(2 * F, 1152, NCH)
         assert np.abs(g.astype(np.int32) - ref.astype(np.int32)).max() <= 1, s
+
+
+def test_c2_state_tails_across_calls():
+    """Segmented synth-only calls leave each stream's overlap + FIFO in a
+    packed tail that the next segmented call reads (two tails in turn, no
+    state copy per call); a one-segment call or a state read first copies
+    the live tail back into the stream state.  Every mix of the two must be
+    bit-identical to the one-wave-per-stream decode, PCM and final state."""
+    xr, bt, mx = _gen.c2_spectra(N, 3 * F, NCH, seed=777)
+    ref_pcm, ref_st = _run(xr, bt, mx, seg=F, calls=3, state=True)
+    for sched in ([None, None, None], [None, None, F], [F, None, None], [None, F, 7]):
+        pcm, st = _run(xr, bt, mx, seg=sched, calls=3, state=True)
+        assert np.array_equal(pcm, ref_pcm), sched
+        assert np.array_equal(st, ref_st), sched
 
 
 def test_clipping_saturates_like_the_oracle():
