@@ -24,7 +24,7 @@ def main():
     reps = [
         ("namespace mp3d {\n", "namespace mp3d {\n__device__ unsigned long long g_ptime[8];\n"),
         ("    for (int f = fw; f < f1; f++) {\n",
-         "    unsigned long long pt_[5] = {0, 0, 0, 0, 0}, tl_ = __builtin_amdgcn_s_memtime();\n"
+         "    unsigned long long pt_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tl_ = __builtin_amdgcn_s_memtime();\n"
          "    for (int f = fw; f < f1; f++) {\n"),
         (Q, "            unsigned long long tq_ = __builtin_amdgcn_s_memtime(); pt_[4] += tq_ - tl_;\n" + Q),
         (I, "            unsigned long long ti_ = __builtin_amdgcn_s_memtime(); pt_[0] += ti_ - tq_;\n" + I),
@@ -32,7 +32,17 @@ def main():
         (W, "            unsigned long long tw_ = __builtin_amdgcn_s_memtime(); pt_[2] += tw_ - tm_;\n" + W),
         (E, E + "\n            tl_ = __builtin_amdgcn_s_memtime(); pt_[3] += tl_ - tw_;"),
         (S, "    if ((threadIdx.x & 63) == 0 && !SRC_XR && PF == 0)\n"
-            "        for (int k = 0; k < 5; k++) atomicAdd(&g_ptime[k], pt_[k]);\n" + S),
+            "        for (int k = 0; k < 8; k++) atomicAdd(&g_ptime[k], pt_[k]);\n" + S),
+        # phase Q sub-marks (decode path): after the band scales, after the
+        # requantise loop, after escapes + stereo (the rest of Q = scatter)
+        ("                (void)m12a;\n",
+         "                (void)m12a;\n                unsigned long long tq1_ = __builtin_amdgcn_s_memtime(); pt_[5] += tq1_ - tq_;\n"),
+        ("                if (__ballot((bigacc & 0xF800F800u) != 0u)) {\n",
+         "                unsigned long long tq2_ = __builtin_amdgcn_s_memtime(); pt_[6] += tq2_ - tq1_;\n"
+         "                if (__ballot((bigacc & 0xF800F800u) != 0u)) {\n"),
+        ("                /* the next granule's loads fly during phases I, M, W (issued\n",
+         "                pt_[7] += __builtin_amdgcn_s_memtime() - tq2_;\n"
+         "                /* the next granule's loads fly during phases I, M, W (issued\n"),
     ]
     for a, b in reps:
         assert src.count(a) == 1, a

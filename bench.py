@@ -377,7 +377,12 @@ def run_per_frame(args):
             "config": {"workload": "C1: one 128 kbps 44.1 kHz joint-stereo stream (21 audio frames + Info frame) "
                                    "through mp3d_decode_frame, host buffers, one call per frame",
                        "streams_per_gpu": 1, "parallelism": "none (per-frame player call)"},
-            "latency_us": {"median": float(np.median(lat_us)), "p99": float(np.percentile(lat_us, 99))},
+            "latency_us": {"median": float(np.median(lat_us)), "p90": float(np.percentile(lat_us, 90)),
+                           "p99": float(np.percentile(lat_us, 99)), "mean": float(lat_us.mean())},
+            "readahead_frames": int(os.environ.get("MP3D_PF_READAHEAD", 16)),
+            "note": "one call per frame as a player's loop makes them, the rest of the file passed each time: the "
+                    "decoder reads up to readahead_frames frames ahead in one batch call and serves the next calls "
+                    "from it (MP3D_PF_READAHEAD=0: every call decodes its own frame)",
             "roofline": None, "cpu_baseline": cpu}
 
 

@@ -31,7 +31,7 @@ void launch_demux(const uint8_t *, const uint64_t *, const uint32_t *, uint8_t *
 void launch_huffman(const uint8_t *, const uint64_t *, const FrameRec *, const uint64_t *, const DevTables *, int16_t *,
                     UnitMeta *, int, int, int, bool, hipStream_t);
 void launch_synth(const FrameRec *, const int16_t *, const UnitMeta *, const DevTables *, StreamState *, void *, bool, int,
-                  int, int, hipStream_t);
+                  int, int, int, float *, const float *, hipStream_t);
 void launch_synth_xr(const float *, const uint8_t *, const uint8_t *, const DevTables *, StreamState *, int16_t *, int,
                      int, int, int, int, float *, const float *, hipStream_t);
 void launch_gather_frames(const void *, void *, const void *, void *, const int *, int, int, int, int, int,
@@ -374,14 +374,82 @@ static hipEvent_t end_event(mp3d_batch *b) {
     return b->ev_done;
 }
 
+static int grow(void **p, size_t *cap, size_t need) {
+    if (need <= *cap) return MP3D_OK;
+    if (*p) HIPCHK(hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    HIPCHK(hipMalloc(p, need));
+    *cap = need;
+    return MP3D_OK;
+}
+
+/* Frames per k_synth segment for n streams x F frames: few streams leave
+ * the chip idle (one wave walks one stream), so each stream is split into
+ * frame-parallel segments (one wave each, warm-up frames before; k_synth)
+ * until ~2 rounds of resident waves (3 per SIMD) are in the grid, keeping
+ * segments >= min_len frames.  MP3D_SEG_FRAMES overrides (0 = never split). */
+static int seg_frames(int n, int F, int n_cu, int min_len) {
+    int seg_len = F;
+    const long long want = 2LL * 3 * 4 * n_cu;
+    if ((long long)n < want && F >= 2 * min_len) {
+        const int nseg = (int)std::min<long long>((want + n - 1) / n, F / min_len);
+        seg_len = (F + nseg - 1) / nseg;
+    }
+    const char *e = getenv("MP3D_SEG_FRAMES");
+    if (e && atoi(e) > 0) seg_len = std::min(F, atoi(e));
+    if (e && atoi(e) == 0 && e[0] == '0') seg_len = F;
+    return seg_len;
+}
+
+/* where k_synth takes each stream's overlap + fifo from and puts them:
+ * in = the live tail when it holds these n streams (else StreamState, after
+ * copying back a tail of another shape); out = the other tail when the
+ * call is segmented (the first segment may still be reading the state),
+ * else StreamState.  tail_commit() after the launch. */
+struct TailPlan {
+    const float *in = nullptr;
+    float *out = nullptr;
+    int t_out = 0;
+};
+static int tail_plan(mp3d_batch *b, int n, int F, int seg_len, hipStream_t s, TailPlan *tp);
+static void tail_commit(mp3d_batch *b, int n, int F, int seg_len, const TailPlan &tp) {
+    if (seg_len < F) {
+        b->tail_live = tp.t_out;
+        b->tail_n = n;
+    }
+}
+
 static constexpr size_t STATE_TAIL = sizeof(((StreamState *)0)->overlap) + sizeof(((StreamState *)0)->fifo);
 
-/* the live synth-only tail back into StreamState (on stream s) */
+/* the live tail back into StreamState (on stream s) */
 static int flush_tail(mp3d_batch *b, hipStream_t s) {
     if (b->tail_live < 0) return MP3D_OK;
     HIPCHK(hipMemcpy2DAsync(&b->st[0].overlap[0][0][0], sizeof(StreamState), b->st_tail[b->tail_live], STATE_TAIL,
                             STATE_TAIL, b->tail_n, hipMemcpyDeviceToDevice, s));
     b->tail_live = -1;
+    return MP3D_OK;
+}
+
+static int tail_plan(mp3d_batch *b, int n, int F, int seg_len, hipStream_t s, TailPlan *tp) {
+    if (b->tail_live >= 0 && (seg_len >= F || b->tail_n != n)) {
+        int r = flush_tail(b, s);
+        if (r) return r;
+    }
+    tp->in = b->tail_live >= 0 ? b->st_tail[b->tail_live] : nullptr;
+    tp->t_out = b->tail_live >= 0 ? b->tail_live ^ 1 : 0;
+    tp->out = nullptr;
+    if (seg_len < F) {
+        const size_t need = STATE_TAIL * (size_t)n;
+        const bool fresh = need > b->tail_cap[tp->t_out];
+        int r = grow((void **)&b->st_tail[tp->t_out], &b->tail_cap[tp->t_out], need);
+        if (r) return r;
+        /* k_synth writes the fifo slots the synthesis reads back (slot 0 only
+         * at the columns some lane's window needs): zero the rest once, as
+         * StreamState is, so a flushed tail leaves the same state bytes */
+        if (fresh) HIPCHK(hipMemsetAsync(b->st_tail[tp->t_out], 0, b->tail_cap[tp->t_out], s));
+        tp->out = b->st_tail[tp->t_out];
+    }
     return MP3D_OK;
 }
 
@@ -408,25 +476,25 @@ struct CallEnd {
     }
 };
 
-static bool is_device_ptr(const void *p) {
-    if (!p) return false;
+/* Where a caller's buffer lives, seen from the handle's device: its own
+ * device memory (or managed memory) is read and written in place by the
+ * kernels; host memory and another GPU's memory are staged through the
+ * handle's buffers with hipMemcpyDefault copies (no peer access assumed). */
+enum PtrKind { PTR_HOST, PTR_DEV, PTR_OTHER_DEV };
+static PtrKind ptr_kind(const void *p, int device) {
+    if (!p) return PTR_HOST;
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();
-        return false;
+        return PTR_HOST;
     }
-    return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+    if (a.type == hipMemoryTypeManaged) return PTR_DEV;
+    if (a.type != hipMemoryTypeDevice) return PTR_HOST;
+    return a.device == device ? PTR_DEV : PTR_OTHER_DEV;
 }
+/* memory the handle's kernels may read / write in place */
+static bool is_device_ptr(const void *p, int device) { return ptr_kind(p, device) == PTR_DEV; }
 
-static int grow(void **p, size_t *cap, size_t need) {
-    if (need <= *cap) return MP3D_OK;
-    if (*p) HIPCHK(hipFree(*p));
-    *p = nullptr;
-    *cap = 0;
-    HIPCHK(hipMalloc(p, need));
-    *cap = need;
-    return MP3D_OK;
-}
 
 extern "C" int mp3d_batch_create(int device, int max_streams, int max_frames, mp3d_batch **out) {
     if (!out || max_streams <= 0 || max_frames <= 0) return MP3D_E_ARG;
@@ -616,17 +684,15 @@ static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offse
                      mp3d_frame_info *dev_infos = nullptr) {
     if (!b || !frames || !offsets || !sizes || n <= 0 || F <= 0) return MP3D_E_ARG;
     if (n > b->max_streams || F > b->max_frames) return MP3D_E_CAPACITY;
-    int r = call_begin(b, s);
-    if (r) return r;
-    r = flush_tail(b, s);
+    int r = call_begin(b, s); /* (the demux and Huffman stages never touch a live tail's overlap / fifo) */
     if (r) return r;
     uint64_t total = 0;
     for (int i = 0; i < n; i++) total = std::max<uint64_t>(total, offsets[i] + sizes[i]);
     const uint8_t *din = frames;
-    if (!mapped && !is_device_ptr(frames)) {
+    if (!mapped && !is_device_ptr(frames, b->device)) {
         r = grow((void **)&b->d_in, &b->in_cap, total + 64);
         if (r) return r;
-        HIPCHK(hipMemcpyAsync(b->d_in, frames, total, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(b->d_in, frames, total, hipMemcpyDefault, s));
         din = b->d_in;
         *sync_needed = true;
     }
@@ -657,7 +723,7 @@ static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offse
  * call ends with one stream sync */
 static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets, const uint32_t *sizes, int n,
                         int F, void *pcm, bool f32, mp3d_frame_info *infos, void *hip_stream, bool overwrite,
-                        int kinds = 3, bool mapped = false) {
+                        int kinds = 3, bool mapped = false, int seg_len_req = 0) {
     if (!b || !pcm) return MP3D_E_ARG;
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : b->own;
     CallEnd done{b, s};
@@ -665,23 +731,34 @@ static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *of
     /* frame infos: written in place when the caller's array is device memory
      * (or the per-frame decoder's mapped buffer), else into d_infos and
      * copied to the host after the call */
-    const bool inf_host = infos && !mapped && !is_device_ptr(infos);
+    const bool inf_host = infos && !mapped && !is_device_ptr(infos, b->device); /* or another GPU's */
     mp3d_frame_info *dinf = infos && !inf_host ? infos : b->d_infos;
     int r = run_front(b, frames, offsets, sizes, n, F, s, &sync_needed, mapped, dinf);
     if (r) return r;
     const size_t PB = f32 ? sizeof(float) : sizeof(int16_t), row = 2304 * PB;
     const size_t pcm_bytes = (size_t)n * F * row;
     void *dpcm = pcm;
-    bool pcm_host = !mapped && !is_device_ptr(pcm);
-    if (pcm_host) {
+    const PtrKind pk = mapped ? PTR_DEV : ptr_kind(pcm, b->device);
+    bool pcm_host = pk == PTR_HOST;
+    if (pk != PTR_DEV) {
         r = grow((void **)&b->d_pcm, &b->pcm_cap, pcm_bytes);
         if (r) return r;
         dpcm = b->d_pcm;
+        /* another GPU's buffer: its rows the kernel does not write keep their
+         * bytes, as in place (copied over, decoded into, copied back) */
+        if (pk == PTR_OTHER_DEV) HIPCHK(hipMemcpyAsync(dpcm, pcm, pcm_bytes, hipMemcpyDefault, s));
     }
     DeviceCtx &dc = g_dev[b->device];
-    launch_synth(b->rec, b->is_buf, b->meta, dc.tables, b->st, dpcm, f32, n, F, kinds, s);
+    /* few streams: frame-parallel segments per stream (>= 4 frames each,
+     * or the caller's seg_len) */
+    const int seg_len = seg_len_req > 0 ? std::min(F, seg_len_req) : seg_frames(n, F, dc.n_cu, 4);
+    TailPlan tp;
+    r = tail_plan(b, n, F, seg_len, s, &tp);
+    if (r) return r;
+    launch_synth(b->rec, b->is_buf, b->meta, dc.tables, b->st, dpcm, f32, n, F, kinds, seg_len, tp.out, tp.in, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[3], s));
     HIPCHK(hipGetLastError());
+    tail_commit(b, n, F, seg_len, tp);
     const size_t ib = sizeof(mp3d_frame_info) * (size_t)n * F;
     if (pcm_host && !overwrite) {
         /* A host sink is read back whole, but each row keeps the caller's
@@ -715,13 +792,13 @@ static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *of
         }
         return MP3D_OK;
     }
-    if (pcm_host) { /* internal callers that read only the rows with audio */
-        HIPCHK(hipMemcpyAsync(pcm, dpcm, pcm_bytes, hipMemcpyDeviceToHost, s));
-        sync_needed = true;
+    if (pk != PTR_DEV) { /* another GPU's buffer, or internal callers that read only the rows with audio */
+        HIPCHK(hipMemcpyAsync(pcm, dpcm, pcm_bytes, hipMemcpyDefault, s));
+        sync_needed = pcm_host;
     }
     if (inf_host) {
-        HIPCHK(hipMemcpyAsync(infos, b->d_infos, ib, hipMemcpyDeviceToHost, s));
-        sync_needed = true;
+        HIPCHK(hipMemcpyAsync(infos, b->d_infos, ib, hipMemcpyDefault, s));
+        sync_needed = sync_needed || ptr_kind(infos, b->device) == PTR_HOST;
     }
     if (sync_needed) HIPCHK(hipStreamSynchronize(s));
     return MP3D_OK;
@@ -756,15 +833,12 @@ extern "C" int mp3d_batch_huffman_only(mp3d_batch *b, const uint8_t *frames, con
     int r = run_front(b, frames, offsets, sizes, n, F, s, &sync_needed);
     if (r) return r;
     if (is_out) {
-        hipMemcpyKind k = is_device_ptr(is_out) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-        HIPCHK(hipMemcpyAsync(is_out, b->is_buf, units * 576 * sizeof(int16_t), k, s));
-        sync_needed |= k == hipMemcpyDeviceToHost;
+        HIPCHK(hipMemcpyAsync(is_out, b->is_buf, units * 576 * sizeof(int16_t), hipMemcpyDefault, s));
+        sync_needed |= ptr_kind(is_out, b->device) == PTR_HOST;
     }
     if (sf_out) {
-        bool dev = is_device_ptr(sf_out);
-        HIPCHK(hipMemcpy2DAsync(sf_out, 40, b->meta, sizeof(UnitMeta), 40, units,
-                                dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
-        sync_needed |= !dev;
+        HIPCHK(hipMemcpy2DAsync(sf_out, 40, b->meta, sizeof(UnitMeta), 40, units, hipMemcpyDefault, s));
+        sync_needed |= ptr_kind(sf_out, b->device) == PTR_HOST;
     }
     if (sync_needed) HIPCHK(hipStreamSynchronize(s));
     return MP3D_OK;
@@ -786,7 +860,7 @@ extern "C" int mp3d_batch_synth_only(mp3d_batch *b, const float *xr, const uint8
     size_t nx = (size_t)n * F * 2 * nch;
     const float *dxr = xr;
     const uint8_t *dbt = block_type, *dmx = mixed;
-    if (!is_device_ptr(xr) || !is_device_ptr(block_type) || !is_device_ptr(mixed)) {
+    if (!is_device_ptr(xr, b->device) || !is_device_ptr(block_type, b->device) || !is_device_ptr(mixed, b->device)) {
         size_t need = nx * 576 * sizeof(float) + 2 * nx + 64;
         int r = grow((void **)&b->d_xr, &b->xr_cap, need);
         if (r) return r;
@@ -801,56 +875,34 @@ extern "C" int mp3d_batch_synth_only(mp3d_batch *b, const float *xr, const uint8
     }
     size_t pcm_bytes = (size_t)n * F * 2304 * sizeof(int16_t);
     int16_t *dpcm = pcm;
-    bool pcm_host = !is_device_ptr(pcm);
+    const PtrKind pk = ptr_kind(pcm, b->device);
+    const bool pcm_host = pk != PTR_DEV; /* host, or another GPU's (staged like host) */
     if (pcm_host) {
         int r = grow((void **)&b->d_pcm, &b->pcm_cap, pcm_bytes);
         if (r) return r;
         dpcm = b->d_pcm;
+        /* mono rows are half written: the rest keeps the caller's bytes */
+        if (pk == PTR_OTHER_DEV || nch == 1) HIPCHK(hipMemcpyAsync(dpcm, pcm, pcm_bytes, hipMemcpyDefault, s));
     }
     DeviceCtx &dc = g_dev[b->device];
     if (b->timing) {
         for (int i = 0; i < 3; i++) HIPCHK(hipEventRecord(b->ev[i], s));
     }
-    /* Few streams leave the chip idle (one wave walks one stream): split
-     * each stream into frame-parallel segments (k_synth, one warm-up frame
-     * each) until ~2 rounds of resident waves (3 per SIMD) are in the grid,
-     * keeping segments >= 4 frames (warm-up overhead <= 25 %).
-     * MP3D_SEG_FRAMES overrides the segment length. */
-    int seg_len = F;
+    /* few streams: frame-parallel segments (seg_frames; one warm-up frame
+     * each, so >= 4 frames per segment: warm-up overhead <= 25 %) */
+    const int seg_len = seg_frames(n, F, dc.n_cu, 4);
+    TailPlan tp;
     {
-        const long long want = 2LL * 3 * 4 * dc.n_cu;
-        if ((long long)n < want && F >= 8) {
-            const int nseg = (int)std::min<long long>((want + n - 1) / n, F / 4);
-            seg_len = (F + nseg - 1) / nseg;
-        }
-        const char *e = getenv("MP3D_SEG_FRAMES");
-        if (e && atoi(e) > 0) seg_len = std::min(F, atoi(e));
-    }
-    /* state in: the live tail when it holds these n streams, else
-     * StreamState (after copying back a tail of another shape); state out:
-     * the other tail (segments), or StreamState (one segment per stream) */
-    if (b->tail_live >= 0 && (seg_len >= F || b->tail_n != n)) {
-        int r = flush_tail(b, s);
+        int r = tail_plan(b, n, F, seg_len, s, &tp);
         if (r) return r;
     }
-    const float *tail_in = b->tail_live >= 0 ? b->st_tail[b->tail_live] : nullptr;
-    float *tail_out = nullptr;
-    const int t_out = b->tail_live >= 0 ? b->tail_live ^ 1 : 0;
-    if (seg_len < F) {
-        int r = grow((void **)&b->st_tail[t_out], &b->tail_cap[t_out], STATE_TAIL * (size_t)n);
-        if (r) return r;
-        tail_out = b->st_tail[t_out];
-    }
-    launch_synth_xr(dxr, dbt, dmx, dc.tables, b->st, dpcm, n, F, nch, sr, seg_len, tail_out, tail_in, s);
+    launch_synth_xr(dxr, dbt, dmx, dc.tables, b->st, dpcm, n, F, nch, sr, seg_len, tp.out, tp.in, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[3], s));
     HIPCHK(hipGetLastError());
-    if (seg_len < F) {
-        b->tail_live = t_out;
-        b->tail_n = n;
-    }
+    tail_commit(b, n, F, seg_len, tp);
     if (pcm_host) {
-        HIPCHK(hipMemcpyAsync(pcm, dpcm, pcm_bytes, hipMemcpyDeviceToHost, s));
-        sync_needed = true;
+        HIPCHK(hipMemcpyAsync(pcm, dpcm, pcm_bytes, hipMemcpyDefault, s));
+        sync_needed = sync_needed || pk == PTR_HOST;
     }
     if (sync_needed) HIPCHK(hipStreamSynchronize(s));
     return MP3D_OK;
@@ -906,7 +958,7 @@ extern "C" int mp3d_long_plan(const uint8_t *data, size_t bytes, int L, long lon
 
 static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets, const uint32_t *sizes, int n,
                         int F, void *pcm, bool f32, mp3d_frame_info *infos, void *hip_stream, bool overwrite,
-                        int kinds, bool mapped);
+                        int kinds, bool mapped, int seg_len_req);
 
 extern "C" int mp3d_batch_decode_long(mp3d_batch *b, const uint8_t *data, size_t bytes, int L, void *pcm, int f32,
                                       long long max_frames, mp3d_frame_info *infos, long long *n_frames,
@@ -914,12 +966,12 @@ extern "C" int mp3d_batch_decode_long(mp3d_batch *b, const uint8_t *data, size_t
     if (!b || !data || !pcm || L <= 0 || max_frames <= 0 || !n_frames) return MP3D_E_ARG;
     *n_frames = 0;
     HIPCHK(hipSetDevice(b->device));
-    const bool dev_in = is_device_ptr(data);
+    const bool dev_in = ptr_kind(data, b->device) != PTR_HOST; /* any GPU's: the walk needs a host copy */
     std::vector<uint8_t> host_copy;
     const uint8_t *hp = data;
     if (dev_in) { /* the frame walk runs on the host */
         host_copy.resize(bytes);
-        HIPCHK(hipMemcpy(host_copy.data(), data, bytes, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(host_copy.data(), data, bytes, hipMemcpyDefault));
         hp = host_copy.data();
     }
     std::vector<uint64_t> off;
@@ -943,14 +995,14 @@ extern "C" int mp3d_batch_decode_long(mp3d_batch *b, const uint8_t *data, size_t
         if (r) return r;
     }
     const uint8_t *din = data;
-    if (!dev_in) {
+    if (!is_device_ptr(data, b->device)) { /* host or another GPU's: staged */
         int r = grow((void **)&b->d_in, &b->in_cap, bytes + 64);
         if (r) return r;
-        HIPCHK(hipMemcpyAsync(b->d_in, data, bytes, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(b->d_in, data, bytes, hipMemcpyDefault, s));
         din = b->d_in;
     }
     const size_t row = 2304 * (f32 ? sizeof(float) : sizeof(int16_t));
-    const bool pcm_dev = is_device_ptr(pcm), inf_dev = infos && is_device_ptr(infos);
+    const bool pcm_dev = is_device_ptr(pcm, b->device), inf_dev = infos && is_device_ptr(infos, b->device);
     const int chunk = b->max_streams;
     void *seg_pcm = nullptr, *out_pcm = nullptr;
     int *d_a = nullptr;
@@ -992,6 +1044,7 @@ extern "C" int mp3d_batch_decode_long(mp3d_batch *b, const uint8_t *data, size_t
         }
         /* fresh decoder state for every virtual stream */
         LCHK(hipMemsetAsync(b->st, 0, sizeof(StreamState) * ns, s));
+        b->tail_live = -1; /* fresh states: no tail of the previous chunk */
         rc = batch_decode(b, din, so.data(), ss.data(), ns, F, seg_pcm, f32 != 0, nullptr, s, false);
         if (rc) goto done;
         if (k0 == 0 && sinfo) rc = mp3d_batch_stream_info(b, 1, sinfo);
@@ -1001,13 +1054,14 @@ extern "C" int mp3d_batch_decode_long(mp3d_batch *b, const uint8_t *data, size_t
                              d_a + k0, L, F, (int)k0, (int)(j1 - j0), (int)row, s);
         LCHK(hipGetLastError());
     }
-    if (!pcm_dev) LCHK(hipMemcpyAsync(pcm, out_pcm, (size_t)N * row, hipMemcpyDeviceToHost, s));
-    if (infos && !inf_dev) LCHK(hipMemcpyAsync(infos, out_inf, sizeof(mp3d_frame_info) * (size_t)N, hipMemcpyDeviceToHost, s));
+    if (!pcm_dev) LCHK(hipMemcpyAsync(pcm, out_pcm, (size_t)N * row, hipMemcpyDefault, s));
+    if (infos && !inf_dev) LCHK(hipMemcpyAsync(infos, out_inf, sizeof(mp3d_frame_info) * (size_t)N, hipMemcpyDefault, s));
     LCHK(hipStreamSynchronize(s));
 done:
 #undef LCHK
     (void)hipStreamSynchronize(s);
     b->st = own_st;
+    b->tail_live = -1; /* a tail left by the segments belongs to the scratch states */
     if (seg_st) (void)hipFree(seg_st);
     if (seg_pcm) (void)hipFree(seg_pcm);
     if (d_a) (void)hipFree(d_a);
@@ -1024,6 +1078,8 @@ done:
  * zero-padded to a fixed MP3D_PF_BYTES, which keeps the batch geometry
  * constant (uploaded once) across calls. */
 #define MP3D_PF_BYTES 4096
+#define MP3D_PF_READAHEAD 16 /* frames per read-ahead by default */
+#define MP3D_PF_RA_SEG 2     /* synthesis segment (frames) of a read-ahead */
 struct mp3d_dec {
     mp3d_batch *b = nullptr;
     long frames = 0;
@@ -1041,6 +1097,29 @@ struct mp3d_dec {
     uint32_t *h_done = nullptr, *m_done = nullptr;
     uint32_t seq = 0;
     bool fused = false;
+    /* Read-ahead: the player hands over the rest of its
+     * buffer, so one call decodes up to ra_max of the frames found there in
+     * ONE batch call (n = 1, F = ra_max, frame-parallel synthesis segments)
+     * into mapped buffers, and the next calls are served from them after
+     * checking that the caller's bytes at the located frame are the same.
+     * Any other input (a seek, a new buffer, other options or sink) settles
+     * first: the state saved before the read-ahead is restored and the
+     * frames already served are decoded again (exact), then the call runs
+     * normally.  MP3D_PF_READAHEAD = frames per read-ahead (0 / 1: off). */
+    int ra_max = 0;
+    uint8_t *ra_in = nullptr, *ra_in_m = nullptr;          /* frames back to back (pinned, mapped) */
+    void *ra_pcm = nullptr, *ra_pcm_m = nullptr;           /* [ra_max][2304] f32-sized slots       */
+    mp3d_frame_info *ra_inf = nullptr, *ra_inf_m = nullptr;
+    StreamState *snap = nullptr;                           /* device: the state before the read-ahead */
+    struct RaEnt {
+        uint32_t off, len; /* the frame's bytes in ra_in */
+        size_t pos;        /* bytes skipped before it in its call's buffer */
+    };
+    std::vector<RaEnt> ra;
+    size_t ra_next = 0;
+    bool ra_f32 = false;
+    long ra_frames0 = 0; /* frames / kind before the read-ahead */
+    int ra_kind0 = 0;
 };
 
 static void dec_free(mp3d_dec *d) {
@@ -1049,6 +1128,10 @@ static void dec_free(mp3d_dec *d) {
     if (d->h_out) (void)hipHostFree(d->h_out);
     if (d->h_info) (void)hipHostFree(d->h_info);
     if (d->h_done) (void)hipHostFree(d->h_done);
+    if (d->ra_in) (void)hipHostFree(d->ra_in);
+    if (d->ra_pcm) (void)hipHostFree(d->ra_pcm);
+    if (d->ra_inf) (void)hipHostFree(d->ra_inf);
+    if (d->snap) (void)hipFree(d->snap);
     delete d;
 }
 
@@ -1057,7 +1140,12 @@ extern "C" int mp3d_dec_create_on(int device, mp3d_dec **out) {
     *out = nullptr;
     mp3d_dec *d = new (std::nothrow) mp3d_dec;
     if (!d) return MP3D_E_NOMEM;
-    int r = mp3d_batch_create(device, 1, 1, &d->b);
+    {
+        const char *e = getenv("MP3D_PF_READAHEAD");
+        d->ra_max = e ? std::max(0, std::min(64, atoi(e))) : MP3D_PF_READAHEAD;
+        if (d->ra_max < 2) d->ra_max = 0;
+    }
+    int r = mp3d_batch_create(device, 1, std::max(1, d->ra_max), &d->b);
     if (r) {
         dec_free(d);
         return r;
@@ -1088,6 +1176,21 @@ extern "C" int mp3d_dec_create_on(int device, mp3d_dec **out) {
         d->m_info = nullptr;
         d->m_done = nullptr;
     }
+    if (d->ra_max && d->m_in) {
+        const size_t K = (size_t)d->ra_max;
+        if (hipHostMalloc((void **)&d->ra_in, K * MP3D_MAX_FRAME_BYTES + 64, hipHostMallocMapped) != hipSuccess ||
+            hipHostMalloc(&d->ra_pcm, K * 2304 * sizeof(float), co) != hipSuccess ||
+            hipHostMalloc((void **)&d->ra_inf, K * sizeof(mp3d_frame_info), co) != hipSuccess ||
+            hipMalloc((void **)&d->snap, sizeof(StreamState)) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&d->ra_in_m, d->ra_in, 0) != hipSuccess ||
+            hipHostGetDevicePointer(&d->ra_pcm_m, d->ra_pcm, 0) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&d->ra_inf_m, d->ra_inf, 0) != hipSuccess) {
+            dec_free(d);
+            return MP3D_E_NOMEM;
+        }
+    } else {
+        d->ra_max = 0;
+    }
     *out = d;
     return MP3D_OK;
 }
@@ -1103,8 +1206,12 @@ extern "C" void mp3d_dec_destroy(mp3d_dec *d) {
     dec_free(d);
 }
 
+static int ra_settle(mp3d_dec *d);
+
 extern "C" void mp3d_dec_reset(mp3d_dec *d) {
     if (!d) return;
+    d->ra.clear(); /* the state is zeroed whole */
+    d->ra_next = 0;
     (void)mp3d_batch_reset(d->b);
     d->frames = 0;
     d->kind = 0;
@@ -1112,6 +1219,8 @@ extern "C" void mp3d_dec_reset(mp3d_dec *d) {
 
 extern "C" int mp3d_dec_set_options(mp3d_dec *d, int flags) {
     if (!d) return MP3D_E_ARG;
+    const int r = ra_settle(d); /* frames read ahead under the old options */
+    if (r) return r;
     return mp3d_batch_set_options(d->b, flags);
 }
 
@@ -1122,8 +1231,11 @@ extern "C" int mp3d_dec_stream_info(mp3d_dec *d, mp3d_stream_info *out) {
 
 /* One frame through k_frame (one launch), then a poll of the mapped
  * completion word instead of a stream sync (~5 us less per
- * call).  The frame is in d->h_in[0, have).  A kernel that never completes
- * is caught by a stream query every few thousand polls. */
+ * call).  The frame is in d->h_in[0, have).  Every few thousand polls a
+ * stream query catches a kernel that faulted or aborted; a kernel that
+ * never completes keeps the stream busy, so after ~1 ms of polling the host
+ * stops spinning and blocks in hipStreamSynchronize (a hung kernel then
+ * costs a blocked thread, not a spinning core). */
 static int pf_fused(mp3d_dec *d, uint32_t have, bool f32, bool lsf) {
     mp3d_batch *b = d->b;
     hipStream_t s = b->own;
@@ -1133,6 +1245,7 @@ static int pf_fused(mp3d_dec *d, uint32_t have, bool f32, bool lsf) {
     const uint64_t off = 0;
     const uint32_t sz = MP3D_PF_BYTES;
     r = prepare_geometry(b, &off, &sz, 1, s); /* uploaded once, then cached */
+    if (!r) r = flush_tail(b, s); /* k_frame reads the state from StreamState */
     if (r) return r;
     const mp3d_batch::Geo &g = b->geo[b->geo_i];
     const uint32_t seq = ++d->seq ? d->seq : ++d->seq; /* never 0, the word's initial value */
@@ -1143,7 +1256,7 @@ static int pf_fused(mp3d_dec *d, uint32_t have, bool f32, bool lsf) {
     for (uint32_t n = 1;; n++) {
         if (__atomic_load_n(d->h_done, __ATOMIC_ACQUIRE) == seq) return MP3D_OK;
         if ((n & 4095u) == 0) {
-            const hipError_t e = hipStreamQuery(s);
+            const hipError_t e = n >= (64u << 12) ? hipStreamSynchronize(s) : hipStreamQuery(s);
             if (e == hipErrorNotReady) continue;
             HIPCHK(e);
             /* the stream is idle: the word must be there now */
@@ -1151,6 +1264,83 @@ static int pf_fused(mp3d_dec *d, uint32_t have, bool f32, bool lsf) {
             return MP3D_E_HIP;
         }
     }
+}
+
+/* Settle a read-ahead: the frames decoded ahead but not served are
+ * dropped, and the device state is put back to "after the frames served":
+ * the state saved before the read-ahead, then those frames decoded again
+ * (the same bytes, so the same state).  A no-op without a read-ahead. */
+static int ra_settle(mp3d_dec *d) {
+    if (d->ra.empty()) return MP3D_OK;
+    const size_t served = d->ra_next;
+    const bool all = served == d->ra.size();
+    d->ra_next = 0;
+    if (all) { /* every frame was served: the state is where the caller is */
+        d->ra.clear();
+        return MP3D_OK;
+    }
+    mp3d_batch *b = d->b;
+    HIPCHK(hipSetDevice(b->device));
+    int r = own_after_last(b);
+    if (r) return r;
+    b->tail_live = -1; /* the tail holds the state after the whole read-ahead */
+    HIPCHK(hipMemcpyAsync(b->st, d->snap, sizeof(StreamState), hipMemcpyDeviceToDevice, b->own));
+    if (served) {
+        const uint64_t off = 0;
+        const uint32_t len = d->ra[served - 1].off + d->ra[served - 1].len;
+        r = batch_decode(b, d->ra_in_m, &off, &len, 1, (int)served, d->ra_pcm_m, d->ra_f32, d->ra_inf_m, nullptr, true,
+                         3, true, MP3D_PF_RA_SEG);
+        if (r) return r;
+    } else {
+        HIPCHK(hipStreamSynchronize(b->own));
+    }
+    d->ra.clear();
+    return MP3D_OK;
+}
+
+/* Read ahead from the call's buffer: the complete frames found there (up to
+ * ra_max, located exactly as consecutive calls would locate them) are
+ * decoded in one batch call; returns 1 when the first of them is to be
+ * served, 0 when there are too few frames (the single-frame path then). */
+static int ra_fill(mp3d_dec *d, const uint8_t *buf, size_t bytes, bool f32) {
+    if (!d->ra_max) return 0;
+    size_t cur = 0;
+    uint32_t o = 0;
+    int kind = d->kind, kinds = 0;
+    std::vector<mp3d_dec::RaEnt> ents;
+    for (int j = 0; j < d->ra_max; j++) {
+        size_t pos = 0, have = 0;
+        int fb = -1;
+        if (pf_locate(buf + cur, bytes - cur, kind, d->frames == 0 && j == 0, false, &pos, &fb, &have) <= 0 ||
+            have < (size_t)fb)
+            break;
+        memcpy(d->ra_in + o, buf + cur + pos, (size_t)fb);
+        ents.push_back({o, (uint32_t)fb, pos});
+        const int k = host_frame_kind(buf + cur + pos);
+        if (!kind) kind = k; /* checked again when each is served */
+        kinds |= k;
+        o += (uint32_t)fb;
+        cur += pos + (size_t)fb;
+    }
+    if (ents.size() < 2) return 0;
+    mp3d_batch *b = d->b;
+    HIPCHK(hipSetDevice(b->device));
+    int r = own_after_last(b);
+    if (!r) r = flush_tail(b, b->own);
+    if (r) return r;
+    /* the state before the read-ahead, for ra_settle */
+    HIPCHK(hipMemcpyAsync(d->snap, b->st, sizeof(StreamState), hipMemcpyDeviceToDevice, b->own));
+    memset(d->ra_in + o, 0, 64);
+    const uint64_t off = 0;
+    r = batch_decode(b, d->ra_in_m, &off, &o, 1, (int)ents.size(), d->ra_pcm_m, f32, d->ra_inf_m, nullptr, true, kinds,
+                     true, MP3D_PF_RA_SEG);
+    if (r) return r;
+    d->ra.swap(ents);
+    d->ra_next = 0;
+    d->ra_f32 = f32;
+    d->ra_frames0 = d->frames;
+    d->ra_kind0 = d->kind;
+    return 1;
 }
 
 static int decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, void *pcm, bool f32, bool last,
@@ -1164,29 +1354,55 @@ static int decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, void *pcm
     /* next frame (ID3v2 / junk skipped); a final frame cut short only with
      * MP3D_FRAME_LAST: decoded with the missing bytes as zeros (k_demux) */
     const int loc = pf_locate(buf, bytes, d->kind, d->frames == 0, last, &pos, &fb, &have);
+    /* a frame read ahead: the same bytes at the same place, the same sink */
+    if (d->ra_next < d->ra.size()) {
+        const mp3d_dec::RaEnt &e = d->ra[d->ra_next];
+        if (!(loc > 0 && f32 == d->ra_f32 && pos == e.pos && have == (size_t)fb && (size_t)fb == e.len &&
+              !memcmp(buf + pos, d->ra_in + e.off, e.len))) {
+            const int r = ra_settle(d);
+            if (r) return r;
+        }
+    } else if (!d->ra.empty()) {
+        d->ra.clear(); /* all served */
+        d->ra_next = 0;
+    }
     if (loc <= 0) {
         info->frame_bytes = (int)pos;
         return loc;
     }
-    uint64_t off = 0;
-    uint32_t sz = MP3D_PF_BYTES;
-    memcpy(d->h_in, buf + pos, have); /* have <= fb <= MP3D_MAX_FRAME_BYTES */
-    int r;
-    if (d->fused) {
-        r = pf_fused(d, (uint32_t)have, f32, host_frame_kind(buf + pos) == 2);
-    } else {
-        memset(d->h_in + have, 0, MP3D_PF_BYTES - have);
-        /* mapped pinned buffers: the kernels read the frame and write PCM +
-         * info in place (three launches + one sync); else staged copies */
-        const bool mapped = d->m_in != nullptr;
-        r = mapped ? batch_decode(d->b, d->m_in, &off, &sz, 1, 1, d->m_out, f32, d->m_info, nullptr, true,
-                                  host_frame_kind(buf + pos), true)
-                   : batch_decode(d->b, d->h_in, &off, &sz, 1, 1, d->h_out, f32, d->h_info, nullptr, true,
-                                  host_frame_kind(buf + pos)); /* 1 MPEG-1, 2 LSF */
+    bool cached = d->ra_next < d->ra.size();
+    if (!cached && have == (size_t)fb) {
+        const int r = ra_fill(d, buf, bytes, f32);
+        if (r < 0) return r;
+        cached = r == 1;
     }
-    if (r) return r;
-    const mp3d_frame_info fi = *d->h_info;
-    const float *out = d->h_out;
+    mp3d_frame_info fi;
+    const void *out;
+    if (cached) {
+        fi = d->ra_inf[d->ra_next];
+        out = (const uint8_t *)d->ra_pcm + d->ra_next * 2304 * (f32 ? sizeof(float) : sizeof(int16_t));
+        d->ra_next++;
+    } else {
+        uint64_t off = 0;
+        uint32_t sz = MP3D_PF_BYTES;
+        memcpy(d->h_in, buf + pos, have); /* have <= fb <= MP3D_MAX_FRAME_BYTES */
+        int r;
+        if (d->fused) {
+            r = pf_fused(d, (uint32_t)have, f32, host_frame_kind(buf + pos) == 2);
+        } else {
+            memset(d->h_in + have, 0, MP3D_PF_BYTES - have);
+            /* mapped pinned buffers: the kernels read the frame and write PCM +
+             * info in place (three launches + one sync); else staged copies */
+            const bool mapped = d->m_in != nullptr;
+            r = mapped ? batch_decode(d->b, d->m_in, &off, &sz, 1, 1, d->m_out, f32, d->m_info, nullptr, true,
+                                      host_frame_kind(buf + pos), true)
+                       : batch_decode(d->b, d->h_in, &off, &sz, 1, 1, d->h_out, f32, d->h_info, nullptr, true,
+                                      host_frame_kind(buf + pos)); /* 1 MPEG-1, 2 LSF */
+        }
+        if (r) return r;
+        fi = *d->h_info;
+        out = d->h_out;
+    }
     d->frames++;
     if (fi.frame_bytes) d->kind = host_frame_kind(buf + pos);
     *info = fi;
@@ -1241,11 +1457,15 @@ extern "C" int mp3d_batch_set_state(mp3d_batch *b, int first, int n, const void 
 
 extern "C" int mp3d_dec_get_state(mp3d_dec *d, void *buf) {
     if (!d) return MP3D_E_ARG;
+    const int r = ra_settle(d); /* the state after the frames served, not after those read ahead */
+    if (r) return r;
     return mp3d_batch_get_state(d->b, 0, 1, buf);
 }
 
 extern "C" int mp3d_dec_set_state(mp3d_dec *d, const void *buf) {
     if (!d || !buf) return MP3D_E_ARG;
+    d->ra.clear(); /* replaced whole: nothing read ahead applies */
+    d->ra_next = 0;
     const int r = mp3d_batch_set_state(d->b, 0, 1, buf);
     if (r) return r;
     /* host mirror of the family lock and "past the stream start" (ID3v2 skip) */

@@ -54,6 +54,64 @@ __device__ __forceinline__ void dct3_9(const float *a, float *v) {
 }
 
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 pfma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 bc(float c) { return (f32x2){c, c}; }
+
+/* dct3_9 on packed pairs: both 9-point DCT-IIIs of the fast IMDCT (the even
+ * input in .x, the odd one in .y) in one pass of packed FP32 ops
+ * (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: half the VALU issues); per
+ * element the same operations in the same order as dct3_9, so bit-identical */
+/* the packed constants (c, c) come from LDS (kc, a broadcast read per use):
+ * as literals they take SGPR pairs, which the kernel does not have to spare
+ * (spills) */
+#define IMDCT36_K {5.019099188e-01f, 5.176380902e-01f, 5.516889595e-01f, 6.103872944e-01f, 7.071067812e-01f, \
+                   8.717233978e-01f, 1.183100792e+00f, 1.931851653e+00f, 5.736856623e+00f}
+#define DCT9_KC {9.848077530e-01f, 9.396926208e-01f, 8.660254038e-01f, 7.660444431e-01f, \
+                 6.427876097e-01f, 3.420201433e-01f, 1.736481777e-01f}
+__device__ __forceinline__ void dct3_9p(const f32x2 *a, f32x2 *v, const f32x2 *kc) {
+    auto ld = [&](int i) { return ((const __attribute__((address_space(3))) f32x2 *)(uintptr_t)kc)[i]; };
+    const f32x2 C10 = ld(0), C20 = ld(1), C30 = ld(2), C40 = ld(3), C50 = ld(4), C70 = ld(5), C80 = ld(6);
+    const f32x2 ev0 = pfma(a[8], C80, pfma(a[6], bc(0.5f), pfma(a[4], C40, pfma(a[2], C20, a[0]))));
+    const f32x2 od0 = pfma(a[7], C70, pfma(a[5], C50, pfma(a[3], C30, a[1] * C10)));
+    v[0] = ev0 + od0;
+    v[8] = ev0 - od0;
+    const f32x2 ev1 = pfma(a[8], bc(-0.5f), (pfma(a[4], bc(-0.5f), pfma(a[2], bc(0.5f), a[0])) - a[6]));
+    const f32x2 od1 = pfma(a[7], -C30, pfma(a[5], -C30, a[1] * C30));
+    v[1] = ev1 + od1;
+    v[7] = ev1 - od1;
+    const f32x2 ev2 = pfma(a[8], C40, pfma(a[6], bc(0.5f), pfma(a[4], -C20, pfma(a[2], -C80, a[0]))));
+    const f32x2 od2 = pfma(a[7], C10, pfma(a[5], -C70, pfma(a[3], -C30, a[1] * C50)));
+    v[2] = ev2 + od2;
+    v[6] = ev2 - od2;
+    const f32x2 ev3 = pfma(a[8], -C20, pfma(a[6], bc(0.5f), pfma(a[4], C80, pfma(a[2], -C40, a[0]))));
+    const f32x2 od3 = pfma(a[7], -C50, pfma(a[5], C10, pfma(a[3], -C30, a[1] * C70)));
+    v[3] = ev3 + od3;
+    v[5] = ev3 - od3;
+    v[4] = a[0] - a[2] + a[4] - a[6] + a[8];
+}
+
+/* imdct36_w with the two 9-point DCT-IIIs packed (dct3_9p) and the output
+ * in pairs W[n] = (w[n], w[17 - n]), n < 9: the window stage takes w[9 + i]
+ * and w[8 - i] from one pair.  Bit-identical to imdct36_w. */
+__device__ __forceinline__ void imdct36_wp(const float *X, f32x2 *W, const f32x2 *kc) {
+    f32x2 a[9], V[9];
+    float zprev = 0.f;
+#pragma unroll
+    for (int m = 0; m < 9; m++) {
+        const float e = m ? X[2 * m] + X[2 * m - 1] : X[0];
+        const float zo = X[2 * m + 1] + X[2 * m];
+        a[m] = (f32x2){e, zo + zprev};
+        zprev = zo;
+    }
+    dct3_9p(a, V, kc);
+    /* w[n] = E[n] + P[n] K[n], w[17 - n] = E[n] - P[n] K[n]: one packed fma
+     * with the pair (K[n], -K[n]) (kc[7 + n]); fused like the scalar form */
+    const __attribute__((address_space(3))) f32x2 *kk = (const __attribute__((address_space(3))) f32x2 *)(uintptr_t)kc;
+#pragma unroll
+    for (int n = 0; n < 9; n++) W[n] = pfma((f32x2){V[n].y, V[n].y}, kk[7 + n], (f32x2){V[n].x, V[n].x});
+}
+
 /* 36-point IMDCT of one subband's 18 lines (ISO 2.4.3.4) without the 18x36
  * matrix: x_i = y_(i+9) / -y_(26-i) / -y_(i-27) with y the 18-point DCT-IV
  * of X; y_n = w_n / (2 cos(pi (2n+1) / 72)) (scale folded into c_win36), w
@@ -117,7 +175,6 @@ __device__ __forceinline__ void imdct36_w(const float *X, float *w) {
                       * even / odd matrixing halves as the MFMA leaves them) */
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 /* Opaque copy of a loop-invariant LDS index: keeps the compiler from
  * hoisting one address VGPR per unrolled access out of the frame loop
@@ -153,7 +210,16 @@ template <bool LSF> struct SynShared { /* read-only, one copy per workgroup     
     float ce[16][16], co[16][16];    /* matrixing A: C[2m][i], C[2m+1][i], i < 16  */
     float dw[32][16];                /* window taps per output j                   */
     float p43s[512];                 /* sign(k - 256) |k - 256|^(4/3), k < 512     */
-    float w36[4][36];                /* long-block windows (x IMDCT output scale)  */
+    /* long-block windows (x IMDCT output scale) in output pairs (i, 17 - i)
+     * of both halves, wp[par][bt][i] = (w[i], w[17 - i], w[18 + i],
+     * w[35 - i]), with the frequency inversion folded in for odd subbands
+     * (par = sb & 1: the odd output slots negated, which the overlap then
+     * carries negated too; StreamState holds the true values) */
+    f32x4 wp[2][4][9];
+    /* packed-op constants: the 9-point DCT-III cosines (c, c) (DCT9_KC),
+     * then the DCT-IV output scales (K, -K) (IMDCT36_K) */
+    f32x2 kc[7 + 9];
+    float p2q[4]; /* 2^(i/4): pow2_quarter's mantissas, a branch-free lookup */
     float isr[LSF ? 32 : 7][2];      /* intensity ratios: MPEG-1 [is_pos], LSF      */
                                      /* [intensity_scale * 16 + is_pos]            */
 };
@@ -200,7 +266,17 @@ __device__ __forceinline__ void synth_tables(SynShared<LSF> &T, const DevTables 
      * arrive in PCM units without a multiply per sample */
     for (int i = tid; i < 32 * 16; i += NT)
         (&T.dw[0][0])[i] = (&tab->dwin[0][0])[i] * (F32 ? 1.0f : 32768.0f);
-    for (int i = tid; i < 4 * 36; i += NT) (&T.w36[0][0])[i] = (&c_win36[0][0])[i];
+    if (tid < 7 + 9) {
+        const float c9[7] = DCT9_KC, k9[9] = IMDCT36_K;
+        T.kc[tid] = tid < 7 ? (f32x2){c9[tid], c9[tid]} : (f32x2){k9[tid - 7], -k9[tid - 7]};
+    }
+    if (tid < 4) T.p2q[tid] = pow2_quarter(tid);
+    for (int k = tid; k < 2 * 4 * 9; k += NT) {
+        const int par = k / 36, bt = (k / 9) % 4, i = k % 9;
+        const float *w = c_win36[bt];
+        const float sa = (par && (i & 1)) ? -1.f : 1.f, sb = (par && !(i & 1)) ? -1.f : 1.f; /* slots i, 17 - i */
+        T.wp[par][bt][i] = (f32x4){sa * w[i], sb * w[17 - i], sa * w[18 + i], sb * w[35 - i]};
+    }
     if (LSF) {
         if (tid < 64) (&T.isr[0][0])[tid] = (&c_is_lsf[0][0][0])[tid];
     } else if (tid < 14) (&T.isr[0][0])[tid] = (&c_is_ratio[0][0])[tid];
@@ -233,7 +309,48 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                                              float *xch = nullptr) {
     static_assert(PF == 0 || (!SRC_XR && !LSF), "PF: k_frame's MPEG-1 decode path only");
     const int f0 = seg * seg_len, f1 = min(F, f0 + seg_len);
-    const int fw = seg ? f0 - 1 : 0; /* first frame decoded (warm-up below f0) */
+    /* first frame decoded (warm-up frames below f0 leave state, no PCM) and
+     * where the state starts: the call's state (StreamState or the previous
+     * call's tail) for segment 0; zeros before a warm-up that fixes it */
+    int fw = seg ? f0 - 1 : 0;
+    bool from_state = seg == 0, ch1_state = false;
+    if (!SRC_XR && seg > 0) {
+        /* decode path (frame-parallel segments of a stream):
+         * the state at f0 is fixed by the last audio frame before it (its
+         * granule 0 the IMDCT overlap, granule 1 the 15 FIFO slots; an LSF
+         * frame has one granule, so the last two).  Frames without audio
+         * (tag, dropped) leave the state alone and are skipped.  A mono
+         * warm-up fixes channel 0 only: channel 1 keeps the call's state,
+         * unless a stereo frame came in between -- then, as when fewer audio
+         * frames precede f0, the segment decodes from the call's state at
+         * frame 0 (exact, just longer). */
+        const uint32_t *rw = (const uint32_t *)(rec + (size_t)s * F);
+        auto audio = [&](int f) {
+            const uint32_t r4 = __builtin_amdgcn_readfirstlane(rw[8 * f + 4]);
+            const uint32_t r6 = __builtin_amdgcn_readfirstlane(rw[8 * f + 6]);
+            return (r4 & 0xFFFFu) != 0u && !(((r6 >> 8) & 0xFFu) & (REC_TAG | REC_DROP));
+        };
+        auto stereo = [&](int f) { return (__builtin_amdgcn_readfirstlane(rw[8 * f + 5]) >> 24) == 2u; };
+        const int need = LSF ? 2 : 1;
+        int found = 0, fa = f0;
+        bool mono = false;
+        for (int f = f0 - 1; f >= 0 && found < need; f--)
+            if (audio(f)) {
+                found++;
+                fa = f;
+                mono = mono || !stereo(f);
+            }
+        bool stereo_before = false;
+        if (found == need && mono)
+            for (int f = 0; f < fa && !stereo_before; f++) stereo_before = audio(f) && stereo(f);
+        if (found < need || stereo_before) {
+            fw = 0;
+            from_state = true;
+        } else {
+            fw = fa;
+            ch1_state = mono;
+        }
+    }
     float *const sBuf = Wd.buf;
     const int lane = threadIdx.x & 63;
     const int ch = lane >> 5;
@@ -242,25 +359,31 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
 
     StreamState &S = st[s];
     const int wa = tab->win_a[sb], wb = tab->win_b[sb];
-    float ov[18];
+    /* IMDCT overlap in output pairs ovp[i] = (ov[i], ov[17 - i]), with the
+     * odd slots of odd subbands negated (the frequency inversion folded into
+     * the window tables, SynShared::wp); state in and out as true values */
+    f32x2 ovp[9];
+    const float sgo = (sb & 1) ? -1.f : 1.f; /* slot sign of odd slots */
+    const f32x2 sgp[2] = {(f32x2){1.f, sgo}, (f32x2){sgo, 1.f}}; /* pair i even / odd */
     /* synthesis history: ha[k] = X_{k-14}[wa], hb[k] = X_{k-15}[wb] (slot
      * index relative to the granule's first slot; fifo[t] = slot t - 15)  */
     float ha[14], hb[15];
     constexpr int TAIL = (int)(sizeof(S.overlap) + sizeof(S.fifo)) / 4; /* floats per stream tail */
-    if (seg == 0) {
-        /* state in: StreamState, or the previous synth-only call's tail
-         * (the same overlap + fifo layout, packed per stream) */
+    if (from_state || (ch1_state && ch == 1)) {
+        /* state in: StreamState, or the previous call's tail (the same
+         * overlap + fifo layout, packed per stream) */
         const float *ovi = st_tail_in ? st_tail_in + (size_t)s * TAIL : &S.overlap[0][0][0];
         const float *ffi = ovi + sizeof(S.overlap) / 4;
 #pragma unroll
-        for (int i = 0; i < 18; i++) ov[i] = ovi[(ch * 32 + sb) * 18 + i];
+        for (int i = 0; i < 9; i++)
+            ovp[i] = (f32x2){ovi[(ch * 32 + sb) * 18 + i], ovi[(ch * 32 + sb) * 18 + 17 - i]} * sgp[i & 1];
 #pragma unroll
         for (int k = 0; k < 14; k++) ha[k] = ffi[(ch * MP3D_FIFO_SLOTS + k + 1) * 32 + wa];
 #pragma unroll
         for (int k = 0; k < 15; k++) hb[k] = ffi[(ch * MP3D_FIFO_SLOTS + k) * 32 + wb];
     } else {
 #pragma unroll
-        for (int i = 0; i < 18; i++) ov[i] = 0.f;
+        for (int i = 0; i < 9; i++) ovp[i] = (f32x2){0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < 14; k++) ha[k] = 0.f;
 #pragma unroll
@@ -286,17 +409,24 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
      * 0 .. 27) and the FrameRec words (lanes 32 .. 39) TWO granules ahead,
      * so each is[] load is masked by its unit's nz_end: the rzero tail that
      * k_huffman never wrote is not fetched (HBM read traffic ~ nonzero
-     * prefix, not 2 x 576 lines).  nmeta = words of the current granule,
-     * nmeta2 = words of the next one. */
-    uint32_t nis[2][5], nmeta = 0, nmeta2 = 0;
+     * prefix, not 2 x 576 lines).  wm / wr = the UnitMeta / FrameRec words
+     * of two consecutive granules.  MPEG-1 decode (PAR): slot = granule
+     * parity, with the granule loop unrolled, so each load writes its
+     * loop-carried register directly; otherwise slot 0 = the current
+     * granule, slot 1 the next, shifted after each prefetch. */
+    constexpr bool PAR = !SRC_XR && !LSF && PF == 0;
+    uint32_t nis[2][5], wm[2] = {0u, 0u}, wr[2] = {0u, 0u};
     constexpr int GSTEP = LSF ? 2 : 1; /* is[] granule slots per decoded granule */
-    auto load_words = [&](int g) { /* buffer loads past F return 0 */
+    /* two unconditional loads; a lane outside a word range gets an offset
+     * past the buffer (reads 0), and so do granules past F.  (As one value
+     * loaded in two divergent branches, the merged result was copied into
+     * the loop-carried register right after the loads -- a vmcnt(0) wait
+     * that made the whole prefetch synchronous.) */
+    auto load_words = [&](int g, uint32_t &vm, uint32_t &vr) {
         const int lo = opaque(lane * 4);
-        uint32_t v = 0u;
-        if (lane < 2 * MW) v = __builtin_amdgcn_raw_buffer_load_b32(r_meta, lo, g * 2 * (int)sizeof(UnitMeta), 0);
-        else if (lane >= 32 && lane < 40)
-            v = __builtin_amdgcn_raw_buffer_load_b32(r_rec, lo - 128, (g >> 1) * (int)sizeof(FrameRec), 0);
-        return v;
+        const int om = lane < 2 * MW ? lo : 0x40000000, orr = (lane >= 32 && lane < 40) ? lo - 128 : 0x40000000;
+        vm = __builtin_amdgcn_raw_buffer_load_b32(r_meta, om, g * 2 * (int)sizeof(UnitMeta), 0);
+        vr = __builtin_amdgcn_raw_buffer_load_b32(r_rec, orr, (g >> 1) * (int)sizeof(FrameRec), 0);
     };
     auto load_is = [&](int g, int nz0, int nz1) {
         const int lo = opaque(lane * 4);
@@ -314,25 +444,35 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
     /* is[g] masked by granule g's nz_end from its meta words m (channel 1
      * only in a stereo frame: FrameRec.nch, lane 37): every line >= nz_end
      * then reads as 0 in registers, so phase Q needs no rzero mask */
-    auto load_is_masked = [&](int g, uint32_t m) {
-        const bool st = ((uint32_t)__builtin_amdgcn_readlane((int)m, 37) >> 24) == 2u;
-        const int nz0 = __builtin_amdgcn_readlane((int)m, 12) & 0xFFFF;
-        const int nz1 = st ? __builtin_amdgcn_readlane((int)m, MW + 12) & 0xFFFF : 0;
+    auto load_is_masked = [&](int g, uint32_t mm, uint32_t mr) {
+        const bool st = ((uint32_t)__builtin_amdgcn_readlane((int)mr, 37) >> 24) == 2u;
+        const int nz0 = __builtin_amdgcn_readlane((int)mm, 12) & 0xFFFF;
+        const int nz1 = st ? __builtin_amdgcn_readlane((int)mm, MW + 12) & 0xFFFF : 0;
         load_is(g, nz0, nz1);
     };
-    /* steady state: is[g] masked by nmeta2 (granule g's words), then shift */
-    auto prefetch = [&](int g) {
-        load_is_masked(g, nmeta2);
-        nmeta = nmeta2;
-        nmeta2 = load_words(g + GSTEP);
+    /* steady state, from granule slot cs: is[g] masked by the next
+     * granule's words, then granule g + 1's words (PAR: into the slot the
+     * current granule frees; else a shift).  As one rotated variable, the
+     * merged load result was copied into the loop-carried register right
+     * after the loads -- a vmcnt(0) wait that made the prefetch synchronous
+     * (k_synth spent ~28 % of its wave time there, abx/ptime.py). */
+    auto prefetch = [&](int g, int cs) {
+        load_is_masked(g, wm[cs ^ 1], wr[cs ^ 1]);
+        if (PAR) {
+            load_words(g + GSTEP, wm[cs], wr[cs]);
+        } else {
+            wm[0] = wm[1];
+            wr[0] = wr[1];
+            load_words(g + GSTEP, wm[1], wr[1]);
+        }
     };
-    /* entry and after a frame without audio: the words first, drained, then
-     * the masked is[] (off the common path) */
+    /* entry and after a frame without audio (g even for PAR): the words
+     * first, drained, then the masked is[] (off the common path) */
     auto prefetch_full = [&](int g) {
-        nmeta = load_words(g);
-        nmeta2 = load_words(g + GSTEP);
+        load_words(g, wm[0], wr[0]);
+        load_words(g + GSTEP, wm[1], wr[1]);
         WAIT_VMCNT0();
-        load_is_masked(g, nmeta);
+        load_is_masked(g, wm[0], wr[0]);
     };
     /* SRC_XR (config 2): the next granule's spectra (lane: line pairs
      * lane + 64 i of both channels, as is[] on the decode path) and block
@@ -375,9 +515,9 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
             sr = xr_sr;
         } else {
             /* FrameRec words 4 .. 6 from the prefetch (lanes 36 .. 38) */
-            const uint32_t r4 = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, 36);
-            const uint32_t r5 = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, 37);
-            const uint32_t r6 = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, 38);
+            const uint32_t r4 = (uint32_t)__builtin_amdgcn_readlane((int)wr[0], 36);
+            const uint32_t r5 = (uint32_t)__builtin_amdgcn_readlane((int)wr[0], 37);
+            const uint32_t r6 = (uint32_t)__builtin_amdgcn_readlane((int)wr[0], 38);
             const uint32_t first_gr = (r6 >> 8) & 0xFFu;
             if (!(r4 & 0xFFFFu) || (first_gr & (REC_TAG | REC_DROP))) {
                 /* no audio in this frame: fetch the next frame's granule 0
@@ -394,7 +534,9 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
         const bool active = ch < nch;
         const uint64_t amask = __ballot(active); /* lanes of coded channels */
         const uint32_t(*lpair)[288] = T.lpair[sr];
+#pragma unroll /* the words' slot (cs) is then a constant per copy */
         for (int gr = PF == 2 ? 1 : 0; gr < (LSF || PF == 1 ? 1 : 2); gr++) { /* LSF: one granule per frame */
+            const int cs = PAR ? gr : 0; /* slot of this granule's words */
             /* lane-derived indices are re-derived from an opaque copy each
              * granule so they are not hoisted and held live across the loop */
             const int lane = opaque((int)(threadIdx.x & 63));
@@ -448,15 +590,15 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                     for (int i = 0; i < 5; i++) cis[c][i] = nis[c][i];
                 /* UnitMeta into LDS for the (rare) intensity path; the common
                  * path reads the prefetched words straight from registers */
-                if (lane < 2 * MW && lane / MW < nch) ((uint32_t *)&Wd.m[0])[lane] = nmeta;
+                if (lane < 2 * MW && lane / MW < nch) ((uint32_t *)&Wd.m[0])[lane] = wm[cs];
                 /* words 10..12: gain, block type, mixed, scalefac_scale |
                  * preflag, sbg[3] | nz_end (UnitMeta layout) */
-                const uint32_t m10a = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, 10);
-                const uint32_t m11a = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, 11);
-                const uint32_t m12a = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, 12);
-                const uint32_t m10b = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, MW + 10);
-                const uint32_t m11b = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, MW + 11);
-                const uint32_t m12b = (uint32_t)__builtin_amdgcn_readlane((int)nmeta, MW + 12);
+                const uint32_t m10a = (uint32_t)__builtin_amdgcn_readlane((int)wm[cs], 10);
+                const uint32_t m11a = (uint32_t)__builtin_amdgcn_readlane((int)wm[cs], 11);
+                const uint32_t m12a = (uint32_t)__builtin_amdgcn_readlane((int)wm[cs], 12);
+                const uint32_t m10b = (uint32_t)__builtin_amdgcn_readlane((int)wm[cs], MW + 10);
+                const uint32_t m11b = (uint32_t)__builtin_amdgcn_readlane((int)wm[cs], MW + 11);
+                const uint32_t m12b = (uint32_t)__builtin_amdgcn_readlane((int)wm[cs], MW + 12);
                 bt0 = (int)(m10a >> 8) & 0xFF;
                 mx0 = (int)(m10a >> 16) & 0xFF;
                 if (nch == 2) {
@@ -470,7 +612,25 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                 /* per-band scale 2^(q/4), lane = band idx (long b | 22 + 3 b + w);
                  * the lane's scalefactor byte comes from the prefetched meta
                  * words by one cross-lane read per channel */
-                {
+                /* 2^(q/4) = ldexp(2^((q & 3) / 4), q >> 2): the mantissa from a
+                 * 4-entry LDS table (as a select chain the compiler built
+                 * divergent branches) */
+                auto p2q = [&](int q) {
+                    const float v = ldexpf(T.p2q[q & 3], q >> 2);
+                    return ms_fold ? v * isq : v;
+                };
+                if (var[0] == 0 && (nch == 1 || var[1] == 0)) {
+                    /* long blocks in every coded channel (the common case): both
+                     * channels' 22 band scales in one pass, lane = (ch, band) */
+                    const int c = lane >> 5, bl = lane & 31, j = bl < 22 ? bl : 21;
+                    const uint32_t g10 = c ? m10b : m10a, g11 = c ? m11b : m11a;
+                    const int gain = (int)(g10 & 0xFFu) - 210, shift = (int)(g10 >> 24) + 1;
+                    const uint32_t wd = (uint32_t)__shfl((int)wm[cs], c * MW + (j >> 2));
+                    const int sf = (int)(wd >> (8 * (j & 3))) & 0xFF;
+                    const int pre = (g11 & 0xFFu) ? (int)(MP3D_PRETAB_BITS >> (2 * j)) & 3 : 0;
+                    const float v = p2q(gain - ((sf + pre) << shift));
+                    if (bl < 22) Wd.scale[c][bl] = v;
+                } else {
                     const bool lng = lane < 22;
                     const int b = (lane - 22) / 3, w = lane - 22 - 3 * b;
                     auto band_scale = [&](uint32_t g10, uint32_t g11, int cbase) {
@@ -478,12 +638,11 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                         const bool mixed = ((g10 >> 16) & 0xFFu) != 0u, preflag = (g11 & 0xFFu) != 0u;
                         int j = mixed ? 8 + 3 * (b - 3) + w : 3 * b + w;
                         j = lng ? lane : (j < 0 ? 0 : (j > 39 ? 39 : j));
-                        const uint32_t wd = (uint32_t)__shfl((int)nmeta, cbase + (j >> 2));
+                        const uint32_t wd = (uint32_t)__shfl((int)wm[cs], cbase + (j >> 2));
                         const int sf = (int)(wd >> (8 * (j & 3))) & 0xFF;
                         const int pre = preflag ? (int)(MP3D_PRETAB_BITS >> (2 * (lane & 31))) & 3 : 0;
                         const int sbg = (int)(g11 >> (8 * (1 + (w < 3 ? w : 0)))) & 0xFF;
-                        const int q = lng ? gain - ((sf + pre) << shift) : gain - 8 * sbg - (sf << shift);
-                        return ms_fold ? pow2_quarter(q) * isq : pow2_quarter(q);
+                        return p2q(lng ? gain - ((sf + pre) << shift) : gain - 8 * sbg - (sf << shift));
                     };
                     Wd.scale[0][lane] = band_scale(m10a, m11a, 0);
                     if (nch == 2) Wd.scale[1][lane] = band_scale(m10b, m11b, MW);
@@ -619,7 +778,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                 }
                 /* the next granule's loads fly during phases I, M, W (issued
                  * after cis is consumed: fewer live registers in phase Q) */
-                if (PF == 0 && (LSF ? f + 1 < f1 : (gr == 0 || f + 1 < f1))) prefetch(LSF ? 2 * f + 2 : 2 * f + gr + 1);
+                if (PF == 0 && (LSF ? f + 1 < f1 : (gr == 0 || f + 1 < f1))) prefetch(LSF ? 2 * f + 2 : 2 * f + gr + 1, cs);
                 /* scatter in (short-block reordered) position */
 #pragma unroll
                 for (int i = 0; i < 5; i++) {
@@ -647,7 +806,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
             if (PF == 2) { /* granule 0's overlap from the other wave */
                 __syncthreads();
 #pragma unroll
-                for (int i = 0; i < 18; i++) ov[i] = xch[i * 64 + lane];
+                for (int i = 0; i < 9; i++) ovp[i] = (f32x2){xch[2 * i * 64 + lane], xch[(2 * i + 1) * 64 + lane]};
             }
             const int bt = ch ? bt1 : bt0, mixed = ch ? mx1 : mx0;
             float o18[18];
@@ -677,6 +836,8 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                 /* both butterflies computed, then selected: written as
                  * conditional stores the compiler built a divergent branch
                  * plus ~50 register copies around it */
+                /* scalar: as packed pairs the operands need a register move
+                 * each (they arrive as consecutive pairs from LDS) */
 #pragma unroll
                 for (int k = 0; k < 8; k++) {
                     const float lo = x[17 - k], hi = x[k];
@@ -687,17 +848,20 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                 }
                 const bool long_imdct = bt != 2 || (mixed && sb < 2);
                 if (long_imdct) {
-                    const float *wv = T.w36[bt == 2 ? 0 : bt];
-                    float w[18];
-                    imdct36_w(x, w);
+                    /* packed window + overlap: pair i = output slots (i, 17 - i)
+                     * from W[8 - i] = (w[8 - i], w[9 + i]) */
+                    const f32x4 *wq = T.wp[sb & 1][bt == 2 ? 0 : bt];
+                    f32x2 W[9];
+                    imdct36_wp(x, W, T.kc);
 #pragma unroll
                     for (int i = 0; i < 9; i++) {
-                        o18[i] = fmaf(w[9 + i], wv[i], ov[i]);
-                        o18[17 - i] = fmaf(w[9 + i], wv[17 - i], ov[17 - i]);
-                        const float n0 = w[8 - i] * wv[18 + i];
-                        const float n1 = w[8 - i] * wv[35 - i];
-                        ov[i] = lane_sel(amask, ov[i], n0);
-                        ov[17 - i] = lane_sel(amask, ov[17 - i], n1);
+                        const f32x4 q = wq[i];
+                        const f32x2 o = pfma(bc(W[8 - i].y), (f32x2){q.x, q.y}, ovp[i]);
+                        o18[i] = o.x;
+                        o18[17 - i] = o.y;
+                        const f32x2 nv = bc(W[8 - i].x) * (f32x2){q.z, q.w};
+                        ovp[i].x = lane_sel(amask, ovp[i].x, nv.x);
+                        ovp[i].y = lane_sel(amask, ovp[i].y, nv.y);
                     }
                 } else {
                     /* z[6w+6+i] += y_w[i] * win12[i], w = 0..2, i = 0..11 */
@@ -722,25 +886,37 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                             z[6 * w + 11 - i] = fmaf(h[3 + i], MP3D_K_WIN12[11 - i], z[6 * w + 11 - i]);
                         }
                     }
+                    /* true overlap in, slots in the folded sign convention out */
+                    float ovt[18];
 #pragma unroll
-                    for (int i = 0; i < 18; i++) o18[i] = (i < 6 ? 0.f : z[i - 6]) + ov[i];
+                    for (int i = 0; i < 9; i++) {
+                        const f32x2 t = ovp[i] * sgp[i & 1];
+                        ovt[i] = t.x;
+                        ovt[17 - i] = t.y;
+                    }
 #pragma unroll
-                    for (int i = 0; i < 18; i++) {
-                        const float n = i < 12 ? z[12 + i] : 0.f;
-                        ov[i] = lane_sel(amask, ov[i], n);
+                    for (int i = 0; i < 18; i++) o18[i] = ((i < 6 ? 0.f : z[i - 6]) + ovt[i]) * ((i & 1) ? sgo : 1.f);
+#pragma unroll
+                    for (int i = 0; i < 9; i++) {
+                        const f32x2 n = (f32x2){i < 12 ? z[12 + i] : 0.f, 17 - i < 12 ? z[29 - i] : 0.f} * sgp[i & 1];
+                        ovp[i].x = lane_sel(amask, ovp[i].x, n.x);
+                        ovp[i].y = lane_sel(amask, ovp[i].y, n.y);
                     }
                 }
             }
             if (PF == 1) { /* granule 0's overlap for the other wave */
 #pragma unroll
-                for (int i = 0; i < 18; i++) xch[i * 64 + lane] = ov[i];
+                for (int i = 0; i < 9; i++) {
+                    xch[2 * i * 64 + lane] = ovp[i].x;
+                    xch[(2 * i + 1) * 64 + lane] = ovp[i].y;
+                }
                 __syncthreads();
             }
             wave_sync(); /* every lane has read its xr before S overwrites it */
             {
                 const int sw = opaque(18 * ch * SROW + sb);
 #pragma unroll
-                for (int t = 0; t < 18; t++) sBuf[sw + t * SROW] = ((sb & 1) && (t & 1)) ? -o18[t] : o18[t];
+                for (int t = 0; t < 18; t++) sBuf[sw + t * SROW] = o18[t]; /* frequency inversion already in */
             }
             wave_sync();
             /* ---------------- phase M: matrixing on the matrix cores ------- */
@@ -937,7 +1113,11 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
         float *ovo = st_tail ? st_tail + (size_t)s * TAIL : &S.overlap[0][0][0];
         float *ffo = ovo + sizeof(S.overlap) / 4;
 #pragma unroll
-        for (int i = 0; i < 18; i++) ovo[(ch * 32 + sb) * 18 + i] = ov[i];
+        for (int i = 0; i < 9; i++) {
+            const f32x2 t = ovp[i] * sgp[i & 1];
+            ovo[(ch * 32 + sb) * 18 + i] = t.x;
+            ovo[(ch * 32 + sb) * 18 + 17 - i] = t.y;
+        }
 #pragma unroll
         for (int k = 0; k < 14; k++) ffo[(ch * MP3D_FIFO_SLOTS + k + 1) * 32 + wa] = ha[k];
 #pragma unroll
@@ -965,9 +1145,10 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
          * stream of its variant leaves before staging any table (the same
          * decision in every lane: no barrier is skipped by part of it). */
         bool any = false;
+        const int nsg = (F + seg_len - 1) / seg_len;
 #pragma unroll
         for (int k = 0; k < SYN_WAVES; k++) {
-            const int sk = blockIdx.x * SYN_WAVES + k;
+            const int sk = (blockIdx.x * SYN_WAVES + k) / nsg;
             if (sk < n_streams) any |= (st[sk].kind == 2) == LSF;
         }
         if (!any) return;
@@ -1151,17 +1332,22 @@ void launch_frame(const uint8_t *in_host, uint32_t in_have, const uint64_t *in_o
 #undef MP3D_FRAME_LAUNCH
 }
 
+/* seg_len < F: frame-parallel segments (one wave each, warm-up frames
+ * before each; synth_stream); the final overlap + fifo then go to st_tail
+ * (st_tail_in, when given, holds the streams' state in place of st) */
 void launch_synth(const FrameRec *rec, const int16_t *is_buf, const UnitMeta *meta, const DevTables *tab,
-                  StreamState *st, void *pcm, bool f32, int n_streams, int F, int kinds, hipStream_t strm) {
-    const dim3 grid((n_streams + SYN_WAVES - 1) / SYN_WAVES), block(64 * SYN_WAVES);
+                  StreamState *st, void *pcm, bool f32, int n_streams, int F, int kinds, int seg_len, float *st_tail,
+                  const float *st_tail_in, hipStream_t strm) {
+    const int waves = n_streams * ((F + seg_len - 1) / seg_len);
+    const dim3 grid((waves + SYN_WAVES - 1) / SYN_WAVES), block(64 * SYN_WAVES);
     /* the family variants in `kinds` (bit 0 MPEG-1, bit 1 LSF; a batch
      * launches both); a workgroup without a stream of its variant exits
      * after SYN_WAVES scalar loads (the LSF launch on an all-MPEG-1 batch
      * costs only its workgroup dispatch) */
 #define MP3D_SYNTH_LAUNCH(F32_, LSF_)                                                                            \
     hipLaunchKernelGGL((k_synth<false, F32_, LSF_>), grid, block, 0, strm, rec, is_buf, meta, (const float *)nullptr, \
-                       (const uint8_t *)nullptr, (const uint8_t *)nullptr, tab, st, pcm, n_streams, F, 2, 0, F,     \
-                       (float *)nullptr, (const float *)nullptr)
+                       (const uint8_t *)nullptr, (const uint8_t *)nullptr, tab, st, pcm, n_streams, F, 2, 0, seg_len, \
+                       st_tail, st_tail_in)
     if (f32) {
         if (kinds & 1) MP3D_SYNTH_LAUNCH(true, false);
         if (kinds & 2) MP3D_SYNTH_LAUNCH(true, true);

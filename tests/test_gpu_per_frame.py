@@ -15,16 +15,20 @@ import mp3_amd
 pytestmark = pytest.mark.gpu
 
 
-def _decoder(fused, opts=0):
-    old = os.environ.get("MP3D_PF_FUSED")
-    os.environ["MP3D_PF_FUSED"] = "1" if fused else "0"
+def _decoder(fused, opts=0, readahead=0):
+    """readahead=0: every call through the single-frame path under test
+    (the read-ahead has its own tests, tests/test_gpu_readahead.py)"""
+    env = {"MP3D_PF_FUSED": "1" if fused else "0", "MP3D_PF_READAHEAD": str(readahead)}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         d = mp3_amd.Decoder()
     finally:
-        if old is None:
-            del os.environ["MP3D_PF_FUSED"]
-        else:
-            os.environ["MP3D_PF_FUSED"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
     if opts:
         d.set_options(opts)
     return d

@@ -36,10 +36,12 @@ def main():
     dec.decode(d_in, offs, sizes, F, pcm=pcm)
     torch.cuda.synchronize()
     assert L.mp3d_dbg_ptime(out.ctypes.data) == 0
-    names = ["Q", "I", "M", "W", "head"]
+    names = ["Q", "I", "M", "W", "head", "Q:scales", "Q:requant", "Q:esc+stereo"]
     tot = float(out[:5].sum())
     gran = n * F * 2
-    print(json.dumps({"fraction": {k: round(float(out[i]) / tot, 3) for i, k in enumerate(names)},
+    frac = {k: round(float(out[i]) / tot, 3) for i, k in enumerate(names)}
+    frac["Q:scatter"] = round(frac["Q"] - frac["Q:scales"] - frac["Q:requant"] - frac["Q:esc+stereo"], 3)
+    print(json.dumps({"fraction": frac,
                       "cycles_per_granule_per_wave": {k: round(float(out[i]) / gran, 1) for i, k in enumerate(names)},
                       "total_per_granule": round(tot / gran, 1), "streams": n}))
 
