@@ -9,13 +9,51 @@
 
 namespace mp3d {
 
-/* k_demux: one wave per stream (demux_stream, mp3d_demux_dev.h) */
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) k_demux(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
-                                              const uint32_t *__restrict__ in_len, uint8_t *__restrict__ md,
-                                              const uint64_t *__restrict__ md_off, StreamState *__restrict__ st,
-                                              FrameRec *__restrict__ rec, uint64_t *__restrict__ sideu,
-                                              DevInfo *__restrict__ infos, int F, int opts) {
-    demux_stream(in, in_off, in_len, md, md_off, st, rec, sideu, infos, F, opts, blockIdx.x, threadIdx.x);
+/* k_demux: one wave per stream (demux_stream, mp3d_demux_dev.h).  The
+ * frame walk is serial: each header's position follows from the previous
+ * frame's size, so from global memory every frame costs a dependent HBM
+ * round trip (~2.5 us a frame on MI355X).  A stream of at most DMX_STAGE
+ * bytes is first staged whole into LDS -- its aligned 16-B blocks, all
+ * loads of a round in flight together -- and walked from there: the serial
+ * chain then runs on LDS latency.  Longer streams walk global memory. */
+#define DMX_STAGE (48 * 1024)
+#define DMX_ROUND 16 /* 16-B blocks per lane in flight per staging round */
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 8)))
+k_demux(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ in_len,
+        uint8_t *__restrict__ md, const uint64_t *__restrict__ md_off, StreamState *__restrict__ st,
+        FrameRec *__restrict__ rec, uint64_t *__restrict__ sideu, DevInfo *__restrict__ infos, int F, int opts) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4))); /* (an array of HIP's uint4 stays in scratch) */
+    __shared__ __attribute__((aligned(16))) u32x4 s_stage[DMX_STAGE / 16];
+    const int s = blockIdx.x, lane = threadIdx.x;
+    const uint64_t base = in_off[s];
+    const uint32_t len = in_len[s];
+    const uint8_t *g = in + base;
+    /* the blocks holding stream bytes: each is an aligned 16-B block with at
+     * least one byte of [g, g + len), so no load leaves the caller's pages */
+    const uintptr_t g0 = (uintptr_t)g & ~(uintptr_t)15;
+    const uint32_t nblk = len ? (uint32_t)(((uintptr_t)g + len - g0 + 15) / 16) : 0u;
+    if (nblk + 1u <= DMX_STAGE / 16) {
+        const u32x4 *src = (const u32x4 *)g0;
+        for (uint32_t b0 = 0; b0 < nblk; b0 += 64u * DMX_ROUND) {
+            u32x4 v[DMX_ROUND];
+#pragma unroll
+            for (int k = 0; k < DMX_ROUND; k++) {
+                const uint32_t i = b0 + 64u * k + (uint32_t)lane;
+                v[k] = src[i < nblk ? i : 0u]; /* unconditional: the loads stay in flight together */
+            }
+#pragma unroll
+            for (int k = 0; k < DMX_ROUND; k++) {
+                const uint32_t i = b0 + 64u * k + (uint32_t)lane;
+                if (i < nblk) s_stage[i] = v[k];
+            }
+        }
+        if (lane == 0) s_stage[nblk] = (u32x4){0u, 0u, 0u, 0u};
+        wave_sync(); /* one wave: its LDS stores land before its loads */
+        SrcLds::u8 *p0 = (SrcLds::u8 *)(uintptr_t)s_stage + ((uintptr_t)g - g0);
+        demux_stream<SrcLds>(p0, base, len, md, md_off, st, rec, sideu, infos, F, opts, s, lane);
+    } else {
+        demux_stream<SrcGlobal>(g, base, len, md, md_off, st, rec, sideu, infos, F, opts, s, lane);
+    }
 }
 
 /* ------------------------------------------------------------------------ */

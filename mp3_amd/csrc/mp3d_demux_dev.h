@@ -23,9 +23,12 @@ inline namespace MP3D_DEMUX_TU {
 
 /* Layer III frame bytes without padding per (sample-rate index 0..8,
  * bitrate index): 144000 kbps / Hz (MPEG-1), 72000 kbps / Hz (LSF); 0 for
- * free format / bad index.  A table read instead of a scalar division in
- * the per-frame header check. */
-__constant__ uint16_t c_frame_bytes[9][16];
+ * free format / bad index -- in the low 16 bits, the bitrate in kbps in the
+ * high 16.  A table read instead of a scalar division in the per-frame
+ * header check; dwords, so that a wave-uniform index is a scalar load (a
+ * sub-dword load is a vector load, and its wait drains the stream's
+ * outstanding payload stores with it). */
+__constant__ uint32_t c_frame_word[9][16];
 /* CRC-16 check tables (crc16_ok): x^(8 j) mod P and 0xFFFF x^(8 n) mod P */
 __constant__ uint32_t c_crc_pow[40];
 __constant__ uint32_t c_crc_init[40];
@@ -47,7 +50,7 @@ __device__ __forceinline__ int hdr_frame_bytes(uint32_t b1, uint32_t b2, int kin
     const int bi = (int)(b2 >> 4);
     if (bi == 0 || bi == 15 || ((b2 >> 2) & 3) == 3) return -1;
     if (kind && hdr_kind(b1) != kind) return -1;
-    return (int)c_frame_bytes[hdr_sr_idx(b1, b2)][bi] + (int)((b2 >> 1) & 1);
+    return (int)(c_frame_word[hdr_sr_idx(b1, b2)][bi] & 0xFFFFu) + (int)((b2 >> 1) & 1);
 }
 
 /* bit offset of unit (gr, ch) inside the side info: MPEG-1 9-bit
@@ -75,17 +78,32 @@ struct HdrWin {        /* 64 bytes at a stream position, spread over lanes 0..15
     __device__ __forceinline__ uint32_t le() const { return raw & keep; }
 };
 
+/* Where demux_stream reads the stream's bytes: global memory (the caller's
+ * buffer in HBM or a mapped host buffer) or LDS (a stream staged whole by
+ * k_demux, the frame staged by k_frame) -- typed pointers, so that the loads
+ * are global_load / ds_read and never flat (a flat load waits on both the
+ * vector-memory and the LDS counter). */
+struct SrcGlobal {
+    typedef const uint8_t u8;
+    typedef const uint32_t u32;
+};
+struct SrcLds {
+    typedef const __attribute__((address_space(3))) uint8_t u8;
+    typedef const __attribute__((address_space(3))) uint32_t u32;
+};
+
 /* Every load is an ALIGNED dword that holds at least one byte of the stream
  * [0, len), so it never leaves the pages of the caller's buffer, however the
  * stream is placed; bytes outside the stream read as zero. */
-__device__ __forceinline__ HdrWin load_win(const uint8_t *p0, uint32_t len, uint32_t pos, int lane) {
+template <class M>
+__device__ __forceinline__ HdrWin load_win(typename M::u8 *p0, uint32_t len, uint32_t pos, int lane) {
     HdrWin w;
     w.pos = pos;
     w.mis = (uint32_t)((uintptr_t)(p0 + pos) & 3u);
     const int64_t a = (int64_t)pos - (int64_t)w.mis + 4 * lane; /* stream offset of the lane's dword */
     const int64_t over = a + 4 - (int64_t)len;                   /* bytes past the stream end */
     w.keep = (lane >= 16 || over >= 4) ? 0u : over > 0 ? 0xFFFFFFFFu >> (8 * over) : 0xFFFFFFFFu;
-    w.raw = w.keep ? *(const uint32_t *)(p0 + a) : 0u;
+    w.raw = w.keep ? *(typename M::u32 *)(p0 + a) : 0u;
     return w;
 }
 
@@ -146,7 +164,7 @@ __device__ bool crc16_ok(const HdrWin &w, uint32_t side_bytes, int lane) {
  * its start, BE24 = encoder delay << 12 | padding, honoured only for
  * "LAME" / "Lavf" / "Lavc" encoders.  t points at "Xing"/"Info", n bytes of
  * the frame follow it.  Returns StreamState.tag_info. */
-__device__ uint32_t parse_info_tag(const uint8_t *t, uint32_t n, uint32_t &frames) {
+template <class P> __device__ uint32_t parse_info_tag(P t, uint32_t n, uint32_t &frames) {
     auto be32 = [&](uint32_t o) {
         return (uint32_t)t[o] << 24 | (uint32_t)t[o + 1] << 16 | (uint32_t)t[o + 2] << 8 | t[o + 3];
     };
@@ -173,32 +191,35 @@ __device__ uint32_t parse_info_tag(const uint8_t *t, uint32_t n, uint32_t &frame
 }
 
 /* one stream's demux (k_demux's wave; also the per-frame k_frame's first
- * phase): stream s, lane 0..63 of the calling wave.  No workgroup barrier
- * inside, so one wave of a larger workgroup may run it. */
-__device__ __forceinline__ void demux_stream(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
-                                             const uint32_t *__restrict__ in_len, uint8_t *__restrict__ md,
+ * phase): stream s, lane 0..63 of the calling wave, its bytes [0, len) at p0
+ * (global memory or LDS, M), base = their offset in the call's input (the
+ * FrameRec frame_off origin).  No workgroup barrier inside, so one wave of a
+ * larger workgroup may run it. */
+template <class M>
+__device__ __forceinline__ void demux_stream(typename M::u8 *p0, uint64_t base, uint32_t len, uint8_t *__restrict__ md,
                                              const uint64_t *__restrict__ md_off, StreamState *__restrict__ st,
                                              FrameRec *__restrict__ rec, uint64_t *__restrict__ sideu,
                                              DevInfo *__restrict__ infos, int F, int opts, int s, int lane) {
-    const uint8_t *p0 = in + in_off[s];
-    const uint32_t len = in_len[s];
     uint8_t *dst = md + md_off[s];
     StreamState &S = st[s];
-    const int carry_in = S.res_len;
-    const bool stream_start = S.frames == 0;
-    int kind = S.kind; /* MPEG family lock (0 until the first frame) */
+    /* the state's scalars in SGPRs before the frame loop: a loop-invariant
+     * value still pending in a VGPR makes the compiler wait for vmcnt(0) at
+     * the loop header -- every frame, behind the previous frame's stores */
+    const int carry_in = __builtin_amdgcn_readfirstlane(S.res_len);
+    const bool stream_start = __builtin_amdgcn_readfirstlane((int)S.frames) == 0;
+    int kind = __builtin_amdgcn_readfirstlane(S.kind); /* MPEG family lock (0 until the first frame) */
     for (int i = lane; i < (carry_in + 3) / 4; i += 64) ((uint32_t *)dst)[i] = ((const uint32_t *)S.res)[i];
     __threadfence_block(); /* carry words may spill past carry_in into payload 0's head */
 
     uint32_t P = (uint32_t)carry_in; /* md position of the next payload         */
     int avail = carry_in;            /* bytes after the previous main-data end */
     uint32_t cur = 0;
-    HdrWin w = load_win(p0, len, 0, lane);
+    HdrWin w = load_win<M>(p0, len, 0, lane);
     if (stream_start && len >= 10 && win_byte(w, 0) == 'I' && win_byte(w, 1) == 'D' && win_byte(w, 2) == '3') {
         const uint32_t sz = (win_byte(w, 6) & 0x7Fu) << 21 | (win_byte(w, 7) & 0x7Fu) << 14 |
                             (win_byte(w, 8) & 0x7Fu) << 7 | (win_byte(w, 9) & 0x7Fu);
         cur = 10 + sz + ((win_byte(w, 5) & 0x10u) ? 10u : 0u);
-        w = load_win(p0, len, cur, lane);
+        w = load_win<M>(p0, len, cur, lane);
     }
     int decoded = 0;
     for (int f = 0; f < F; f++) {
@@ -206,7 +227,7 @@ __device__ __forceinline__ void demux_stream(const uint8_t *__restrict__ in, con
         /* ---- sync: the next valid header at or after cur (resync over junk) */
         int fb = -1;
         while (cur + 4 <= len) {
-            if (w.pos != cur) w = load_win(p0, len, cur, lane);
+            if (w.pos != cur) w = load_win<M>(p0, len, cur, lane);
             const uint32_t lim = min(57u, len - cur - 4);
             uint32_t k = 0;
             for (; k <= lim; k++) {
@@ -227,7 +248,7 @@ __device__ __forceinline__ void demux_stream(const uint8_t *__restrict__ in, con
         bool copy = false;
         uint32_t src_off = 0, frame_at = 0; /* payload and header positions in the stream */
         if (fb > 0) {
-            if (w.pos != cur) w = load_win(p0, len, cur, lane);
+            if (w.pos != cur) w = load_win<M>(p0, len, cur, lane);
             const uint32_t h1 = win_byte(w, 1), h2 = win_byte(w, 2), h3 = win_byte(w, 3);
             const int nch = (h3 >> 6) == 3 ? 1 : 2;
             const int crc = (h1 & 1) ? 0 : 2;
@@ -241,7 +262,7 @@ __device__ __forceinline__ void demux_stream(const uint8_t *__restrict__ in, con
             if (cur + (uint32_t)fb <= len || cur + need <= len) {
                 const uint32_t have = min(len - cur, (uint32_t)fb);
                 const int plen = fb - 4 - crc - side_bytes;
-                r.frame_off = in_off[s] + cur;
+                r.frame_off = base + cur;
                 r.frame_bytes = (uint16_t)fb;
                 r.payload_len = (uint16_t)(plen > 0 ? plen : 0);
                 r.hdr1 = (uint8_t)h1; r.hdr2 = (uint8_t)h2; r.hdr3 = (uint8_t)h3;
@@ -250,7 +271,7 @@ __device__ __forceinline__ void demux_stream(const uint8_t *__restrict__ in, con
                 r.sr_idx = (uint8_t)hdr_sr_idx(h1, h2);
                 r.lsf = (uint8_t)lsf;
                 inf.frame_bytes = fb; inf.channels = nch; inf.hz = (int)MP3D_SAMPLE_RATE[r.sr_idx];
-                inf.layer = 3; inf.bitrate_kbps = lsf ? MP3D_BITRATE_L3_LSF[h2 >> 4] : MP3D_BITRATE_L3[h2 >> 4];
+                inf.layer = 3; inf.bitrate_kbps = (int)(c_frame_word[r.sr_idx][h2 >> 4] >> 16);
                 /* side info: bit offsets relative to the window's dword base */
                 const uint32_t sbit = 8u * (w.mis + 4u + (uint32_t)crc);
                 const int mdb = (int)(win_bits64(w, sbit) >> (lsf ? 56 : 55));
@@ -282,11 +303,11 @@ __device__ __forceinline__ void demux_stream(const uint8_t *__restrict__ in, con
                  * window switching with the reserved block_type 0 */
                 const bool mybad = unit_ok && (((v59 >> 38) & 0x1FFu) > 288u || (v59 & (7ull << 23)) == (4ull << 23));
                 sw = unit_ok ? (v59 << 5) | low5 : 0ull;
-                int p23[2][2];
-                p23[0][0] = __builtin_amdgcn_readlane((int)myp23, 0);
-                p23[0][1] = __builtin_amdgcn_readlane((int)myp23, 1);
-                p23[1][0] = __builtin_amdgcn_readlane((int)myp23, 2);
-                p23[1][1] = __builtin_amdgcn_readlane((int)myp23, 3);
+                /* part2_3_length of unit (gr, ch), by select (an indexed
+                 * array would live in scratch) */
+                const int p00 = __builtin_amdgcn_readlane((int)myp23, 0), p01 = __builtin_amdgcn_readlane((int)myp23, 1),
+                          p10 = __builtin_amdgcn_readlane((int)myp23, 2), p11 = __builtin_amdgcn_readlane((int)myp23, 3);
+                auto p23 = [&](int gr, int ch) { return gr ? (ch ? p11 : p10) : (ch ? p01 : p00); };
                 /* MP3D_OPT_CRC_CHECK: a protected frame whose CRC-16 mismatches
                  * is dropped like a bad one (FFmpeg handle_crc + explode) */
                 const bool crc_bad = (opts & MP3D_OPT_CRC_CHECK) && crc && !crc16_ok(w, (uint32_t)side_bytes, lane);
@@ -315,14 +336,14 @@ __device__ __forceinline__ void demux_stream(const uint8_t *__restrict__ in, con
                     } else {
                         uint32_t bits = (uint32_t)avail * 8u;
                         while (gr0 < ngr && (int)(bits >> 3) < mdb) {
-                            for (int ch = 0; ch < nch; ch++) bits += (uint32_t)p23[gr0][ch];
+                            for (int ch = 0; ch < nch; ch++) bits += (uint32_t)p23(gr0, ch);
                             gr0++;
                         }
                         mdbit = (P - (uint32_t)avail) * 8u + bits - 8u * (uint32_t)mdb;
                     }
                     uint32_t end = mdbit;
                     for (int gr = gr0; gr < 2; gr++)
-                        for (int ch = 0; ch < nch; ch++) end += (uint32_t)p23[gr][ch];
+                        for (int ch = 0; ch < nch; ch++) end += (uint32_t)p23(gr, ch);
                     r.md_bit = mdbit;
                     r.first_gr = (uint8_t)gr0;
                     P += (uint32_t)plen;
@@ -351,9 +372,9 @@ __device__ __forceinline__ void demux_stream(const uint8_t *__restrict__ in, con
          * (issued after the record stores: a store issued behind a pending
          * load made the compiler drain vmcnt(0) before it, i.e. wait for the
          * window right here) */
-        if (cur + 4 <= len && f + 1 < F) w = load_win(p0, len, cur, lane);
+        if (cur + 4 <= len && f + 1 < F) w = load_win<M>(p0, len, cur, lane);
         if (copy) {
-            const uint8_t *src = p0 + src_off;
+            typename M::u8 *src = p0 + src_off;
             const uint32_t Pm = r.payload_md, L = r.payload_avail;
             for (uint32_t i = L + lane; i < r.payload_len; i += 64) dst[Pm + i] = 0; /* cut-short final frame */
             const uint32_t h = min((4u - (Pm & 3u)) & 3u, L);     /* head bytes up to an aligned word */
@@ -365,16 +386,16 @@ __device__ __forceinline__ void demux_stream(const uint8_t *__restrict__ in, con
              * load of the payload is in flight before the first store waits */
             /* (unconditional: lanes without an edge byte re-read the frame's
              * first header byte, which is always in the stream) */
-            const uint8_t *hb0 = p0 + frame_at;
+            typename M::u8 *hb0 = p0 + frame_at;
             const uint8_t hbv = *((uint32_t)lane < h ? src + lane : hb0);
             const uint8_t tbv = *((uint32_t)lane < L - t0 ? src + t0 + lane : hb0);
             if (wb < we) {
                 /* pointer arithmetic, not an integer round trip: the loads
                  * stay global_load (a flat load waits on lgkmcnt too) */
-                const uint8_t *sb = src + (4u * wb - Pm);
+                typename M::u8 *sb = src + (4u * wb - Pm);
                 const uint32_t mis = (uint32_t)((uintptr_t)sb & 3u);
                 const uint32_t sh = mis * 8u;
-                const uint32_t *swd = (const uint32_t *)(sb - mis);
+                typename M::u32 *swd = (typename M::u32 *)(sb - mis);
                 /* all words in flight before the first store (straight-line,
                  * so no loop-header wait drains them early): one load latency
                  * per frame instead of one per 64-word round; the next header
@@ -426,7 +447,12 @@ __device__ __forceinline__ void demux_stream(const uint8_t *__restrict__ in, con
 /* this translation unit's copies of the demux constants */
 static inline hipError_t upload_demux_tables(const uint16_t *frame_bytes) {
     hipError_t e;
-    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_frame_bytes), frame_bytes, sizeof(uint16_t) * 9 * 16))) return e;
+    uint32_t fw[9][16];
+    for (int sr = 0; sr < 9; sr++)
+        for (int bi = 0; bi < 16; bi++)
+            fw[sr][bi] = frame_bytes[16 * sr + bi] |
+                         (uint32_t)(bi < 15 ? (sr < 3 ? MP3D_BITRATE_L3[bi] : MP3D_BITRATE_L3_LSF[bi]) : 0) << 16;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_frame_word), fw, sizeof(fw)))) return e;
     /* x^(8 j) mod P and 0xFFFF x^(8 n) mod P, P = x^16 + x^15 + x^2 + 1 */
     uint32_t pw[40], in[40];
     auto mulx = [](uint32_t c) { return (c & 0x8000u) ? ((c << 1) ^ 0x8005u) & 0xFFFFu : (c << 1) & 0xFFFFu; };

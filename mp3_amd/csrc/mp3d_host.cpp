@@ -1078,8 +1078,8 @@ done:
  * zero-padded to a fixed MP3D_PF_BYTES, which keeps the batch geometry
  * constant (uploaded once) across calls. */
 #define MP3D_PF_BYTES 4096
-#define MP3D_PF_READAHEAD 16 /* frames per read-ahead by default */
-#define MP3D_PF_RA_SEG 2     /* synthesis segment (frames) of a read-ahead */
+#define MP3D_PF_READAHEAD 32 /* frames per read-ahead by default */
+#define MP3D_PF_RA_SEG 1     /* synthesis segment (frames) of a read-ahead */
 struct mp3d_dec {
     mp3d_batch *b = nullptr;
     long frames = 0;
@@ -1107,7 +1107,10 @@ struct mp3d_dec {
      * frames already served are decoded again (exact), then the call runs
      * normally.  MP3D_PF_READAHEAD = frames per read-ahead (0 / 1: off). */
     int ra_max = 0;
-    uint8_t *ra_in = nullptr, *ra_in_m = nullptr;          /* frames back to back (pinned, mapped) */
+    int ra_seg = MP3D_PF_RA_SEG; /* MP3D_PF_RA_SEG env: synthesis segment of a read-ahead */
+    uint8_t *ra_in = nullptr;                              /* frames back to back (pinned)         */
+    uint8_t *ra_dev = nullptr;                             /* their device copy (one DMA): the
+                                                            * demux then reads HBM, not PCIe       */
     void *ra_pcm = nullptr, *ra_pcm_m = nullptr;           /* [ra_max][2304] f32-sized slots       */
     mp3d_frame_info *ra_inf = nullptr, *ra_inf_m = nullptr;
     StreamState *snap = nullptr;                           /* device: the state before the read-ahead */
@@ -1129,6 +1132,7 @@ static void dec_free(mp3d_dec *d) {
     if (d->h_info) (void)hipHostFree(d->h_info);
     if (d->h_done) (void)hipHostFree(d->h_done);
     if (d->ra_in) (void)hipHostFree(d->ra_in);
+    if (d->ra_dev) (void)hipFree(d->ra_dev);
     if (d->ra_pcm) (void)hipHostFree(d->ra_pcm);
     if (d->ra_inf) (void)hipHostFree(d->ra_inf);
     if (d->snap) (void)hipFree(d->snap);
@@ -1143,6 +1147,8 @@ extern "C" int mp3d_dec_create_on(int device, mp3d_dec **out) {
     {
         const char *e = getenv("MP3D_PF_READAHEAD");
         d->ra_max = e ? std::max(0, std::min(64, atoi(e))) : MP3D_PF_READAHEAD;
+        const char *g = getenv("MP3D_PF_RA_SEG");
+        if (g) d->ra_seg = std::max(1, atoi(g));
         if (d->ra_max < 2) d->ra_max = 0;
     }
     int r = mp3d_batch_create(device, 1, std::max(1, d->ra_max), &d->b);
@@ -1178,11 +1184,11 @@ extern "C" int mp3d_dec_create_on(int device, mp3d_dec **out) {
     }
     if (d->ra_max && d->m_in) {
         const size_t K = (size_t)d->ra_max;
-        if (hipHostMalloc((void **)&d->ra_in, K * MP3D_MAX_FRAME_BYTES + 64, hipHostMallocMapped) != hipSuccess ||
+        if (hipHostMalloc((void **)&d->ra_in, K * MP3D_MAX_FRAME_BYTES + 64) != hipSuccess ||
+            hipMalloc((void **)&d->ra_dev, K * MP3D_MAX_FRAME_BYTES + 64) != hipSuccess ||
             hipHostMalloc(&d->ra_pcm, K * 2304 * sizeof(float), co) != hipSuccess ||
             hipHostMalloc((void **)&d->ra_inf, K * sizeof(mp3d_frame_info), co) != hipSuccess ||
             hipMalloc((void **)&d->snap, sizeof(StreamState)) != hipSuccess ||
-            hipHostGetDevicePointer((void **)&d->ra_in_m, d->ra_in, 0) != hipSuccess ||
             hipHostGetDevicePointer(&d->ra_pcm_m, d->ra_pcm, 0) != hipSuccess ||
             hipHostGetDevicePointer((void **)&d->ra_inf_m, d->ra_inf, 0) != hipSuccess) {
             dec_free(d);
@@ -1288,8 +1294,8 @@ static int ra_settle(mp3d_dec *d) {
     if (served) {
         const uint64_t off = 0;
         const uint32_t len = d->ra[served - 1].off + d->ra[served - 1].len;
-        r = batch_decode(b, d->ra_in_m, &off, &len, 1, (int)served, d->ra_pcm_m, d->ra_f32, d->ra_inf_m, nullptr, true,
-                         3, true, MP3D_PF_RA_SEG);
+        r = batch_decode(b, d->ra_dev, &off, &len, 1, (int)served, d->ra_pcm_m, d->ra_f32, d->ra_inf_m, nullptr, true,
+                         3, true, d->ra_seg);
         if (r) return r;
     } else {
         HIPCHK(hipStreamSynchronize(b->own));
@@ -1328,12 +1334,13 @@ static int ra_fill(mp3d_dec *d, const uint8_t *buf, size_t bytes, bool f32) {
     int r = own_after_last(b);
     if (!r) r = flush_tail(b, b->own);
     if (r) return r;
-    /* the state before the read-ahead, for ra_settle */
+    /* the state before the read-ahead, for ra_settle; the frames to HBM */
     HIPCHK(hipMemcpyAsync(d->snap, b->st, sizeof(StreamState), hipMemcpyDeviceToDevice, b->own));
     memset(d->ra_in + o, 0, 64);
+    HIPCHK(hipMemcpyAsync(d->ra_dev, d->ra_in, o + 64, hipMemcpyHostToDevice, b->own));
     const uint64_t off = 0;
-    r = batch_decode(b, d->ra_in_m, &off, &o, 1, (int)ents.size(), d->ra_pcm_m, f32, d->ra_inf_m, nullptr, true, kinds,
-                     true, MP3D_PF_RA_SEG);
+    r = batch_decode(b, d->ra_dev, &off, &o, 1, (int)ents.size(), d->ra_pcm_m, f32, d->ra_inf_m, nullptr, true, kinds,
+                     true, d->ra_seg);
     if (r) return r;
     d->ra.swap(ents);
     d->ra_next = 0;

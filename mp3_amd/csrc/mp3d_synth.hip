@@ -1254,7 +1254,8 @@ __global__ void __launch_bounds__(256) k_frame(const uint8_t *__restrict__ in_ho
 #pragma unroll
         for (int k = 0; k < 4; k++) ((uint4 *)s_in)[lane + 64 * k] = k < 2 ? v[k] : make_uint4(0u, 0u, 0u, 0u);
         wave_sync();
-        demux_stream((const uint8_t *)s_in, in_off, in_len, md, md_off, st, rec, sideu, infos, 1, opts, 0, lane);
+        demux_stream<SrcLds>((SrcLds::u8 *)(uintptr_t)s_in + in_off[0], in_off[0], in_len[0], md, md_off, st, rec, sideu,
+                             infos, 1, opts, 0, lane);
     } else {
         /* waves 1..3 meanwhile: the Huffman and synthesis tables */
         huff_tables<192>(tab, s_lut, s_tsel, s_lbnd, s_slen, tid - 64);
