@@ -155,7 +155,9 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                     if (r.lsf) {
                         /* off the MPEG-1 path: a call keeps its registers out of
                          * the kernel's allocation; bits passed as an LDS pointer */
-                        pos = read_sf_lsf((lds_cu32)bits, pos, side, (uint8_t *)&meta[u], &lsf_pre);
+                        const uint32_t pp = read_sf_lsf((lds_cu32)bits, pos, side, (uint8_t *)&meta[u]);
+                        pos = pp & 0x7FFFFFFFu;
+                        lsf_pre = (int)(pp >> 31);
                     } else {
                         uint32_t sfw[10];
 #pragma unroll

@@ -169,10 +169,13 @@ __device__ __forceinline__ uint32_t read_sf_lsf_i(lds_cu32 bits, uint32_t pos, u
 }
 /* k_huffman's call: out of line, so its registers stay out of the kernel's
  * allocation (the one-wave-per-unit decode inlines read_sf_lsf_i: no call,
- * no stack) */
-__device__ __attribute__((noinline)) uint32_t read_sf_lsf(lds_cu32 bits, uint32_t pos, uint64_t side, uint8_t *sf,
-                                                          int *preflag) {
-    return read_sf_lsf_i(bits, pos, side, sf, preflag);
+ * no stack).  Returns pos | preflag << 31 (pos < 2^31): a preflag returned
+ * through a pointer lived in scratch, and reloading it at the UnitMeta store
+ * waited for vmcnt(0) -- for every is[] row store of the round. */
+__device__ __attribute__((noinline)) uint32_t read_sf_lsf(lds_cu32 bits, uint32_t pos, uint64_t side, uint8_t *sf) {
+    int pre;
+    const uint32_t p = read_sf_lsf_i(bits, pos, side, sf, &pre);
+    return p | (uint32_t)pre << 31;
 }
 
 /* the block's LDS tables: the LUT (the whole array: past the last table it
