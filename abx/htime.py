@@ -35,6 +35,8 @@ def main():
         ("                    k = bv2;\n", "                    tx_ = %s; ht_[4] += tx_ - tm_; tm_ = tx_;\n                    k = bv2;\n" % T, 1),
         ("                    const int nz_end = k;\n",
          "                    tx_ = %s; ht_[5] += tx_ - tm_; tm_ = tx_;\n                    const int nz_end = k;\n" % T, 1),
+        ("                    /* everything after sf[40]: one 16-B store */\n",
+         "                    tx_ = %s; ht_[7] += tx_ - tm_; tm_ = tx_;\n                    /* everything after sf[40]: one 16-B store */\n" % T, 1),
         ("                pending = pending && !inb;\n",
          "                tx_ = %s; ht_[6] += tx_ - tm_;\n                pending = pending && !inb;\n" % T, 1),
         ("    }\n}\n\n/* k_huffman_wave",

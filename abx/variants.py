@@ -144,6 +144,16 @@ VARS = {
              "    const uint32_t ln = " + LID + "; (void)w;\n    const uint32_t w0 = bits[ln], w1 = bits[ln + 64];")],
     "LUT0": [("const uint32_t e1 = s_lut[i1];", "const uint32_t e1 = s_lut[(i1 & ~63u) + (uint32_t)lane];"),
              ("const uint32_t e = s_lut[i2];", "const uint32_t e = s_lut[(i2 & ~63u) + (uint32_t)lane];")],
+    # k_huffman row stores: suppressed (compute kept) / coalesced into one
+    # contiguous 1 KB per wave instruction (output wrong; timing only)
+    "NS1": [("                        *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);",
+             "                        if ((wv[0] ^ wv[1] ^ wv[2] ^ wv[3]) == 0x9E3779B9u) *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);"),
+            ("                        *(uint2 *)(row + k) = make_uint2(",
+             "                        if (((uint32_t)q0 ^ (uint32_t)q3) == 0x9E3779B9u) *(uint2 *)(row + k) = make_uint2(")],
+    "CS1": [("                        *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);",
+             "                        *(uint4 *)(is_buf + (size_t)(ubase + 64 * rd) * 576 + 32 * k + 8 * lane) = make_uint4(wv[0], wv[1], wv[2], wv[3]);"),
+            ("                        *(uint2 *)(row + k) = make_uint2(",
+             "                        *(uint2 *)(is_buf + (size_t)(ubase + 64 * rd) * 576 + 32 * k + 4 * lane) = make_uint2(")],
     "BASE": [],
     "XPF4": [],
     "DM2": [],

@@ -37,8 +37,8 @@ def main():
     dec.decode(d_in, offs, sizes, F, pcm=pcm)
     torch.cuda.synchronize()
     assert L.mp3d_dbg_ptime(out.ctypes.data) == 0
-    names = ["rank", "round", "stage", "scalefactors", "big_values", "count1", "meta"]
-    tot = float(out[:7].sum())
+    names = ["rank", "round", "stage", "scalefactors", "big_values", "count1", "meta_store", "meta_build"]
+    tot = float(out[:8].sum())
     units = n * F * 4
     print(json.dumps({"fraction": {k: round(float(out[i]) / tot, 3) for i, k in enumerate(names)},
                       "cycles_per_unit_per_wave": {k: round(float(out[i]) / units, 1) for i, k in enumerate(names)},
