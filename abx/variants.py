@@ -155,6 +155,12 @@ VARS = {
             ("                        *(uint2 *)(row + k) = make_uint2(",
              "                        *(uint2 *)(is_buf + (size_t)(ubase + 64 * rd) * 576 + 32 * k + 4 * lane) = make_uint2(")],
     "BASE": [],
+    # r03: lane_sel as a plain select of t (wrong for mono frames; C3 is all stereo): what the history and
+    # overlap selects cost (NOSEL)
+    "NOSEL": [("""    __asm__("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+    return r;""", """    (void)m; (void)f; r = t;
+    return r;""")],
+    "S2": [],
     "XPF4": [],
     "DM2": [],
     "H2": [],

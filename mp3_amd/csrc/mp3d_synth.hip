@@ -810,6 +810,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
             }
             const int bt = ch ? bt1 : bt0, mixed = ch ? mx1 : mx0;
             float o18[18];
+            f32x2 nvp[9]; /* the next overlap (folded sign convention) */
             {
                 const int base = ch * 576 + 18 * sb;
                 float x[18], up[8], dn[8];
@@ -859,9 +860,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                         const f32x2 o = pfma(bc(W[8 - i].y), (f32x2){q.x, q.y}, ovp[i]);
                         o18[i] = o.x;
                         o18[17 - i] = o.y;
-                        const f32x2 nv = bc(W[8 - i].x) * (f32x2){q.z, q.w};
-                        ovp[i].x = lane_sel(amask, ovp[i].x, nv.x);
-                        ovp[i].y = lane_sel(amask, ovp[i].y, nv.y);
+                        nvp[i] = bc(W[8 - i].x) * (f32x2){q.z, q.w};
                     }
                 } else {
                     /* z[6w+6+i] += y_w[i] * win12[i], w = 0..2, i = 0..11 */
@@ -897,10 +896,20 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
 #pragma unroll
                     for (int i = 0; i < 18; i++) o18[i] = ((i < 6 ? 0.f : z[i - 6]) + ovt[i]) * ((i & 1) ? sgo : 1.f);
 #pragma unroll
+                    for (int i = 0; i < 9; i++)
+                        nvp[i] = (f32x2){i < 12 ? z[12 + i] : 0.f, 17 - i < 12 ? z[29 - i] : 0.f} * sgp[i & 1];
+                }
+                /* overlap update: a mono frame's channel-1 lanes keep theirs
+                 * (a per-lane select, on mono frames only: on the stereo
+                 * path the select kept register copies alive) */
+                if (nch == 2) {
+#pragma unroll
+                    for (int i = 0; i < 9; i++) ovp[i] = nvp[i];
+                } else {
+#pragma unroll
                     for (int i = 0; i < 9; i++) {
-                        const f32x2 n = (f32x2){i < 12 ? z[12 + i] : 0.f, 17 - i < 12 ? z[29 - i] : 0.f} * sgp[i & 1];
-                        ovp[i].x = lane_sel(amask, ovp[i].x, n.x);
-                        ovp[i].y = lane_sel(amask, ovp[i].y, n.y);
+                        ovp[i].x = lane_sel(amask, ovp[i].x, nvp[i].x);
+                        ovp[i].y = lane_sel(amask, ovp[i].y, nvp[i].y);
                     }
                 }
             }
@@ -914,7 +923,9 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
             }
             wave_sync(); /* every lane has read its xr before S overwrites it */
             {
-                const int sw = opaque(18 * ch * SROW + sb);
+                /* S row layout: subbands 0..15, then 31 down to 16, so the
+                 * matrixing's mirror run S[31 - i] is in register order */
+                const int sw = opaque(18 * ch * SROW + (sb < 16 ? sb : 47 - sb));
 #pragma unroll
                 for (int t = 0; t < 18; t++) sBuf[sw + t * SROW] = o18[t]; /* frequency inversion already in */
             }
@@ -926,7 +937,8 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
              * = two 16x16 products: half the MFMAs of the dense 32x32.
              * v_mfma_f32_16x16x4_f32, rows m, cols n = (ch, t), K order
              * i = 4 q + ks (q = lane >> 4): a lane's 4 B values and their
-             * mirrors are two 16-B runs of an S row. */
+             * mirrors are two 16-B runs of an S row (the mirror run stored
+             * reversed by phase I), so the butterfly is 2 + 2 packed ops. */
             {
                 const int q = lane >> 4, r16 = lane & 15;
                 const float4 ae = *(const float4 *)&T.ce[r16][4 * q];
@@ -937,14 +949,12 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                 for (int nt = 0; nt < 3; nt++) {
                     int n = 16 * nt + r16;
                     n = n < 36 ? n : 35;
-                    const float4 a4 = *(const float4 *)&sBuf[n * SROW + 4 * q];
-                    const float4 b4 = *(const float4 *)&sBuf[n * SROW + 28 - 4 * q]; /* S[31-i] = b4[3-ks] */
-                    const float av[4] = {a4.x, a4.y, a4.z, a4.w}, bv[4] = {b4.w, b4.z, b4.y, b4.x};
-#pragma unroll
-                    for (int ks = 0; ks < 4; ks++) {
-                        Be[nt][ks] = av[ks] + bv[ks];
-                        Bo[nt][ks] = av[ks] - bv[ks];
-                    }
+                    const f32x4 a4 = *(const f32x4 *)&sBuf[n * SROW + 4 * q];
+                    const f32x4 b4 = *(const f32x4 *)&sBuf[n * SROW + 16 + 4 * q]; /* S[31 - 4 q - ks] */
+                    const f32x2 e01 = pfma(bc(1.f), a4.xy, b4.xy), e23 = pfma(bc(1.f), a4.zw, b4.zw);
+                    const f32x2 o01 = pfma(bc(-1.f), b4.xy, a4.xy), o23 = pfma(bc(-1.f), b4.zw, a4.zw);
+                    Be[nt][0] = e01.x; Be[nt][1] = e01.y; Be[nt][2] = e23.x; Be[nt][3] = e23.y;
+                    Bo[nt][0] = o01.x; Bo[nt][1] = o01.y; Bo[nt][2] = o23.x; Bo[nt][3] = o23.y;
                 }
                 f32x4 ce[3], co[3];
 #pragma unroll
@@ -995,6 +1005,22 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                 /* X index k sits at (k & 1) 16 + k / 2 of its row */
                 const int pa = opaque(18 * ch * XROW + (wa & 1) * 16 + (wa >> 1));
                 const int pb = opaque(18 * ch * XROW + (wb & 1) * 16 + (wb >> 1));
+                if (nch == 1) {
+                    /* mono frame: channel 1 keeps its synthesis history.  Its
+                     * lanes put the history back into the X slots it came from
+                     * (ha[k] = row k + 4 at wa, hb[k] = row k + 3 at wb; lanes
+                     * sharing a slot write the same value), so the plain
+                     * update below reloads it: no per-lane select on the
+                     * stereo path (a select there kept ~30 register copies
+                     * per granule alive: -45 VALU / granule, A/B NOSEL) */
+                    if (ch == 1) {
+#pragma unroll
+                        for (int k = 0; k < 14; k++) sBuf[pa + (k + 4) * XROW] = ha[k];
+#pragma unroll
+                        for (int k = 0; k < 15; k++) sBuf[pb + (k + 3) * XROW] = hb[k];
+                    }
+                    wave_sync();
+                }
 #pragma unroll
                 for (int t = 0; t < 18; t++) {
                     xa[t] = sBuf[pa + t * XROW];
@@ -1090,9 +1116,9 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                     }
                 }
 #pragma unroll
-                for (int k = 0; k < 14; k++) ha[k] = lane_sel(amask, ha[k], xa[k + 4]);
+                for (int k = 0; k < 14; k++) ha[k] = xa[k + 4]; /* mono: channel 1 reloaded its own (above) */
 #pragma unroll
-                for (int k = 0; k < 15; k++) hb[k] = lane_sel(amask, hb[k], xb[k + 3]);
+                for (int k = 0; k < 15; k++) hb[k] = xb[k + 3];
                 if (PF == 1) {
 #pragma unroll
                     for (int k = 0; k < 14; k++) xch[(18 + k) * 64 + lane] = ha[k];
