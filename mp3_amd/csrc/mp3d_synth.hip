@@ -662,6 +662,8 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                  * short band width is even, tests/test_tables.py): one scale
                  * read per pair. */
                 uint32_t bigacc = 0u;
+                uint32_t k1024 = 1024u; /* in an SGPR (a literal is not a VOP3P operand here) */
+                __asm__ volatile("" : "+s"(k1024));
                 const uint32_t sc_base[2] = {(uint32_t)(uintptr_t)(lds_cf32 *)&Wd.scale[0][0],
                                              (uint32_t)(uintptr_t)(lds_cf32 *)&Wd.scale[1][0]};
 #pragma unroll
@@ -670,10 +672,12 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                     const bool ok = i < 4 || lane < 32;
 #pragma unroll
                     for (int c = 0; c < 2; c++) {
-                        const uint32_t tv2 = ok ? lpair[var[c]][l0 >> 1] : 0u;
+                        const uint32_t tv2 = ok ? lpair[var[c]][lane + 64 * i] : 0u;
                         /* lines >= nz_end arrive as 0 (load_is_masked) */
-                        const uint32_t t = __builtin_bit_cast(
-                            uint32_t, (__builtin_bit_cast(u16x2, cis[c][i]) << (uint16_t)2) + (u16x2){1024, 1024});
+                        /* one v_pk_mad_u16: 4 v + 1024 in both halves (as C the
+                         * compiler emitted a packed shift and a packed add) */
+                        uint32_t t;
+                        __asm__("v_pk_mad_u16 %0, %1, 4, %2 op_sel_hi:[1,0,0]" : "=v"(t) : "v"(cis[c][i]), "s"(k1024));
                         bigacc |= t;
                         const float sc = *(lds_cf32 *)(uintptr_t)(sc_base[c] | (tv2 & 0xFCu));
                         const uint8_t *p43b = (const uint8_t *)T.p43s;
@@ -695,7 +699,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                                 const int v = (int)(int16_t)(e ? (cis[c][i] >> 16) : (cis[c][i] & 0xFFFFu));
                                 const int a = v < 0 ? -v : v;
                                 if ((uint32_t)(v + 256) >= 512u) {
-                                    const uint32_t tv2 = lpair[var[c]][l0 >> 1];
+                                    const uint32_t tv2 = lpair[var[c]][lane + 64 * i];
                                     const float mag = pow43_big(a) * Wd.scale[c][(tv2 >> 2) & 63u];
                                     XV(c, 2 * i + e) = v < 0 ? -mag : mag;
                                 }
@@ -720,7 +724,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
 #pragma unroll
                     for (int i = 0; i < 5; i++) {
                         const int l0 = 2 * lane + 128 * i;
-                        const uint32_t tv2 = (i < 4 || lane < 32) ? lpair[var[1]][l0 >> 1] : 0u;
+                        const uint32_t tv2 = (i < 4 || lane < 32) ? lpair[var[1]][lane + 64 * i] : 0u;
                         if (fmaxf(fabsf(XV(1, 2 * i)), fabsf(XV(1, 2 * i + 1))) >= FLUSH)
                             nzR |= 1ull << ((tv2 >> 2) & 63u);
                     }
@@ -753,7 +757,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
 #pragma unroll
                     for (int i = 0; i < 5; i++) {
                         const int l0 = 2 * lane + 128 * i;
-                        const uint32_t tv2 = (i < 4 || lane < 32) ? lpair[var[1]][l0 >> 1] : 0u;
+                        const uint32_t tv2 = (i < 4 || lane < 32) ? lpair[var[1]][lane + 64 * i] : 0u;
                         const int ipl = Wd.is[(tv2 >> 2) & 63u];
 #pragma unroll
                         for (int e = 0; e < 2; e++) {
@@ -790,7 +794,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                                 if (var[c] == 0) { /* long block: in place, one 8-B store */
                                     *(f32x2 *)&sBuf[576 * c + l0] = xp[c][i];
                                 } else {
-                                    const uint32_t tv2 = lpair[var[c]][l0 >> 1];
+                                    const uint32_t tv2 = lpair[var[c]][lane + 64 * i];
                                     sBuf[576 * c + ((tv2 >> 8) & 1023u)] = XV(c, 2 * i);
                                     sBuf[576 * c + ((tv2 >> 18) & 1023u)] = XV(c, 2 * i + 1);
                                 }
@@ -838,7 +842,9 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                  * conditional stores the compiler built a divergent branch
                  * plus ~50 register copies around it */
                 /* scalar: as packed pairs the operands need a register move
-                 * each (they arrive as consecutive pairs from LDS) */
+                 * each (they arrive as consecutive pairs from LDS; r03 AL1:
+                 * with op_sel swizzles and LDS coefficient pairs -8 VALU but
+                 * +3 VGPRs, 168 of 168) */
 #pragma unroll
                 for (int k = 0; k < 8; k++) {
                     const float lo = x[17 - k], hi = x[k];
