@@ -772,35 +772,38 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                             }
                         }
                     }
-                } else if (ms_fold) {
-#pragma unroll
-                    for (int k = 0; k < 10; k++) {
-                        const float lv = XV(0, k), rv = XV(1, k);
-                        XV(0, k) = lv + rv;
-                        XV(1, k) = lv - rv;
-                    }
                 }
                 /* the next granule's loads fly during phases I, M, W (issued
                  * after cis is consumed: fewer live registers in phase Q) */
                 if (PF == 0 && (LSF ? f + 1 < f1 : (gr == 0 || f + 1 < f1))) prefetch(LSF ? 2 * f + 2 : 2 * f + gr + 1, cs);
-                /* scatter in (short-block reordered) position */
-#pragma unroll
-                for (int i = 0; i < 5; i++) {
-                    if (i < 4 || lane < 32) {
-                        const int l0 = 2 * lane + 128 * i;
-#pragma unroll
-                        for (int c = 0; c < 2; c++) {
-                            if (c < nch) {
-                                if (var[c] == 0) { /* long block: in place, one 8-B store */
-                                    *(f32x2 *)&sBuf[576 * c + l0] = xp[c][i];
-                                } else {
-                                    const uint32_t tv2 = lpair[var[c]][lane + 64 * i];
-                                    sBuf[576 * c + ((tv2 >> 8) & 1023u)] = XV(c, 2 * i);
-                                    sBuf[576 * c + ((tv2 >> 18) & 1023u)] = XV(c, 2 * i + 1);
-                                }
-                            }
-                        }
+                /* scatter in (short-block reordered) position; M/S-only frames
+                 * store (L + R, L - R) from their own copy of the loop (as an
+                 * in-place update before one scatter, the branch merge cost a
+                 * register copy per line pair) */
+                auto scatter = [&](int i, int c, f32x2 v) {
+                    if (var[c] == 0) { /* long block: in place, one 8-B store */
+                        *(f32x2 *)&sBuf[576 * c + 2 * lane + 128 * i] = v;
+                    } else {
+                        const uint32_t tv2 = lpair[var[c]][lane + 64 * i];
+                        sBuf[576 * c + ((tv2 >> 8) & 1023u)] = v.x;
+                        sBuf[576 * c + ((tv2 >> 18) & 1023u)] = v.y;
                     }
+                };
+                if (ms_fold) {
+#pragma unroll
+                    for (int i = 0; i < 5; i++)
+                        if (i < 4 || lane < 32) {
+                            scatter(i, 0, xp[0][i] + xp[1][i]);
+                            scatter(i, 1, xp[0][i] - xp[1][i]);
+                        }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 5; i++)
+                        if (i < 4 || lane < 32) {
+#pragma unroll
+                            for (int c = 0; c < 2; c++)
+                                if (c < nch) scatter(i, c, xp[c][i]);
+                        }
                 }
             }
             wave_sync();
@@ -1061,10 +1064,16 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                     }
                 }
                 auto out2 = [&](int tp) { return acc[tp]; };
-                auto to_pcm = [&](float v) {
-                    const float p = rintf(v); /* taps pre-scaled by 32768 */
-                    return (int)fminf(fmaxf(p, -32768.f), 32767.f);
+                /* int16 sinks (taps pre-scaled by 32768): clamp(floor(x + 0.5)),
+                 * FFmpeg's fixed-point rounding (round_sample: add half, shift),
+                 * by one v_cvt_rpi_i32_f32 per sample: floor of the exact x + 0.5,
+                 * saturating to int32 (tools/dbg/cvt_probe.hip) */
+                auto to_i32 = [&](float v) {
+                    int r;
+                    __asm__("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(v));
+                    return r;
                 };
+                auto to_pcm = [&](float v) { return min(max(to_i32(v), -32768), 32767); }; /* v_med3_i32 */
                 const int so = f * 2304 * PB + gr * 576 * nch * PB;
                 if (f < f0) {
                     /* warm-up frame: state only, no PCM */
@@ -1093,14 +1102,8 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                     }
                 } else if (nch == 2) {
                     const int vo = opaque((sb + 32 * ch) * 4);
-                    /* rint(x 32768) -> int32 (v_cvt_i32_f32 saturates out-of-range
-                     * floats), then v_cvt_pk_i16_i32 saturates to int16 and packs
-                     * (L, R): clamp(rint(x 32768)) as before, 2 VALU less per pair */
-                    auto to_i32 = [&](float v) {
-                        int r;
-                        __asm__("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(rintf(v))); /* taps x 32768 */
-                        return r;
-                    };
+                    /* floor(x + 0.5) -> int32, then v_cvt_pk_i16_i32 saturates to
+                     * int16 and packs (L, R): 4 VALU per slot pair */
 #pragma unroll
                     for (int tp = 0; tp < 9; tp++) {
                         const f32x2 o = out2(tp);

@@ -22,7 +22,9 @@ def names():
 
 
 def to_int16(x):
-    return np.clip(np.rint(np.asarray(x, np.float64) * 32768.0), -32768, 32767).astype(np.int16)
+    """clamp(floor(x 32768 + 0.5)): the decoder's int16 rounding (k_synth's
+    v_cvt_rpi_i32_f32; FFmpeg's fixed-point round_sample adds half and shifts)."""
+    return np.clip(np.floor(np.asarray(x, np.float64) * 32768.0 + 0.5), -32768, 32767).astype(np.int16)
 
 
 def compare(name, ours, ref):

@@ -96,7 +96,7 @@ def test_c2_state_tails_across_calls():
 
 def test_clipping_saturates_like_the_oracle():
     """Spectra scaled far past full scale: int16 PCM saturates to -32768 / 32767
-    exactly where the oracle's clamp(rint(x 32768)) does (the decode paths
+    exactly where the oracle's clamp(floor(x 32768 + 0.5)) does (the decode paths
     convert with saturating int32 / packed-int16 conversions)."""
     n, F = 8, 6
     xr, bt, mx = _gen.c2_spectra(n, F, NCH, seed=99)

@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 import _gen
+import _golden
 import _oracle
 import mp3_amd
 from test_oracle import CRC_CFG, _corrupt_crc
@@ -37,7 +38,7 @@ def test_batch_crc_option_vs_oracle(opts):
     for s, data in enumerate(streams):
         ref = _oracle.decode_stream(data, opts=opts)[0]
         got = mp3_amd.pcm_to_planar(pcm[s], infos[s])
-        o = np.clip(np.rint(ref.astype(np.float64) * 32768), -32768, 32767).astype(np.int16)
+        o = _golden.to_int16(ref)
         assert got.shape == o.shape, (s, opts, got.shape, o.shape)
         assert np.abs(got.astype(np.int32) - o.astype(np.int32)).max() <= 1, (s, opts)
         dropped = int((infos[s]["samples"] == 0).sum())

@@ -1,7 +1,7 @@
 """Float32 PCM sink (mp3d_batch_decode_f32 / mp3d_decode_frame_f32, SURVEY.md
 §8(f) row 3): the same synthesis sums as the int16 sink, unscaled and
 unclipped (FFmpeg's float decoder convention).  Checked (1) exactly against
-the int16 sink (int16 == clamp(rint(f32 * 32768)) bit for bit), (2) against
+the int16 sink (int16 == clamp(floor(f32 * 32768 + 0.5)) bit for bit), (2) against
 the double-precision oracle within 2^-15 (the ±1 LSB north_star tolerance,
 stated on the float scale) and (3) per-frame vs batch API."""
 import numpy as np
@@ -28,7 +28,7 @@ def test_f32_sink_vs_int16_and_oracle(name):
     assert p32.dtype == np.float32 and np.array_equal(i16, i32)
     g16 = mp3_amd.pcm_to_planar(p16[0], i16[0])
     g32 = mp3_amd.pcm_to_planar(p32[0], i32[0])
-    assert np.array_equal(np.clip(np.rint(g32.astype(np.float64) * 32768), -32768, 32767).astype(np.int16), g16)
+    assert np.array_equal(_golden.to_int16(g32), g16)
     o, _ = _oracle.decode_stream(data)
     assert o.shape == g32.shape
     d = np.abs(g32.astype(np.float64) - o)
