@@ -161,6 +161,37 @@ VARS = {
     return r;""", """    (void)m; (void)f; r = t;
     return r;""")],
     "S2": [],
+    # r03: the count1 sign table with the store in the same iteration (no software pipelining)
+    "S13": [("""                    int kp = -1;
+                    uint32_t sp = 0u;
+                    while (k <= 572 && pos < end_bit) {
+                        const uint32_t hw = win32g(bits, pos);
+                        const uint32_t e = s_lut[c1base + (hw >> c1sh)];
+                        if (kp >= 0) c1_store(kp, sp);
+                        kp = -1;""", """                    int kp = -1;
+                    uint32_t sp = 0u;
+                    while (k <= 572 && pos < end_bit) {
+                        const uint32_t hw = win32g(bits, pos);
+                        const uint32_t e = s_lut[c1base + (hw >> c1sh)];"""),
+            ("""                        sp = s_c1s[(v << 4) | ((hw << lq) >> 28)];
+                        kp = k;""", """                        sp = s_c1s[(v << 4) | ((hw << lq) >> 28)];
+                        c1_store(k, sp);"""),
+            ("""                    if (kp >= 0) c1_store(kp, sp);""", """                    (void)kp;""")],
+    # r03: without the two phase-Q tweaks (lane / MW test, M/S factor multiply) of QT1
+    "S9": [("                if (lane < nch * MW) ((uint32_t *)&Wd.m[0])[lane] = wm[cs]; /* lane / MW < nch, no division */",
+            "                if (lane < 2 * MW && lane / MW < nch) ((uint32_t *)&Wd.m[0])[lane] = wm[cs];"),
+           ("""                const float msf = ms_fold ? isq : 1.f; /* uniform: one multiply, no select */
+                auto p2q = [&](int q) { return ldexpf(T.p2q[q & 3], q >> 2) * msf; };""",
+            """                auto p2q = [&](int q) {
+                    const float v = ldexpf(T.p2q[q & 3], q >> 2);
+                    return ms_fold ? v * isq : v;
+                };""")],
+    # r03: is[] prefetch loads unconditional, masked by an out-of-range buffer offset (no exec branch per load)
+    "PB1": [("""                nis[c][i] = 0u;
+                if ((i < 4 || lane < 32) && 2 * lane + 128 * i < nz)
+                    nis[c][i] = __builtin_amdgcn_raw_buffer_load_b32(r_is, lo + c * 1152 + 256 * i, g * gb, 0);""",
+             """                const bool on = (i < 4 || lane < 32) && 2 * lane + 128 * i < nz;
+                nis[c][i] = __builtin_amdgcn_raw_buffer_load_b32(r_is, on ? lo + c * 1152 + 256 * i : 0x40000000, g * gb, 0);""")],
     "XPF4": [],
     "DM2": [],
     "H2": [],

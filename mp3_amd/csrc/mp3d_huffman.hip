@@ -21,7 +21,23 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
     __shared__ uint32_t s_tsel[32]; /* table_select -> LUT base | (32 - bits1) << 16 | linbits << 24 */
     __shared__ uint16_t s_lbnd[9][24]; /* long sfb start line per sample-rate index (23 bounds) */
     __shared__ uint8_t s_slen[32];     /* MPEG-1 slen1 | slen2 per scalefac_compress          */
+    /* count1 values with their signs, by (value bits v, the 4 bits after the
+     * code): signed bytes [q2, q0, q3, q1], so each 2 x int16 output word is
+     * one v_perm_b32 (sign-extension selectors read odd bytes only) */
+    __shared__ uint32_t s_c1s[256];
     huff_tables_lane(tab, s_lut, s_tsel, s_lbnd, s_slen);
+    {
+        const uint32_t v = threadIdx.x >> 4, s4 = threadIdx.x & 15u;
+        int q[4], j = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int bit = (int)(v >> (3 - i)) & 1;
+            q[i] = bit && ((s4 >> (3 - j)) & 1u) ? -1 : bit;
+            j += bit;
+        }
+        s_c1s[threadIdx.x] = (uint32_t)(uint8_t)q[2] | (uint32_t)(uint8_t)q[0] << 8 | (uint32_t)(uint8_t)q[3] << 16 |
+                             (uint32_t)(uint8_t)q[1] << 24;
+    }
     __syncthreads();
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t *bits = s_bits + 4 + wv * (HUFF_CAPW + 4);
@@ -258,27 +274,25 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                     /* table A or B (count1table_select) as one LUT read, no branch */
                     const bool c1b = (side >> 5) & 1;
                     const uint32_t c1base = c1b ? c1b_base : qbase, c1sh = c1b ? 28u : 32u - (uint32_t)qb1;
+                    /* (q0, q1) from bytes 1, 3 of se, (q2, q3) from bytes 5, 7 of
+                     * se << 8, each sign-extended to 16 bits (selectors 8..11) */
+                    auto c1_store = [&](int kq, uint32_t se) {
+                        *(uint2 *)(row + kq) = make_uint2(__builtin_amdgcn_perm(se, se, 0x09030801u),
+                                                          __builtin_amdgcn_perm(se << 8, se, 0x0B070A05u));
+                    };
+                    /* (its store waits for the s_c1s read; made one iteration
+                     * later instead, the time was the same: A/B C1P) */
                     while (k <= 572 && pos < end_bit) {
                         const uint32_t hw = win32g(bits, pos);
                         const uint32_t e = s_lut[c1base + (hw >> c1sh)];
                         const uint32_t v = e & 15u, lq = (e >> 8) & 31u;
                         const uint32_t ns = __builtin_popcount(v);
                         if (pos + lq + ns > end_bit) break;
-                        /* value i's sign bit follows the signs of the nonzero
-                         * values before it: offsets from the top of rb by
-                         * prefix counts of v (bit 3 = value 0); masks 0 / -1 */
-                        const uint32_t rb = hw << lq;
-                        const uint32_t p1 = v >> 3, p2 = __builtin_popcount(v >> 2), p3 = __builtin_popcount(v >> 1);
-                        const int m0 = __builtin_amdgcn_sbfe((int)rb, 31u, 1u);
-                        const int m1 = __builtin_amdgcn_sbfe((int)rb, 31u - p1, 1u);
-                        const int m2 = __builtin_amdgcn_sbfe((int)rb, 31u - p2, 1u);
-                        const int m3 = __builtin_amdgcn_sbfe((int)rb, 31u - p3, 1u);
-                        /* a zero value stays 0 whatever mask it meets */
-                        const int q0 = ((int)p1 ^ m0) - m0, q1 = ((int)((v >> 2) & 1u) ^ m1) - m1;
-                        const int q2 = ((int)((v >> 1) & 1u) ^ m2) - m2, q3 = ((int)(v & 1u) ^ m3) - m3;
+                        /* the signs follow the code, one per nonzero value in
+                         * order: the 4 bits after the code and v index the
+                         * signed values (s_c1s); off the pos chain */
+                        c1_store(k, s_c1s[(v << 4) | ((hw << lq) >> 28)]);
                         pos += lq + ns;
-                        *(uint2 *)(row + k) = make_uint2(__builtin_amdgcn_perm((uint32_t)q1, (uint32_t)q0, 0x05040100u),
-                                                         __builtin_amdgcn_perm((uint32_t)q3, (uint32_t)q2, 0x05040100u));
                         k += 4;
                     }
                     const int nz_end = k;

@@ -28,7 +28,7 @@ namespace mp3d {
 #define HUFF_ROUNDS 4                    /* 64-unit rounds per super-chunk          */
 #define HUFF_SUPER (64 * HUFF_ROUNDS)    /* units ranked together by big_values     */
 #define HUFF_BLOCK (64 * HUFF_WAVES)
-#define HUFF_CAPW 2400 /* LDS words per wave (9.6 KB): staging + round order    */
+#define HUFF_CAPW 2336 /* LDS words per wave (9.3 KB): staging + round order; 3 workgroups of 4 waves per CU with the count1 sign table */
 #define HUFF_STAGEW (HUFF_CAPW - HUFF_SUPER / 2) /* staging words; the u16 order follows */
 
 /* 32 bits of a staged (big-endian word) bitstream starting at bit pos (the

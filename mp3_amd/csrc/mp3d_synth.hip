@@ -590,7 +590,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                     for (int i = 0; i < 5; i++) cis[c][i] = nis[c][i];
                 /* UnitMeta into LDS for the (rare) intensity path; the common
                  * path reads the prefetched words straight from registers */
-                if (lane < 2 * MW && lane / MW < nch) ((uint32_t *)&Wd.m[0])[lane] = wm[cs];
+                if (lane < nch * MW) ((uint32_t *)&Wd.m[0])[lane] = wm[cs]; /* lane / MW < nch, no division */
                 /* words 10..12: gain, block type, mixed, scalefac_scale |
                  * preflag, sbg[3] | nz_end (UnitMeta layout) */
                 const uint32_t m10a = (uint32_t)__builtin_amdgcn_readlane((int)wm[cs], 10);
@@ -615,10 +615,8 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                 /* 2^(q/4) = ldexp(2^((q & 3) / 4), q >> 2): the mantissa from a
                  * 4-entry LDS table (as a select chain the compiler built
                  * divergent branches) */
-                auto p2q = [&](int q) {
-                    const float v = ldexpf(T.p2q[q & 3], q >> 2);
-                    return ms_fold ? v * isq : v;
-                };
+                const float msf = ms_fold ? isq : 1.f; /* uniform: one multiply, no select */
+                auto p2q = [&](int q) { return ldexpf(T.p2q[q & 3], q >> 2) * msf; };
                 if (var[0] == 0 && (nch == 1 || var[1] == 0)) {
                     /* long blocks in every coded channel (the common case): both
                      * channels' 22 band scales in one pass, lane = (ch, band) */
