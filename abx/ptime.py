@@ -40,10 +40,15 @@ def main():
         ("                if (__ballot((bigacc & 0xF800F800u) != 0u)) {\n",
          "                unsigned long long tq2_ = __builtin_amdgcn_s_memtime(); pt_[6] += tq2_ - tq1_;\n"
          "                if (__ballot((bigacc & 0xF800F800u) != 0u)) {\n"),
+    ] + ([  # PT_MARK=prefetch: the last Q sub-mark after the next granule's prefetch is issued
+        ("                /* scatter in (short-block reordered) position; M/S-only frames\n",
+         "                pt_[7] += __builtin_amdgcn_s_memtime() - tq2_;\n"
+         "                /* scatter in (short-block reordered) position; M/S-only frames\n"),
+    ] if os.environ.get("PT_MARK") == "prefetch" else [
         ("                /* the next granule's loads fly during phases I, M, W (issued\n",
          "                pt_[7] += __builtin_amdgcn_s_memtime() - tq2_;\n"
          "                /* the next granule's loads fly during phases I, M, W (issued\n"),
-    ]
+    ])
     for a, b in reps:
         assert src.count(a) == 1, a
         src = src.replace(a, b)
@@ -65,8 +70,9 @@ def main():
     open(d + "/mp3d_host.cpp", "w").write(host)
     os.makedirs(d + "/../../include", exist_ok=True)
     shutil.copy("include/mp3d.h", d + "/../../include/")
-    _build.compile_hip(d, "abx/PT.so", d + "/obj")
-    print("abx/PT.so")
+    out = "abx/PT2.so" if os.environ.get("PT_MARK") == "prefetch" else "abx/PT.so"
+    _build.compile_hip(d, out, d + "/obj")
+    print(out)
 
 
 if __name__ == "__main__":

@@ -17,7 +17,7 @@ sys.path.insert(0, str(ROOT / "tests"))
 
 
 def main():
-    assert os.environ.get("MP3D_LIB", "").endswith("PT.so"), "set MP3D_LIB=abx/PT.so"
+    assert "abx/PT" in os.environ.get("MP3D_LIB", ""), "set MP3D_LIB=abx/PT.so (or PT2.so)"
     import torch
     import _gen
     import mp3_amd
