@@ -161,6 +161,13 @@ VARS = {
     return r;""", """    (void)m; (void)f; r = t;
     return r;""")],
     "S2": [],
+    # r03: the next granule's prefetch issued at the start of phase I (PFI) / after the matrixing MFMAs (PFM)
+    "PFI": [('                if (PF == 0 && (LSF ? f + 1 < f1 : (gr == 0 || f + 1 < f1))) prefetch(LSF ? 2 * f + 2 : 2 * f + gr + 1, cs);\n', ""),
+            ("            /* ---------------- phase I: alias + IMDCT + overlap ------------ */\n",
+             "            /* ---------------- phase I: alias + IMDCT + overlap ------------ */\n" + '            if (!SRC_XR && PF == 0 && (LSF ? f + 1 < f1 : (gr == 0 || f + 1 < f1))) prefetch(LSF ? 2 * f + 2 : 2 * f + gr + 1, cs);\n')],
+    "PFM": [('                if (PF == 0 && (LSF ? f + 1 < f1 : (gr == 0 || f + 1 < f1))) prefetch(LSF ? 2 * f + 2 : 2 * f + gr + 1, cs);\n', ""),
+            ("                wave_sync(); /* all S reads retired before X overwrites them */\n",
+             '            if (!SRC_XR && PF == 0 && (LSF ? f + 1 < f1 : (gr == 0 || f + 1 < f1))) prefetch(LSF ? 2 * f + 2 : 2 * f + gr + 1, cs);\n' + "                wave_sync(); /* all S reads retired before X overwrites them */\n")],
     # r03: the count1 sign table with the store in the same iteration (no software pipelining)
     "S13": [("""                    int kp = -1;
                     uint32_t sp = 0u;
