@@ -26,6 +26,7 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
      * one v_perm_b32 (sign-extension selectors read odd bytes only) */
     __shared__ uint32_t s_c1s[256];
     huff_tables_lane(tab, s_lut, s_tsel, s_lbnd, s_slen);
+    static_assert(HUFF_BLOCK == 256, "s_c1s: one entry per thread");
     {
         const uint32_t v = threadIdx.x >> 4, s4 = threadIdx.x & 15u;
         int q[4], j = 0;
