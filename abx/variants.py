@@ -161,6 +161,14 @@ VARS = {
     return r;""", """    (void)m; (void)f; r = t;
     return r;""")],
     "S2": [],
+    # r03: is[] row stores (big_values groups, count1 quadruples) non-temporal (NT1)
+    "NT1": [("                        *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);",
+             "                        { typedef uint32_t nt4 __attribute__((ext_vector_type(4))); __builtin_nontemporal_store((nt4){wv[0], wv[1], wv[2], wv[3]}, (nt4 *)(row + k)); }"),
+            ("""                        *(uint2 *)(row + kq) = make_uint2(__builtin_amdgcn_perm(se, se, 0x09030801u),
+                                                          __builtin_amdgcn_perm(se << 8, se, 0x0B070A05u));""",
+             """                        typedef uint32_t nt2 __attribute__((ext_vector_type(2)));
+                        __builtin_nontemporal_store((nt2){__builtin_amdgcn_perm(se, se, 0x09030801u),
+                                                          __builtin_amdgcn_perm(se << 8, se, 0x0B070A05u)}, (nt2 *)(row + kq));""")],
     # r03: the next granule's prefetch issued at the start of phase I (PFI) / after the matrixing MFMAs (PFM)
     "PFI": [('                if (PF == 0 && (LSF ? f + 1 < f1 : (gr == 0 || f + 1 < f1))) prefetch(LSF ? 2 * f + 2 : 2 * f + gr + 1, cs);\n', ""),
             ("            /* ---------------- phase I: alias + IMDCT + overlap ------------ */\n",
