@@ -161,6 +161,8 @@ VARS = {
     return r;""", """    (void)m; (void)f; r = t;
     return r;""")],
     "S2": [],
+    # r03: k_mdcopy quadruples by one unaligned 16-B load each instead of 16 + 4 B and four funnel shifts (UA1)
+    "UA1": [('                    const uint32_t *L = q < nq ? lp + 4u * q : (const uint32_t *)dst;\n                    uint4 a;\n                    __builtin_memcpy(&a, L, 16);\n                    const uint32_t e = L[4];\n                    v[j] = make_uint4(__builtin_amdgcn_alignbit(a.y, sh ? a.x : a.y, sh),\n                                      __builtin_amdgcn_alignbit(a.z, sh ? a.y : a.z, sh),\n                                      __builtin_amdgcn_alignbit(a.w, sh ? a.z : a.w, sh),\n                                      __builtin_amdgcn_alignbit(e, sh ? a.w : e, sh));', '                    v[j] = *(const uint4 *)(q < nq ? sb + 16u * q : (const uint8_t *)dst); /* unaligned 16-B load */')],
     # r03: is[] row stores (big_values groups, count1 quadruples) non-temporal (NT1)
     "NT1": [("                        *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);",
              "                        { typedef uint32_t nt4 __attribute__((ext_vector_type(4))); __builtin_nontemporal_store((nt4){wv[0], wv[1], wv[2], wv[3]}, (nt4 *)(row + k)); }"),
