@@ -161,6 +161,10 @@ VARS = {
     return r;""", """    (void)m; (void)f; r = t;
     return r;""")],
     "S2": [],
+    "K1": [],
+    "K2": [],
+    # timing only (C3 holds no LSF stream): the LSF k_synth launch skipped on int16 batches (NL)
+    "NL": [("        if (kinds & 2) MP3D_SYNTH_LAUNCH(false, true);", "")],
     # r03: k_mdcopy quadruples by one unaligned 16-B load each instead of 16 + 4 B and four funnel shifts (UA1)
     "UA1": [('                    const uint32_t *L = q < nq ? lp + 4u * q : (const uint32_t *)dst;\n                    uint4 a;\n                    __builtin_memcpy(&a, L, 16);\n                    const uint32_t e = L[4];\n                    v[j] = make_uint4(__builtin_amdgcn_alignbit(a.y, sh ? a.x : a.y, sh),\n                                      __builtin_amdgcn_alignbit(a.z, sh ? a.y : a.z, sh),\n                                      __builtin_amdgcn_alignbit(a.w, sh ? a.z : a.w, sh),\n                                      __builtin_amdgcn_alignbit(e, sh ? a.w : e, sh));', '                    v[j] = *(const uint4 *)(q < nq ? sb + 16u * q : (const uint8_t *)dst); /* unaligned 16-B load */')],
     # r03: is[] row stores (big_values groups, count1 quadruples) non-temporal (NT1)

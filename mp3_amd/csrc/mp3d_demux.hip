@@ -87,24 +87,47 @@ struct LaneWin {        /* one lane's 64-B window of its stream, staged in LDS *
     }
 };
 
-/* the four 16-B aligned blocks around stream offset pos: every block holds
- * a stream byte (so none leaves the pages of the caller's buffer, which are
- * 16-B aligned units) or is not loaded; bytes at or past len read as zero */
-__device__ __forceinline__ void walk_load(LaneWin &W, const uint8_t *p0, uint32_t len, uint32_t pos) {
-    W.pos = pos;
-    W.mis = (uint32_t)((uintptr_t)(p0 + pos) & 15u);
-    const uint4 *base = (const uint4 *)(p0 + pos - W.mis);
+/* a window's four 16-B aligned blocks around stream offset pos, as loaded
+ * (walk_fetch) and then masked into the lane's LDS words (walk_commit): the
+ * loads of the next frame's window go out before the current frame's record
+ * stores, so its wait does not also wait for them (one vmcnt counter) */
+struct WinRaw {
     uint4 v[4];
+    uint32_t pos, mis;
+};
+/* every loaded block holds a stream byte (so none leaves the pages of the
+ * caller's buffer, which are 16-B aligned units) or is not loaded */
+__device__ __forceinline__ void walk_fetch(WinRaw &R, const uint8_t *p0, uint32_t len, uint32_t pos) {
+    R.pos = pos;
+    R.mis = (uint32_t)((uintptr_t)(p0 + pos) & 15u);
+    const uint4 *base = (const uint4 *)(p0 + pos - R.mis);
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-        const int64_t first = (int64_t)pos - (int64_t)W.mis + 16 * j; /* stream offset of the block */
-        v[j] = make_uint4(0u, 0u, 0u, 0u);
-        if (first < (int64_t)len) v[j] = base[j];
+        const int64_t first = (int64_t)pos - (int64_t)R.mis + 16 * j; /* stream offset of the block */
+        R.v[j] = make_uint4(0u, 0u, 0u, 0u);
+        if (first < (int64_t)len) R.v[j] = base[j];
     }
+}
+/* pos < len: block 0 holds a stream byte, and a block past the end re-reads
+ * it (walk_commit zeroes its bytes) -- no branch around the loads */
+__device__ __forceinline__ void walk_fetch_in(WinRaw &R, const uint8_t *p0, uint32_t len, uint32_t pos) {
+    R.pos = pos;
+    R.mis = (uint32_t)((uintptr_t)(p0 + pos) & 15u);
+    const uint4 *base = (const uint4 *)(p0 + pos - R.mis);
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-        const int64_t over = (int64_t)pos - (int64_t)W.mis + 16 * j + 16 - (int64_t)len; /* bytes past the end */
-        uint32_t q[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+        const int64_t first = (int64_t)pos - (int64_t)R.mis + 16 * j;
+        R.v[j] = *(first < (int64_t)len ? base + j : base);
+    }
+}
+/* bytes at or past len read as zero */
+__device__ __forceinline__ void walk_commit(LaneWin &W, const WinRaw &R, uint32_t len) {
+    W.pos = R.pos;
+    W.mis = R.mis;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int64_t over = (int64_t)R.pos - (int64_t)R.mis + 16 * j + 16 - (int64_t)len; /* bytes past the end */
+        uint32_t q[4] = {R.v[j].x, R.v[j].y, R.v[j].z, R.v[j].w};
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const int64_t o = over - 4 * (3 - i); /* bytes of word i past the end */
@@ -112,6 +135,22 @@ __device__ __forceinline__ void walk_load(LaneWin &W, const uint8_t *p0, uint32_
             W.w[4 * j + i] = q[i];
         }
     }
+}
+__device__ __forceinline__ void walk_load(LaneWin &W, const uint8_t *p0, uint32_t len, uint32_t pos) {
+    WinRaw R;
+    walk_fetch(R, p0, len, pos);
+    walk_commit(W, R, len);
+}
+
+/* the header's frame word from the workgroup's LDS copy of c_frame_word
+ * (frame bytes | bitrate << 16, padding added), or 0: not a Layer III
+ * header of the stream's family (hdr_frame_bytes' checks) */
+__device__ __forceinline__ uint32_t walk_frame_word(const uint32_t *s_fw, uint32_t b1, uint32_t b2, int kind) {
+    if ((b1 & 0xE0) != 0xE0 || ((b1 >> 1) & 3) != 1 || ((b1 >> 3) & 3) == 1) return 0u;
+    const uint32_t bi = b2 >> 4;
+    if (bi == 0 || bi == 15 || ((b2 >> 2) & 3) == 3) return 0u;
+    if (kind && hdr_kind(b1) != kind) return 0u;
+    return s_fw[16 * hdr_sr_idx(b1, b2) + bi] + ((b2 >> 1) & 1u);
 }
 
 /* CRC-16 (poly 0x8005, init 0xFFFF, MSB first) over header bytes 2..3 and
@@ -133,12 +172,19 @@ __global__ void __launch_bounds__(64) k_walk(const uint8_t *__restrict__ in, con
                                              FrameRec *__restrict__ rec, uint64_t *__restrict__ sideu,
                                              DevInfo *__restrict__ infos, int n_streams, int F, int opts) {
     __shared__ uint32_t s_win[64 * WALK_WORDS];
+    /* frame words and sample rates in LDS: a constant-table read per frame
+     * from L2 was a round trip on the frame chain */
+    __shared__ uint32_t s_fw[9 * 16], s_hz[9];
     const int lane = threadIdx.x;
+    for (int i = lane; i < 9 * 16; i += 64) s_fw[i] = (&c_frame_word[0][0])[i];
+    if (lane < 9) s_hz[lane] = MP3D_SAMPLE_RATE[lane];
+    __syncthreads();
     const int s = blockIdx.x * WALK_LANES + lane;
     if (lane >= WALK_LANES || s >= n_streams) return; /* no barrier below */
     LaneWin W;
     W.w = s_win + lane * WALK_WORDS;
-    const uint8_t *p0 = in + in_off[s];
+    const uint64_t off_s = in_off[s];
+    const uint8_t *p0 = in + off_s;
     const uint32_t len = in_len[s];
     StreamState &S = st[s];
     const int carry_in = S.res_len;
@@ -158,13 +204,15 @@ __global__ void __launch_bounds__(64) k_walk(const uint8_t *__restrict__ in, con
         const size_t fi = (size_t)s * F + f;
         /* ---- sync: the next valid header at or after cur (resync over junk) */
         int fb = -1;
+        uint32_t fw = 0u;
         while (cur + 4 <= len) {
             if (W.pos != cur) walk_load(W, p0, len, cur);
             const uint32_t lim = min(46u, len - cur - 4);
             uint32_t k = 0;
             for (; k <= lim; k++) {
                 if (W.byte(k) == 0xFFu) {
-                    fb = hdr_frame_bytes(W.byte(k + 1), W.byte(k + 2), kind);
+                    fw = walk_frame_word(s_fw, W.byte(k + 1), W.byte(k + 2), kind);
+                    fb = fw ? (int)(fw & 0xFFFFu) : -1;
                     if (fb > 0) break;
                 }
             }
@@ -190,7 +238,7 @@ __global__ void __launch_bounds__(64) k_walk(const uint8_t *__restrict__ in, con
             if (cur + (uint32_t)fb <= len || cur + need <= len) {
                 const uint32_t have = min(len - cur, (uint32_t)fb);
                 const int plen = fb - 4 - crc - side_bytes;
-                r.frame_off = in_off[s] + cur;
+                r.frame_off = off_s + cur;
                 r.frame_bytes = (uint16_t)fb;
                 r.payload_len = (uint16_t)(plen > 0 ? plen : 0);
                 r.hdr1 = (uint8_t)h1; r.hdr2 = (uint8_t)h2; r.hdr3 = (uint8_t)h3;
@@ -198,8 +246,8 @@ __global__ void __launch_bounds__(64) k_walk(const uint8_t *__restrict__ in, con
                 r.side_off = (uint8_t)(4 + crc);
                 r.sr_idx = (uint8_t)hdr_sr_idx(h1, h2);
                 r.lsf = (uint8_t)lsf;
-                inf.frame_bytes = fb; inf.channels = nch; inf.hz = (int)MP3D_SAMPLE_RATE[r.sr_idx];
-                inf.layer = 3; inf.bitrate_kbps = lsf ? MP3D_BITRATE_L3_LSF[h2 >> 4] : MP3D_BITRATE_L3[h2 >> 4];
+                inf.frame_bytes = fb; inf.channels = nch; inf.hz = (int)s_hz[r.sr_idx];
+                inf.layer = 3; inf.bitrate_kbps = (int)(fw >> 16);
                 const uint32_t sbit = 8u * (4u + (uint32_t)crc);
                 const int mdb = (int)(W.bits64(sbit) >> (lsf ? 56 : 55));
                 uint32_t p23[2][2] = {{0u, 0u}, {0u, 0u}};
@@ -276,13 +324,18 @@ __global__ void __launch_bounds__(64) k_walk(const uint8_t *__restrict__ in, con
                 cur = len;
             }
         }
+        /* the next frame's window loads first, then this frame's record
+         * stores, then the window into LDS (its wait leaves the stores in
+         * flight); a lane without a next frame re-reads its side words */
+        ulonglong2 *sd = (ulonglong2 *)&sideu[fi * 4];
+        const bool more = cur + 4 <= len && f + 1 < F;
+        WinRaw nx;
+        walk_fetch_in(nx, more ? p0 : (const uint8_t *)sd, more ? len : 16u, more ? cur : 0u);
         rec[fi] = r;
         if (infos) infos[fi] = inf;
-        ulonglong2 *sd = (ulonglong2 *)&sideu[fi * 4];
         sd[0] = make_ulonglong2(sw[0], sw[1]);
         sd[1] = make_ulonglong2(sw[2], sw[3]);
-        /* the next frame's window in flight while this frame's records store */
-        if (cur + 4 <= len && f + 1 < F) walk_load(W, p0, len, cur);
+        if (more) walk_commit(W, nx, len);
     }
     int c = avail < MP3D_RES_BYTES ? avail : MP3D_RES_BYTES;
     if ((uint32_t)c > P) c = (int)P;

@@ -40,7 +40,7 @@ def regions_synth(path):
     wend = find("state out: the stream's last segment", w)
     esc = find("rare path (escapes |is| >= 256)", q)
     isb = find("if (is_on) {", q)
-    ism = find("} else if (ms_fold) {", isb)
+    ism = find("the next granule's loads fly during phases I, M, W", isb)
     bsl = find("const bool lng = lane < 22;", q)
     bsl_end = find("Wd.scale[1][lane] = band_scale", bsl)
     shi = find("/* z[6w+6+i] += y_w[i] * win12[i], w = 0..2, i = 0..11 */", i_)
