@@ -163,6 +163,10 @@ VARS = {
     "S2": [],
     "K1": [],
     "K2": [],
+    "C2S": [],
+    # r03: big_values groups wholly past the lane's big_values not stored (count1 or nothing reads them) (BVZ)
+    "BVZ": [("                        *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);",
+             "                        if (k < bv2) *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);")],
     # timing only (C3 holds no LSF stream): the LSF k_synth launch skipped on int16 batches (NL)
     "NL": [("        if (kinds & 2) MP3D_SYNTH_LAUNCH(false, true);", "")],
     # r03: k_mdcopy quadruples by one unaligned 16-B load each instead of 16 + 4 B and four funnel shifts (UA1)

@@ -281,20 +281,37 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                         *(uint2 *)(row + kq) = make_uint2(__builtin_amdgcn_perm(se, se, 0x09030801u),
                                                           __builtin_amdgcn_perm(se << 8, se, 0x0B070A05u));
                     };
-                    /* (its store waits for the s_c1s read; made one iteration
-                     * later instead, the time was the same: A/B C1P) */
-                    while (k <= 572 && pos < end_bit) {
-                        const uint32_t hw = win32g(bits, pos);
+                    /* one quadruple: its signed values (s_c1s) and bit count,
+                     * or false when it overreads the part2_3 end.  The signs
+                     * follow the code, one per nonzero value in order: the 4
+                     * bits after the code and v index the table. */
+                    auto c1_dec = [&](uint32_t p, uint32_t &se, uint32_t &nb) {
+                        const uint32_t hw = win32g(bits, p);
                         const uint32_t e = s_lut[c1base + (hw >> c1sh)];
                         const uint32_t v = e & 15u, lq = (e >> 8) & 31u;
-                        const uint32_t ns = __builtin_popcount(v);
-                        if (pos + lq + ns > end_bit) break;
-                        /* the signs follow the code, one per nonzero value in
-                         * order: the 4 bits after the code and v index the
-                         * signed values (s_c1s); off the pos chain */
-                        c1_store(k, s_c1s[(v << 4) | ((hw << lq) >> 28)]);
-                        pos += lq + ns;
-                        k += 4;
+                        nb = lq + __builtin_popcount(v);
+                        se = s_c1s[(v << 4) | ((hw << lq) >> 28)];
+                        return p + nb <= end_bit;
+                    };
+                    /* two quadruples per iteration, one 16-B store (4-B aligned:
+                     * k is even) -- half the store instructions of the 8-B form,
+                     * each touching a line per lane; a lane whose second
+                     * quadruple is absent stores the first alone and leaves */
+                    while (k <= 572 && pos < end_bit) {
+                        uint32_t se0, n0, se1, n1;
+                        if (!c1_dec(pos, se0, n0)) break;
+                        pos += n0;
+                        if (k > 568 || pos >= end_bit || !c1_dec(pos, se1, n1)) {
+                            c1_store(k, se0);
+                            k += 4;
+                            break;
+                        }
+                        pos += n1;
+                        const uint4 q = make_uint4(
+                            __builtin_amdgcn_perm(se0, se0, 0x09030801u), __builtin_amdgcn_perm(se0 << 8, se0, 0x0B070A05u),
+                            __builtin_amdgcn_perm(se1, se1, 0x09030801u), __builtin_amdgcn_perm(se1 << 8, se1, 0x0B070A05u));
+                        __builtin_memcpy(row + k, &q, 16);
+                        k += 8;
                     }
                     const int nz_end = k;
                     UnitMeta m;
