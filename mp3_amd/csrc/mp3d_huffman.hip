@@ -270,8 +270,9 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                     }
                     k = bv2;
                     /* count1 quadruples until the part2_3 end; a quadruple that
-                     * overreads it is discarded (FFmpeg); one
-                     * 8-B store each (lines k .. k + 3) */
+                     * overreads it is discarded (FFmpeg); lines
+                     * k .. k + 3 each, stored in pairs (an unpaired last one by
+                     * an 8-B store) */
                     /* table A or B (count1table_select) as one LUT read, no branch */
                     const bool c1b = (side >> 5) & 1;
                     const uint32_t c1base = c1b ? c1b_base : qbase, c1sh = c1b ? 28u : 32u - (uint32_t)qb1;
@@ -281,27 +282,34 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                         *(uint2 *)(row + kq) = make_uint2(__builtin_amdgcn_perm(se, se, 0x09030801u),
                                                           __builtin_amdgcn_perm(se << 8, se, 0x0B070A05u));
                     };
-                    /* one quadruple: its signed values (s_c1s) and bit count,
-                     * or false when it overreads the part2_3 end.  The signs
-                     * follow the code, one per nonzero value in order: the 4
-                     * bits after the code and v index the table. */
-                    auto c1_dec = [&](uint32_t p, uint32_t &se, uint32_t &nb) {
-                        const uint32_t hw = win32g(bits, p);
+                    /* one quadruple from the window hw (its code at the top):
+                     * its signed values (s_c1s) and bit count.  The signs follow
+                     * the code, one per nonzero value in order: the 4 bits after
+                     * the code and v index the table. */
+                    auto c1_dec = [&](uint32_t hw, uint32_t &se, uint32_t &nb) {
                         const uint32_t e = s_lut[c1base + (hw >> c1sh)];
                         const uint32_t v = e & 15u, lq = (e >> 8) & 31u;
                         nb = lq + __builtin_popcount(v);
                         se = s_c1s[(v << 4) | ((hw << lq) >> 28)];
-                        return p + nb <= end_bit;
                     };
-                    /* two quadruples per iteration, one 16-B store (4-B aligned:
-                     * k is even) -- half the store instructions of the 8-B form,
-                     * each touching a line per lane; a lane whose second
-                     * quadruple is absent stores the first alone and leaves */
+                    /* two quadruples per iteration from one 32-bit window (a
+                     * quadruple takes <= 10 bits, so the second's code and signs
+                     * are in hw << n0) and one 16-B store (4-B aligned: k is
+                     * even) -- half the store instructions of the 8-B form, each
+                     * touching a line per lane, and half the window reads; a
+                     * quadruple that overreads the part2_3 end ends the loop */
                     while (k <= 572 && pos < end_bit) {
+                        const uint32_t hw = win32g(bits, pos);
                         uint32_t se0, n0, se1, n1;
-                        if (!c1_dec(pos, se0, n0)) break;
+                        c1_dec(hw, se0, n0);
+                        if (pos + n0 > end_bit) break;
                         pos += n0;
-                        if (k > 568 || pos >= end_bit || !c1_dec(pos, se1, n1)) {
+                        bool two = k <= 568 && pos < end_bit;
+                        if (two) {
+                            c1_dec(hw << n0, se1, n1);
+                            two = pos + n1 <= end_bit;
+                        }
+                        if (!two) {
                             c1_store(k, se0);
                             k += 4;
                             break;
