@@ -165,6 +165,7 @@ VARS = {
     "K2": [],
     "C2S": [],
     "C1W": [],
+    "C4W": [],
     # r03: big_values groups wholly past the lane's big_values not stored (count1 or nothing reads them) (BVZ)
     "BVZ": [("                        *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);",
              "                        if (k < bv2) *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);")],
