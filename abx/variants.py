@@ -166,6 +166,9 @@ VARS = {
     "C2S": [],
     "C1W": [],
     "C4W": [],
+    # r03: each row zeroed from nz_end to the next 128-B / 64-B boundary (no partially written line) (PAD128, PAD64)
+    "PAD128": None,
+    "PAD64": None,
     # r03: big_values groups wholly past the lane's big_values not stored (count1 or nothing reads them) (BVZ)
     "BVZ": [("                        *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);",
              "                        if (k < bv2) *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);")],
@@ -339,6 +342,22 @@ VARS = {
             """                        ce[nt][ks] = Ae[ks] * Be[nt][ks];
                         co[nt][ks] = Ao[ks] * Bo[nt][ks];""")],
 }
+
+def _pad(n):
+    return [("                    const int nz_end = k;\n",
+             "                    const int nz_end = k;\n"
+             "                    {   /* zero the row from nz_end to the next %d-B boundary: no partially written line */\n"
+             "                        uint32_t b = 2u * (uint32_t)nz_end;\n"
+             "                        const uint32_t B = (b + %du) & ~%du;\n"
+             "                        uint8_t *rb = (uint8_t *)row;\n"
+             "                        if (b < B && (b & 4u)) { *(uint32_t *)(rb + b) = 0u; b += 4u; }\n"
+             "                        if (b < B && (b & 8u)) { *(uint2 *)(rb + b) = make_uint2(0u, 0u); b += 8u; }\n"
+             "                        for (; b < B; b += 16u) *(uint4 *)(rb + b) = make_uint4(0u, 0u, 0u, 0u);\n"
+             "                    }\n" % (n, n - 1, n - 1))]
+
+
+VARS["PAD128"] = _pad(128)
+VARS["PAD64"] = _pad(64)
 
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
