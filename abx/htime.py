@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Build abx/HT.so: k_huffman with per-stage cycle accounting (diagnostic;
+"""Build build_ab/HT.so: k_huffman with per-stage cycle accounting (diagnostic;
 the output is unchanged).  Each wave sums s_memtime deltas of: ranking,
 round set-up, staging, scalefactors, big_values, count1, meta stores; lane
 0 adds them to g_htime with one global atomic per stage at the end;
@@ -63,8 +63,8 @@ def main():
     open(d + "/mp3d_host.cpp", "w").write(host)
     os.makedirs(d + "/../../include", exist_ok=True)
     shutil.copy("include/mp3d.h", d + "/../../include/")
-    _build.compile_hip(d, "abx/HT.so", d + "/obj")
-    print("abx/HT.so")
+    _build.compile_hip(d, "build_ab/HT.so", d + "/obj")
+    print("build_ab/HT.so")
 
 
 if __name__ == "__main__":

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Build abx/PT.so: k_synth with per-phase cycle accounting (diagnostic; the
+"""Build build_ab/PT.so: k_synth with per-phase cycle accounting (diagnostic; the
 output is unchanged).  Each wave sums s_memtime deltas over its granules for
 phases Q, I, M, W and the loop head, then adds them to g_ptime with one
 global atomic per phase; mp3d_dbg_ptime() reads and clears them
@@ -70,7 +70,7 @@ def main():
     open(d + "/mp3d_host.cpp", "w").write(host)
     os.makedirs(d + "/../../include", exist_ok=True)
     shutil.copy("include/mp3d.h", d + "/../../include/")
-    out = "abx/PT2.so" if os.environ.get("PT_MARK") == "prefetch" else "abx/PT.so"
+    out = "build_ab/PT2.so" if os.environ.get("PT_MARK") == "prefetch" else "build_ab/PT.so"
     _build.compile_hip(d, out, d + "/obj")
     print(out)
 

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Build k_synth phase-ablation variants (abx/NAME.so) for A/B timing only:
+"""Build k_synth phase-ablation variants (build_ab/NAME.so) for A/B timing only:
 their output is wrong by construction.  Usage: python abx/variants.py"""
 import os
 import shutil
@@ -27,7 +27,7 @@ def variant(name, reps):
     shutil.copy("mp3_amd/csrc/mp3d_host.cpp", d)
     os.makedirs(d + "/../../include", exist_ok=True)
     shutil.copy("include/mp3d.h", d + "/../../include/")
-    _build.compile_hip(d, "abx/%s.so" % name, d + "/obj", extra=flags)
+    _build.compile_hip(d, "build_ab/%s.so" % name, d + "/obj", extra=flags)
 
 
 W4H = ("__global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(",

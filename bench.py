@@ -439,8 +439,17 @@ def main():
         # on a one-GPU box) share them round-robin
         c.gpu = local % max(1, torch.cuda.device_count())
         c.dev = torch.device("cuda", c.gpu)
-    if world > 1:
+    # --gather at N = 1 still initialises a (one-rank) RCCL group, so the
+    # branch an 8-GPU run takes -- init with device_id, the async gather into
+    # preallocated receive lists, work.wait() ordering -- executes on one GPU
+    use_group = world > 1 or (args.gather and not args.plumbing and backend == "nccl")
+    if use_group:
         if backend == "nccl":
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if "MASTER_PORT" not in os.environ:
+                os.environ["MASTER_PORT"] = str(_free_port())
+            os.environ.setdefault("RANK", str(rank))
+            os.environ.setdefault("WORLD_SIZE", str(world))
             torch.cuda.set_device(c.gpu)
             dist.init_process_group("nccl", device_id=c.dev)
         else:
@@ -455,11 +464,14 @@ def main():
     c.F = args.frames or (64 if cfg == "c2" else 32)
     c.gen_threads = max(1, min(16, host_threads() // world))
     c.setup_s = 0.0
-    if args.gather and world > 1:
+    if args.gather and use_group:
         # rank 0's receive lists (one per gather in flight) must fit beside
         # the batch buffers; checked at the FULL per-rank size even when
-        # --plumbing shrinks the data
-        plan = shard.gather_plan(c.n, c.F, world, decoder_bytes=decoder_bytes(c.n, c.F))
+        # --plumbing shrinks the data, against the device's real memory
+        dev_bytes = shard.DEVICE_BYTES_DEFAULT
+        if c.gpu is not None:
+            dev_bytes = torch.cuda.get_device_properties(c.gpu).total_memory
+        plan = shard.gather_plan(c.n, c.F, world, device_bytes=dev_bytes, decoder_bytes=decoder_bytes(c.n, c.F))
         if not plan["fits"]:
             raise SystemExit("bench.py: the --gather receive lists need %.1f GB on rank 0, more than %.1f GB"
                              % (plan["need_bytes"] / 1e9, plan["device_bytes"] / 1e9))
@@ -538,6 +550,13 @@ def main():
         if world > 1:
             dist.barrier()
         sdt = shard.max_over_ranks(time.perf_counter() - t0, c.dev)
+        # the streaming loop's own output: every segment of the last `segs`
+        # steps must have decoded all its frames (a geometry-staging bug that
+        # drops frames would otherwise still report full throughput)
+        sinf = c.stream_buf[3]
+        sframes = int((sinf[..., 5] > 0).sum())
+        if cfg == "c3" and sframes != c.n * c.F:
+            raise SystemExit("streaming decode produced %d/%d frames" % (sframes, c.n * c.F))
         sval = sum(per_rank_frames) * args.steps / sdt
         streaming = {"value": sval, "ms_per_step": sdt / args.steps * 1e3, "segments": segs,
                      "vs_fixed_offsets": sval / value,
@@ -548,19 +567,19 @@ def main():
 
     # --- optional RCCL PCM gather, overlapped with the next step ----------
     gather = None
-    if args.gather and world > 1:
+    if args.gather and use_group:
         gather = time_gather(c, args, dist, shard, torch, sync)
 
     setup_all = shard.all_ranks(c.setup_s, c.dev)  # collective: every rank takes part
     if rank != 0:
-        if world > 1:
+        if use_group:
             dist.destroy_process_group()
         return
     res = {"metric": METRIC, "value": None if args.plumbing else value, "unit": "frames/s", "n_gpus": world,
            "ranks": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
            "per_rank_frames_per_s": [f * args.steps / t for f, t in zip(per_rank_frames, per_rank_dt)],
-           "dist_backend": backend if world > 1 else None,
+           "dist_backend": backend if use_group else None,
            "setup_s_per_rank": setup_all, "gen_threads_per_rank": c.gen_threads}
     if args.plumbing:
         res.update(plumbing_only=True, data="synthetic C3 shard per rank (generated, not decoded)",
@@ -576,7 +595,7 @@ def main():
     if streaming:
         res["streaming"] = streaming
     print(json.dumps(res), flush=True)
-    if world > 1:
+    if use_group:
         dist.destroy_process_group()
 
 
@@ -624,9 +643,14 @@ def time_gather(c, args, dist, shard, torch, sync):
             "ms_per_step_decode_plus_gather": dt / args.steps * 1e3,
             "frames_per_s_with_gather": c.n * c.F * c.world * args.steps / dt,
             "overlapped": dist.get_backend() != "gloo",
+            "world": c.world, "backend": dist.get_backend(),
+            "self_gather_only": c.world == 1,
             "rank0_memory_plan": getattr(c, "gather_plan", None),
             "note": "PCM of step k gathered to rank 0 over RCCL (xGMI) on the process group's stream while step "
-                    "k+1 decodes; reported apart from `value`"}
+                    "k+1 decodes; reported apart from `value`" + (
+                        "; world 1: a one-rank RCCL group gathers rank 0's PCM to itself (device copy, no xGMI), "
+                        "which runs the same init / async gather / wait code an 8-GPU run takes" if c.world == 1
+                        else "")}
 
 
 def decoder_bytes(n, F):

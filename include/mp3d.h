@@ -81,7 +81,9 @@ MP3D_API void mp3d_dec_reset(mp3d_dec *dec);
 MP3D_API int mp3d_decode_frame(mp3d_dec *dec, const uint8_t *buf, size_t bytes, int16_t *pcm /* <= 2304 */,
                       mp3d_frame_info *info);
 /* the same with float32 PCM (FFmpeg's float convention: full scale 1.0,
- * not clipped; the int16 output is clamp(rint(x * 32768)) of these values) */
+ * not clipped; the int16 output is clamp(floor(x * 32768 + 0.5)) of these
+ * values, saturated to [-32768, 32767]: FFmpeg's fixed-point round_sample
+ * convention, so an exact .5 tie rounds up, unlike rint's ties-to-even) */
 MP3D_API int mp3d_decode_frame_f32(mp3d_dec *dec, const uint8_t *buf, size_t bytes, float *pcm /* <= 2304 */,
                           mp3d_frame_info *info);
 /* (ABI v4) either of the above by flags: MP3D_FRAME_F32 selects float32 PCM;

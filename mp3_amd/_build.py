@@ -45,6 +45,7 @@ def compile_hip(src_dir, out, obj_dir, extra=()):
     for cmd, p in procs:
         if p.wait():
             raise subprocess.CalledProcessError(p.returncode, cmd)
+    pathlib.Path(out).parent.mkdir(parents=True, exist_ok=True)
     subprocess.check_call([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", str(out)] + objs)
     return out
 

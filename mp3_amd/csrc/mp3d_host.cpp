@@ -453,11 +453,14 @@ static int tail_plan(mp3d_batch *b, int n, int F, int seg_len, hipStream_t s, Ta
     return MP3D_OK;
 }
 
-/* a call on stream s: order it after the handle's previous call when that
- * one ran on another stream (the handle's buffers are shared) */
+/* a call on stream s: order it after the handle's previous call (the
+ * handle's buffers are shared).  Only two calls in a row on the handle's own
+ * stream skip the wait; after a call on a caller's stream the wait is made
+ * even when s compares equal, since a destroyed stream's handle value can be
+ * reused by the caller's next stream (a no-op once the event completed). */
 static int call_begin(mp3d_batch *b, hipStream_t s) {
     HIPCHK(hipSetDevice(b->device));
-    if (b->last_s && b->last_s != s) HIPCHK(hipStreamWaitEvent(s, end_event(b), 0));
+    if (b->last_s && (b->last_s != s || s != b->own)) HIPCHK(hipStreamWaitEvent(s, end_event(b), 0));
     return MP3D_OK;
 }
 
@@ -652,8 +655,10 @@ static int prepare_geometry(mp3d_batch *b, const uint64_t *offsets, const uint32
     }
     b->geo_i ^= 1;
     mp3d_batch::Geo &g = b->geo[b->geo_i];
+    /* the slot holds no valid geometry until its copy is queued: a failed
+     * stage below can never be served from the cache by a retried call */
+    g.n = -1;
     HIPCHK(hipEventSynchronize(g.staged)); /* this slot's last copy has read g.h */
-    g.n = n;
     uint64_t *h_md = g.h + n;
     size_t o = 0;
     for (int i = 0; i < n; i++) {
@@ -672,6 +677,7 @@ static int prepare_geometry(mp3d_batch *b, const uint64_t *offsets, const uint32
     HIPCHK(hipMemcpyAsync(g.d, g.h, 20 * (size_t)n, hipMemcpyHostToDevice, b->copy));
     HIPCHK(hipEventRecord(g.staged, b->copy));
     HIPCHK(hipStreamWaitEvent(s, g.staged, 0));
+    g.n = n;
     return MP3D_OK;
 }
 
@@ -1123,6 +1129,12 @@ struct mp3d_dec {
     bool ra_f32 = false;
     long ra_frames0 = 0; /* frames / kind before the read-ahead */
     int ra_kind0 = 0;
+    /* back-off: a settle that drops frames decoded ahead wasted
+     * them, so the next ra_cool calls decode their own frame only; each such
+     * settle doubles the pause (up to 64 calls), a read-ahead served whole
+     * clears it.  A player that saves its state every frame then pays one
+     * read-ahead per ~65 frames instead of two batch decodes per frame. */
+    int ra_cool = 0, ra_backoff = 0;
 };
 
 static void dec_free(mp3d_dec *d) {
@@ -1218,6 +1230,7 @@ extern "C" void mp3d_dec_reset(mp3d_dec *d) {
     if (!d) return;
     d->ra.clear(); /* the state is zeroed whole */
     d->ra_next = 0;
+    d->ra_cool = d->ra_backoff = 0;
     (void)mp3d_batch_reset(d->b);
     d->frames = 0;
     d->kind = 0;
@@ -1283,8 +1296,11 @@ static int ra_settle(mp3d_dec *d) {
     d->ra_next = 0;
     if (all) { /* every frame was served: the state is where the caller is */
         d->ra.clear();
+        d->ra_backoff = 0;
         return MP3D_OK;
     }
+    d->ra_backoff = std::min(64, std::max(1, 2 * d->ra_backoff));
+    d->ra_cool = d->ra_backoff;
     mp3d_batch *b = d->b;
     HIPCHK(hipSetDevice(b->device));
     int r = own_after_last(b);
@@ -1310,6 +1326,10 @@ static int ra_settle(mp3d_dec *d) {
  * served, 0 when there are too few frames (the single-frame path then). */
 static int ra_fill(mp3d_dec *d, const uint8_t *buf, size_t bytes, bool f32) {
     if (!d->ra_max) return 0;
+    if (d->ra_cool > 0) { /* backing off after a wasted read-ahead */
+        d->ra_cool--;
+        return 0;
+    }
     size_t cur = 0;
     uint32_t o = 0;
     int kind = d->kind, kinds = 0;
@@ -1372,6 +1392,7 @@ static int decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, void *pcm
     } else if (!d->ra.empty()) {
         d->ra.clear(); /* all served */
         d->ra_next = 0;
+        d->ra_backoff = 0;
     }
     if (loc <= 0) {
         info->frame_bytes = (int)pos;

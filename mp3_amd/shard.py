@@ -73,9 +73,10 @@ def gather_to_root(t: torch.Tensor, root: int = 0, async_op: bool = False, out=N
 
 
 PCM_ROW_BYTES = 2304 * 2  # one int16 stereo frame
+DEVICE_BYTES_DEFAULT = 288 << 30  # MI355X HBM3E; bench.py passes the device's real total
 
 
-def gather_plan(n_per_rank: int, frames: int, world: int, in_flight: int = 2, device_bytes: int = 288 << 30,
+def gather_plan(n_per_rank: int, frames: int, world: int, in_flight: int = 2, device_bytes: int = DEVICE_BYTES_DEFAULT,
                 decoder_bytes: int = 0):
     """Device memory rank 0 needs for the overlapped PCM gather (bench.py
     --gather): `in_flight` receive lists of `world` PCM shards each (one list

@@ -14,7 +14,18 @@ manifest.json without touching the others.
                     (FFmpeg's 8 kHz band tables and region sizes)
   lsf_rand          random LSF rate / mode
 
-Usage:  python tests/golden/make_lsf_golden.py
+At scale (the 16-frame cases pin the LSF reservoir,
+intensity and FIFO carry only briefly), 256 frames per class:
+
+  lsf_scale_22k_js    22.05 kHz joint stereo (M/S and intensity per frame),
+                      short + mixed blocks, VBR
+  lsf_scale_24k_is    24 kHz intensity stereo only
+  lsf_scale_16k_mono  16 kHz mono, CRC on half the frames
+  lsf_scale_11k_msis  11.025 kHz (MPEG-2.5) M/S + intensity
+  lsf_scale_8k_js     8 kHz (MPEG-2.5) joint stereo, short + mixed blocks
+
+Usage:  python tests/golden/make_lsf_golden.py [--scale]   (--scale: only
+the 256-frame classes; the 16-frame ones are left as committed)
 """
 import json
 import pathlib
@@ -40,23 +51,33 @@ CASES = {
     "lsf_8k_js": dict(sr_idx=8, mode=1, mode_ext=-1, short_pct=30, mixed_pct=40),
     "lsf_rand": dict(sr_idx=-2),
 }
+SCALE_FRAMES = 256
+SCALE_CASES = {
+    "lsf_scale_22k_js": dict(sr_idx=3, mode=1, mode_ext=-1, short_pct=25, mixed_pct=30),
+    "lsf_scale_24k_is": dict(sr_idx=4, mode=1, mode_ext=1, short_pct=20, mixed_pct=25),
+    "lsf_scale_16k_mono": dict(sr_idx=5, mode=3, short_pct=20, mixed_pct=25, crc_pct=50),
+    "lsf_scale_11k_msis": dict(sr_idx=6, mode=1, mode_ext=3, short_pct=20, mixed_pct=25),
+    "lsf_scale_8k_js": dict(sr_idx=8, mode=1, mode_ext=-1, short_pct=25, mixed_pct=30),
+}
 
 
 def main():
     manifest = json.loads((HERE / "manifest.json").read_text())
-    for i, (name, upd) in enumerate(CASES.items()):
+    todo = [(name, upd, 7_000_003 + i, N_FRAMES) for i, (name, upd) in enumerate(CASES.items())]
+    scale = [(name, upd, 7_100_003 + i, SCALE_FRAMES) for i, (name, upd) in enumerate(SCALE_CASES.items())]
+    todo = scale if "--scale" in sys.argv[1:] else todo + scale
+    for name, upd, seed, nf in todo:
         cfg = dict(_gen.C5)
         cfg.update(upd)
-        seed = 7_000_003 + i
-        data, _ = _gen.stream(cfg, seed, N_FRAMES)
+        data, _ = _gen.stream(cfg, seed, nf)
         ver, si = (data[1] >> 3) & 3, (data[2] >> 2) & 3
         hz = HZ[si + (0 if ver == 3 else 3 if ver == 2 else 6)]
         nch = 1 if (data[3] >> 6) == 3 else 2
         ref = ffmpeg_oracle.decode(data, hz, nch)
-        assert ref.shape == (nch, N_FRAMES * 576), ref.shape
+        assert ref.shape == (nch, nf * 576), ref.shape
         (HERE / (name + ".mp3")).write_bytes(data)
         np.save(HERE / (name + ".pcm16.npy"), to_int16(ref))
-        manifest[name] = dict(cfg=cfg, seed=seed, frames=N_FRAMES, hz=hz, nch=nch, spf=576)
+        manifest[name] = dict(cfg=cfg, seed=seed, frames=nf, hz=hz, nch=nch, spf=576)
         print(name, hz, nch, len(data))
     (HERE / "manifest.json").write_text(json.dumps(manifest, indent=1, sort_keys=True))
     record_hashes()

@@ -2,8 +2,10 @@
 (VERDICT r02 "do this" 1; fixtures from tests/golden/make_scale_golden.py):
 the bench's own C3 streams (global ids 0..7) and C5 streams (0..3), 256
 frames per C5 corpus class, one 512-frame C3 stream (main_data_begin up to
-511, reservoir / overlap / FIFO carried far past frame 16) and the IS
-flush probes, all in ONE ragged batch through the C ABI.  PCM within +-1
+511, reservoir / overlap / FIFO carried far past frame 16), the IS
+flush probes and 256 frames per MPEG-2 / 2.5 LSF class (8 / 11.025 / 16 /
+22.05 / 24 kHz with intensity, M/S and mono; make_lsf_golden.py --scale),
+all in ONE ragged batch (both families side by side) through the C ABI.  PCM within +-1
 LSB of FFmpeg (north_star's tolerance); the same streams decoded in calls of
 32 frames (state resident in HBM across calls, the streaming loop) are
 bit-identical to the single call."""
@@ -16,7 +18,7 @@ import mp3_amd
 
 pytestmark = pytest.mark.gpu
 
-PREFIXES = ("bench_c3_", "bench_c5_", "scale_", "long_c3_", "probe_flush_")
+PREFIXES = ("bench_c3_", "bench_c5_", "scale_", "long_c3_", "probe_flush_", "lsf_scale_")
 
 
 def _cases():

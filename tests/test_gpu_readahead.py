@@ -99,3 +99,14 @@ def test_readahead_early_exits():
     _same(_run(_dec(16), data, script), _run(_dec(0), data, script))
     for k in (2, 5, 64):  # other read-ahead lengths
         _same(_run(_dec(k), data, script), _run(_dec(0), data, script))
+
+
+def test_readahead_backoff_state_every_frame():
+    """A player saving its state every frame: each save settles
+    a read-ahead after one frame, so the decoder backs off (1, 2, 4 .. 64
+    calls without read-ahead); the output stays bit-identical, through a
+    whole read-ahead served afterwards (back-off cleared) and a reset."""
+    data, _ = _gen.stream(_gen.C5, 77_003, 200)
+    call = [("call", False)]
+    script = (call + [("state",)]) * 90 + call * 70 + [("state",)] + [("reset",)] + (call + [("state",)]) * 20
+    _same(_run(_dec(32), data, script), _run(_dec(0), data, script))

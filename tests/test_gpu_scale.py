@@ -2,7 +2,7 @@
 (C3 oracle coverage was a 5-stream spot check), and
 the multi-rank path actually decoding (weak item 7).
 
-- C3 at its full size (65,536 streams x 32 frames): every frame decodes; a
+- C3 and C5 at their full size (65,536 streams x 32 frames): every frame decodes; a
   stride sample of 256 streams matches the oracle within 1 LSB (oracle on a
   host thread pool); two calls of 16 frames are bit-identical to one call
   of 32 (state resident in HBM); a stream decodes the same alone as inside
@@ -42,15 +42,17 @@ def _oracle_check(buf, offs, sizes, pcm, infos, streams):
         return max(ex.map(one, streams))
 
 
-def test_c3_full_size_properties():
+def _full_size_properties(cfg, base):
     n, F = 65536, 32
-    buf, offs, sizes = _gen.batch(_gen.C3, shard.BASE_SEED_C3, n, F, threads=16)
+    buf, offs, sizes = _gen.batch(cfg, base, n, F, threads=16)
     d_in = torch.from_numpy(buf).cuda()
     pcm = torch.empty((n, F, 2304), dtype=torch.int16, device="cuda")
     inf = torch.zeros((n, F, 6), dtype=torch.int32, device="cuda")
-    dec = mp3_amd.BatchDecoder(n, F)
+    dec = mp3_amd.BatchDecoder(n, F)  # >= 256 streams: the wide k_walk + k_mdcopy demux
     dec.decode(d_in, offs, sizes, F, pcm=pcm, infos=inf)
     torch.cuda.synchronize()
+    # every generated frame is a valid MPEG-1 Layer III frame: 1152 samples
+    # per channel each (the generator's truth: no junk, no dropped frames)
     assert int((inf[..., 5] == 1152).sum()) == n * F
     # the same streams in two calls of 16 frames: bit-identical (state in HBM)
     infs = inf.cpu().numpy()
@@ -72,6 +74,23 @@ def test_c3_full_size_properties():
         data = np.frombuffer(bytes(buf[offs[s]:offs[s] + sizes[s]]), np.uint8)
         p1, _ = mp3_amd.BatchDecoder(1, F).decode(data, [0], [len(data)], F)
         assert np.array_equal(p1[0], host_pcm[s]), s
+    return infos
+
+
+def test_c3_full_size_properties():
+    _full_size_properties(_gen.C3, shard.BASE_SEED_C3)
+
+
+def test_c5_full_size_properties():
+    """BASELINE configs[4] at its bench size: the mixed
+    corpus (VBR, mono / stereo / M/S / IS, 32 / 44.1 / 48 kHz, short + mixed
+    blocks, CRC) through the default wide demux path, with bench.py's own
+    seed base."""
+    infos = _full_size_properties(_gen.C5, 5_000_011)
+    # the corpus really is mixed at this size
+    assert set(np.unique(infos["hz"])) == {32000, 44100, 48000}
+    assert set(np.unique(infos["channels"])) == {1, 2}
+    assert len(np.unique(infos["bitrate_kbps"])) == 14
 
 
 def _free_port():

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Phase times of k_frame inside the per-frame call (diagnostic).  Run with
-MP3D_LIB=abx/FRT.so (abx/variants.py FRT): after every mp3d_decode_frame the
+MP3D_LIB=build_ab/FRT.so (abx/variants.py FRT): after every mp3d_decode_frame the
 variant's g_fdbg holds s_memtime at kernel start, after wave 0's frame
 staging and demux, after waves 1-3's table staging, after the barriers, at each
 wave's Huffman end, after the synthesis and after the completion fence.  Prints medians (us) as one
@@ -20,7 +20,7 @@ sys.path.insert(0, str(ROOT / "tests"))
 
 
 def main():
-    assert os.environ.get("MP3D_LIB", "").endswith("FRT.so"), "set MP3D_LIB=abx/FRT.so"
+    assert os.environ.get("MP3D_LIB", "").endswith("FRT.so"), "set MP3D_LIB=build_ab/FRT.so"
     import _gen
     import mp3_amd
     data, offs = _gen.stream(_gen.C3, 7_000_001, 300)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Where k_huffman wave time goes (diagnostic; MP3D_LIB=abx/HT.so from
+"""Where k_huffman wave time goes (diagnostic; MP3D_LIB=build_ab/HT.so from
 abx/htime.py): one C3 decode step (65 536 x 32 by default), then the summed
 per-wave cycles of its stages (ranking, round set-up, staging,
 scalefactors, big_values, count1, meta) as fractions, and cycles per unit
@@ -18,7 +18,7 @@ sys.path.insert(0, str(ROOT / "tests"))
 
 
 def main():
-    assert os.environ.get("MP3D_LIB", "").endswith("HT.so"), "set MP3D_LIB=abx/HT.so"
+    assert os.environ.get("MP3D_LIB", "").endswith("HT.so"), "set MP3D_LIB=build_ab/HT.so"
     import torch
     import _gen
     import mp3_amd

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Where k_synth's wave time goes (diagnostic; MP3D_LIB=abx/PT.so from
+"""Where k_synth's wave time goes (diagnostic; MP3D_LIB=build_ab/PT.so from
 abx/ptime.py): one C3 decode step (65 536 x 32 by default), then the summed
 per-wave cycles of phases Q, I, M, W and the loop head as fractions, and
 cycles per granule per wave."""
@@ -17,7 +17,7 @@ sys.path.insert(0, str(ROOT / "tests"))
 
 
 def main():
-    assert "abx/PT" in os.environ.get("MP3D_LIB", ""), "set MP3D_LIB=abx/PT.so (or PT2.so)"
+    assert "build_ab/PT" in os.environ.get("MP3D_LIB", ""), "set MP3D_LIB=build_ab/PT.so (or PT2.so)"
     import torch
     import _gen
     import mp3_amd
