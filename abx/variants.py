@@ -356,6 +356,18 @@ def _pad(n):
              "                    }\n" % (n, n - 1, n - 1))]
 
 
+# round 4: the partial-sum history / 4-wave k_synth at the old 3-wave budget
+VARS["S3W"] = [("amdgpu_waves_per_eu(SynCfg<SRC_XR, LSF>::DMA ? 4 : 3, 8)", "amdgpu_waves_per_eu(3, 8)")]
+
+# round 4: k_huffman back at 4-wave workgroups (3 per CU; 161 VGPRs at LDS 53 KB) beside the 16-wave one
+VARS["H4"] = [("#define HUFF_WAVES 16", "#define HUFF_WAVES 4"),
+              ("#define HUFF_CAPW 2304", "#define HUFF_CAPW 2336"),
+              ("    blocks = blocks < n_cu ? (blocks > 0 ? blocks : 1) : n_cu;", "    blocks = blocks > 0 ? blocks : 1;")]
+
+# round 4: the 8-wave k_synth with the is[] prefetch back in registers (no LDS-DMA)
+VARS["NODMA"] = [("        if (PAR) {\n            dma_is(g, nz0, nz1);", "        if (false) {\n            dma_is(g, nz0, nz1);"),
+                 ("cis[c][i] = PAR ? isq[320 * c + 64 * i + lane] : nis[c][i];", "cis[c][i] = nis[c][i];")]
+
 VARS["PAD128"] = _pad(128)
 VARS["PAD64"] = _pad(64)
 

@@ -72,6 +72,9 @@ C2_BYTES_PER_FRAME = 2 * 2 * 576 * 4 + PCM_BYTES_PER_FRAME
 C2_FLOP_PER_FRAME = FLOP_PER_FRAME  # IMDCT + matrixing + window (requantise is outside C2)
 
 
+_json_out = sys.stdout  # the JSON line's stream (main() points it at the real stdout)
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -413,10 +416,16 @@ def main():
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
+    # stdout carries exactly the one JSON line: anything a library prints
+    # there (RCCL's version banner at communicator set-up, ...) goes to stderr
+    global _json_out
+    _json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     if args.config == 1:
         if args.gpus != 1:
             raise SystemExit("config 1 is a single-stream, single-GPU workload")
-        print(json.dumps(run_per_frame(args)), flush=True)
+        print(json.dumps(run_per_frame(args)), file=_json_out, flush=True)
         return
 
     import torch
@@ -594,7 +603,7 @@ def main():
         res["gather"] = gather
     if streaming:
         res["streaming"] = streaming
-    print(json.dumps(res), flush=True)
+    print(json.dumps(res), file=_json_out, flush=True)
     if use_group:
         dist.destroy_process_group()
 

@@ -29,7 +29,7 @@ hipError_t upload_demux_constants(const uint16_t *);
 void launch_demux(const uint8_t *, const uint64_t *, const uint32_t *, uint8_t *, const uint64_t *, StreamState *,
                   FrameRec *, uint64_t *, void *, int, int, int, bool, hipStream_t);
 void launch_huffman(const uint8_t *, const uint64_t *, const FrameRec *, const uint64_t *, const DevTables *, int16_t *,
-                    UnitMeta *, int, int, int, bool, hipStream_t);
+                    UnitMeta *, int, int, int, bool, uint32_t *, uint32_t *, hipStream_t);
 void launch_synth(const FrameRec *, const int16_t *, const UnitMeta *, const DevTables *, StreamState *, void *, bool, int,
                   int, int, int, float *, const float *, hipStream_t);
 void launch_synth_xr(const float *, const uint8_t *, const uint8_t *, const DevTables *, StreamState *, int16_t *, int,
@@ -335,6 +335,10 @@ struct mp3d_batch {
         uint32_t *in_len() const { return (uint32_t *)(d + 2 * (size_t)n); }
     } geo[2];
     int geo_i = 0;
+    /* k_huffman's super-chunk counter (device; reset by each launch's memset
+     * on the call's stream, and a handle's calls are ordered) */
+    uint32_t *d_work = nullptr;
+    uint32_t work_base = 0; /* unused ticket base (launch_huffman signature) */
     hipStream_t copy = nullptr;
     mp3d_frame_info *d_infos = nullptr;
     uint8_t *md = nullptr;
@@ -526,6 +530,7 @@ extern "C" int mp3d_batch_create(int device, int max_streams, int max_frames, mp
     BALLOC(b->meta, sizeof(UnitMeta) * units);
     for (auto &g : b->geo) BALLOC(g.d, 20 * (size_t)max_streams);
     BALLOC(b->d_infos, sizeof(mp3d_frame_info) * (size_t)max_streams * max_frames);
+    BALLOC(b->d_work, 256);
 #undef BALLOC
     bool ok = hipStreamCreateWithFlags(&b->own, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&b->copy, hipStreamNonBlocking) == hipSuccess &&
@@ -539,7 +544,8 @@ extern "C" int mp3d_batch_create(int device, int max_streams, int max_frames, mp
         return MP3D_E_HIP;
     }
     for (int i = 0; i < 4; i++) (void)hipEventCreate(&b->ev[i]);
-    if (hipMemset(b->st, 0, sizeof(StreamState) * max_streams) != hipSuccess) {
+    if (hipMemset(b->st, 0, sizeof(StreamState) * max_streams) != hipSuccess ||
+        hipMemset(b->d_work, 0, 256) != hipSuccess) {
         mp3d_batch_destroy(b);
         return MP3D_E_HIP;
     }
@@ -553,7 +559,7 @@ extern "C" void mp3d_batch_destroy(mp3d_batch *b) {
     if (b->ev_done) (void)hipEventSynchronize(b->ev_done);
     if (b->own) (void)hipStreamSynchronize(b->own);
     if (b->copy) (void)hipStreamSynchronize(b->copy);
-    void *ptrs[] = {b->st, b->rec, b->sideu, b->is_buf, b->meta, b->geo[0].d, b->geo[1].d,
+    void *ptrs[] = {b->st, b->rec, b->sideu, b->is_buf, b->meta, b->geo[0].d, b->geo[1].d, b->d_work,
                     b->d_infos, b->md, b->d_in, b->d_pcm, b->d_xr, b->d_bt, b->d_mx, b->st_tail[0], b->st_tail[1]};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
@@ -713,7 +719,7 @@ static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offse
                  dev_infos ? (void *)dev_infos : b->d_infos, n, F, b->opts, demux_wide(n), s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[1], s));
     launch_huffman(b->md, g.md_off(), b->rec, b->sideu, dc.tables, b->is_buf, b->meta, n, F, dc.n_cu,
-                   huffman_wave(n * F * 4), s);
+                   huffman_wave(n * F * 4), b->d_work, &b->work_base, s);
     HIPCHK(hipEventRecord(g.freed, s)); /* the slot's last reader */
     b->geo[b->geo_i].fresh = true;
     if (b->timing) HIPCHK(hipEventRecord(b->ev[2], s));

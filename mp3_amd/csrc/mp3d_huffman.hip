@@ -9,11 +9,15 @@
 namespace mp3d {
 
 /* k_huffman: one lane per unit (its layout constants and helpers: mp3d_huffman_dev.h) */
+/* work: the handle's super-chunk counter; this launch's tickets start at
+ * ticket0 (every wave takes tickets until one is past the last super-chunk,
+ * so a launch consumes n_super + its wave count: the host advances its copy) */
 __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restrict__ md, const uint64_t *__restrict__ md_off,
                                                         const FrameRec *__restrict__ rec,
                                                         const uint64_t *__restrict__ sideu,
                                                         const DevTables *__restrict__ tab, int16_t *__restrict__ is_buf,
-                                                        UnitMeta *__restrict__ meta, int n_units, int F) {
+                                                        UnitMeta *__restrict__ meta, int n_units, int F,
+                                                        uint32_t *__restrict__ work, uint32_t ticket0) {
     __shared__ __attribute__((aligned(16))) uint16_t s_lut[MP3D_LUT_MAX];
     /* per-wave staging areas after a 4-word guard: win64g / win32g read the
      * word below a window that starts on a word boundary */
@@ -26,8 +30,8 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
      * one v_perm_b32 (sign-extension selectors read odd bytes only) */
     __shared__ uint32_t s_c1s[256];
     huff_tables_lane(tab, s_lut, s_tsel, s_lbnd, s_slen);
-    static_assert(HUFF_BLOCK == 256, "s_c1s: one entry per thread");
-    {
+    static_assert(HUFF_BLOCK >= 256, "s_c1s: one entry per thread");
+    if (threadIdx.x < 256) {
         const uint32_t v = threadIdx.x >> 4, s4 = threadIdx.x & 15u;
         int q[4], j = 0;
 #pragma unroll
@@ -48,7 +52,11 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
     const uint32_t c1b_base = ((qbase + (1u << qb1) + 1u) & ~1u) + MP3D_C1B_OFF;
     const int n_super = (n_units + HUFF_SUPER - 1) / HUFF_SUPER;
 
-    for (int sc = blockIdx.x * HUFF_WAVES + wv; sc < n_super; sc += gridDim.x * HUFF_WAVES) {
+    for (;;) {
+        uint32_t t = 0u;
+        if (lane == 0) t = atomicAdd(work, 1u) - ticket0;
+        const int sc = (int)__builtin_amdgcn_readfirstlane(t);
+        if ((uint32_t)sc >= (uint32_t)n_super) break;
         /* ---- order the super-chunk's units by big_values (counting sort in
          * LDS: histogram by ds_add_rtn, wave scan), so each 64-unit round
          * holds units of similar length -- the big_values loop runs
@@ -75,12 +83,7 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                 c[k] = bits[5 * lane + k];
                 sum += c[k];
             }
-            uint32_t incl = sum;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t t = __shfl_up(incl, o);
-                if (lane >= o) incl += t;
-            }
+            const uint32_t incl = wave_incl_scan(sum);
             uint32_t run = incl - sum;
 #pragma unroll
             for (int k = 0; k < 5; k++) {
@@ -132,21 +135,13 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
             /* words [w0, w0 + len): through the unit end + 2 words of window
              * margin, rounded to 4 words (16-B LDS stores) */
             const uint32_t len = dec ? ((((start + p23 + 31) >> 5) + 2 - w0 + 3) & ~3u) : 0u;
-            uint32_t incl = len;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t t = __shfl_up(incl, o);
-                if (lane >= o) incl += t;
-            }
+            const uint32_t incl = wave_incl_scan(len);
             const uint32_t off = incl - len;
             const uint32_t *src = (const uint32_t *)(md + (dec ? mdo : 0)) + w0;
 
             bool pending = dec;
             while (__ballot(pending)) {
-                uint32_t mo = pending ? off : 0xFFFFFFFFu;
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) mo = min(mo, (uint32_t)__shfl_xor(mo, o));
-                const uint32_t base = mo;
+                const uint32_t base = wave_min(pending ? off : 0xFFFFFFFFu);
                 const bool inb = pending && off + len - base <= HUFF_STAGEW;
                 wave_sync();
                 /* stage: each lane copies its own segment, 4 x 16 B in flight */
@@ -393,22 +388,28 @@ __global__ void __launch_bounds__(64 * HW_UNITS) k_huffman_wave(const uint8_t *_
 /* ------------------------------------------------------------------------ */
 /* wave: one wave per unit (k_huffman_wave; small batches), else one lane
  * per unit (k_huffman) */
+/* work: k_huffman's super-chunk counter (4 B of device memory per handle) */
 void launch_huffman(const uint8_t *md, const uint64_t *md_off, const FrameRec *rec, const uint64_t *sideu,
                     const DevTables *tab, int16_t *is_buf, UnitMeta *meta, int n_streams, int F, int n_cu, bool wave,
-                    hipStream_t strm) {
+                    uint32_t *work, uint32_t *base, hipStream_t strm) {
     int n_units = n_streams * F * 4;
     int supers = (n_units + HUFF_SUPER - 1) / HUFF_SUPER;
-    /* one super-chunk per wave, no grid-stride: the hardware hands out
-     * blocks as CUs free up, so uneven super-chunks balance themselves */
+    /* one workgroup per CU (its LDS is the whole CU's), fewer when there
+     * are fewer super-chunks than waves; the waves take super-chunks from the
+     * counter as they finish, so uneven super-chunks balance themselves */
     int blocks = (supers + HUFF_WAVES - 1) / HUFF_WAVES;
-    (void)n_cu;
+    blocks = blocks < n_cu ? (blocks > 0 ? blocks : 1) : n_cu;
     if (wave) {
         hipLaunchKernelGGL(k_huffman_wave, dim3((n_units + HW_UNITS - 1) / HW_UNITS), dim3(64 * HW_UNITS), 0, strm, md,
                            md_off, rec, sideu, tab, is_buf, meta, n_units, F);
         return;
     }
+    /* the counter restarts at 0 with every launch (a memset node of a few
+     * us): a launch that failed can never leave the next one's tickets off */
+    (void)hipMemsetAsync(work, 0, sizeof(uint32_t), strm);
     hipLaunchKernelGGL(k_huffman, dim3(blocks), dim3(HUFF_BLOCK), 0, strm, md, md_off, rec, sideu, tab, is_buf, meta,
-                       n_units, F);
+                       n_units, F, work, 0u);
+    (void)base;
 }
 
 } // namespace mp3d

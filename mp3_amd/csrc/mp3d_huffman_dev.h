@@ -23,13 +23,42 @@ namespace mp3d {
 /* runs max(big_values) iterations per wave whatever the region tables.     */
 /* Side info arrives pre-extracted by k_demux (one u64 per unit).           */
 /* ------------------------------------------------------------------------ */
-#define HUFF_WAVES 4
+/* One 16-wave workgroup per CU (4 waves per SIMD at <= 128 VGPRs), sharing
+ * one copy of the LUT; the waves take super-chunks from a work counter
+ * (persistent).  4-wave workgroups held 3 LUT copies per CU and fit only 3
+ * waves per SIMD beside the staging areas. */
+#define HUFF_WAVES 16
 #define MP3D_C1B_OFF 2 /* count1 table B after the zero table (huff_tables_lane) */
 #define HUFF_ROUNDS 4                    /* 64-unit rounds per super-chunk          */
 #define HUFF_SUPER (64 * HUFF_ROUNDS)    /* units ranked together by big_values     */
 #define HUFF_BLOCK (64 * HUFF_WAVES)
-#define HUFF_CAPW 2336 /* LDS words per wave (9.3 KB): staging + round order; 3 workgroups of 4 waves per CU with the count1 sign table */
+#define HUFF_CAPW 2304 /* LDS words per wave (9.2 KB): staging + round order; 16 waves + the tables in 160 KB */
 #define HUFF_STAGEW (HUFF_CAPW - HUFF_SUPER / 2) /* staging words; the u16 order follows */
+
+/* wave-wide scan / min by ds_bpermute with the lane id re-derived at each
+ * use (HIP's __shfl_up / __shfl_xor add width bounds whose lane-derived
+ * constants the compiler held across the super-chunk loop and spilled at
+ * 128 VGPRs; a spill reload's vmcnt(0) then waited for the row stores) */
+__device__ __forceinline__ int lane_now() {
+    int l = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    __asm__ volatile("" : "+v"(l));
+    return l;
+}
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int l = lane_now();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = (uint32_t)__builtin_amdgcn_ds_bpermute((l - o) << 2, (int)v);
+        if (l >= o) v += t;
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+    const int l = lane_now();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) v = min(v, (uint32_t)__builtin_amdgcn_ds_bpermute((l ^ o) << 2, (int)v));
+    return v;
+}
 
 /* 32 bits of a staged (big-endian word) bitstream starting at bit pos (the
  * scalefactor readers; a 64-bit funnel shift, so sh = 0 needs no case) */

@@ -55,6 +55,7 @@ __device__ __forceinline__ void dct3_9(const float *a, float *v) {
 
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <bool V> struct BoolC { static constexpr bool value = V; }; /* a compile-time flag argument */
 __device__ __forceinline__ f32x2 pfma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f32x2 bc(float c) { return (f32x2){c, c}; }
 
@@ -167,7 +168,6 @@ __device__ __forceinline__ void imdct36_w(const float *X, float *w) {
 /* frame, LSF rates and intensity ratios) -- each launch decodes only the  */
 /* streams of its MPEG family (StreamState.kind).                           */
 /* ------------------------------------------------------------------------ */
-#define SYN_WAVES 4
 #define SROW 36      /* LDS row stride of S (floats): 16-B rows, few conflicts */
 #define SYN_BUF 1296 /* floats: max(xr 2x576, S 36x36, X 36x36)              */
 #define XROW 36      /* LDS row stride of X: 16-B rows, conflict-free b128 writes;
@@ -208,7 +208,11 @@ template <bool LSF> struct SynShared { /* read-only, one copy per workgroup     
      * rates 0..2, or the six LSF rates 3..8                                */
     uint32_t lpair[LSF ? 6 : 3][3][288];
     float ce[16][16], co[16][16];    /* matrixing A: C[2m][i], C[2m+1][i], i < 16  */
-    float dw[32][16];                /* window taps per output j                   */
+    /* window taps as (D[j][2i], D[j][2i + 1]) pairs, tap-pair major: step i
+     * of the window reads dwp[i][j], 8 B per lane at consecutive addresses,
+     * conflict-free (as dw[j][16], a ds_read_b64 of 32 lanes 64 B apart
+     * was an 8-way bank conflict) */
+    f32x2 dwp[8][32];
     float p43s[512];                 /* sign(k - 256) |k - 256|^(4/3), k < 512     */
     /* long-block windows (x IMDCT output scale) in output pairs (i, 17 - i)
      * of both halves, wp[par][bt][i] = (w[i], w[17 - i], w[18 + i],
@@ -220,17 +224,30 @@ template <bool LSF> struct SynShared { /* read-only, one copy per workgroup     
      * then the DCT-IV output scales (K, -K) (IMDCT36_K) */
     f32x2 kc[7 + 9];
     float p2q[4]; /* 2^(i/4): pow2_quarter's mantissas, a branch-free lookup */
+    uint16_t xcol[2][64]; /* phase W: lane (ch, j)'s X offsets in buf, columns win_a[j], win_b[j] */
     float isr[LSF ? 32 : 7][2];      /* intensity ratios: MPEG-1 [is_pos], LSF      */
                                      /* [intensity_scale * 16 + is_pos]            */
 };
+#define SYN_QOFF 1152 /* floats: phase Q's own data sits after the xr scatter area */
 struct __attribute__((aligned(256))) SynWave { /* one per wave (stream)       */
-    /* 2^(q/4) per (ch, band idx): long b | 22 + 3 b + w.  256-B aligned rows,
-     * so a line pair's scale address is base | (lpair & 0xFC): one VALU op */
-    float scale[2][64];
-    float buf[SYN_BUF];              /* xr -> S -> X hand-offs                     */
-    UnitMeta m[2];
-    uint8_t is[64];                  /* intensity position per right band idx, 0xFF none */
+    /* buf: xr -> S -> X hand-offs.  Phase Q's band scales, UnitMeta words and
+     * intensity positions live only while buf holds xr (2 x 576 floats), so
+     * they share buf's tail: 5.4 KB per wave, 39.4 KB per 4-wave workgroup
+     * (<= 40 KB: 4 workgroups per CU) */
+    union {
+        float buf[SYN_BUF];
+        struct {
+            float xr_[SYN_QOFF];
+            /* 2^(q/4) per (ch, band idx): long b | 22 + 3 b + w.  256-B
+             * aligned rows, so a line pair's scale address is base |
+             * (lpair & 0xFC): one VALU op */
+            float scale[2][64];
+            UnitMeta m[2];
+            uint8_t is[64]; /* intensity position per right band idx, 0xFF none */
+        };
+    };
 };
+static_assert(SYN_QOFF * 4 % 256 == 0, "SynWave::scale rows 256-B aligned");
 typedef __attribute__((address_space(3))) const float lds_cf32;
 
 /* per-lane select on a wave mask, opaque to the optimizer: written as
@@ -245,6 +262,7 @@ __device__ __forceinline__ float lane_sel(uint64_t m, float f, float t) {
 #define WAIT_VMCNT0() __builtin_amdgcn_s_waitcnt(0x0F70) /* vmcnt(0), other counters free */
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 
 /* the workgroup's read-only tables, staged by NT threads (tid = 0 .. NT - 1;
@@ -265,12 +283,17 @@ __device__ __forceinline__ void synth_tables(SynShared<LSF> &T, const DevTables 
     /* int16 sinks: taps x 32768 (exact, a power of two), so the sums
      * arrive in PCM units without a multiply per sample */
     for (int i = tid; i < 32 * 16; i += NT)
-        (&T.dw[0][0])[i] = (&tab->dwin[0][0])[i] * (F32 ? 1.0f : 32768.0f);
+        ((float *)&T.dwp[0][0])[((i & 15) >> 1) * 64 + (i >> 4) * 2 + (i & 1)] = (&tab->dwin[0][0])[i] * (F32 ? 1.0f : 32768.0f);
     if (tid < 7 + 9) {
         const float c9[7] = DCT9_KC, k9[9] = IMDCT36_K;
         T.kc[tid] = tid < 7 ? (f32x2){c9[tid], c9[tid]} : (f32x2){k9[tid - 7], -k9[tid - 7]};
     }
     if (tid < 4) T.p2q[tid] = pow2_quarter(tid);
+    if (tid < 128) {
+        const int l = tid & 63, c = l >> 5, j = l & 31;
+        const int w = (tid >> 6) ? tab->win_b[j] : tab->win_a[j];
+        T.xcol[tid >> 6][l] = (uint16_t)(18 * c * XROW + (w & 1) * 16 + (w >> 1));
+    }
     for (int k = tid; k < 2 * 4 * 9; k += NT) {
         const int par = k / 36, bt = (k / 9) % 4, i = k % 9;
         const float *w = c_win36[bt];
@@ -306,7 +329,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                                              void *__restrict__ pcm, int F, int xr_nch, int xr_sr, int seg_len,
                                              float *__restrict__ st_tail, const float *__restrict__ st_tail_in,
                                              SynShared<LSF> &T, SynWave &Wd, int s, int seg, int nseg,
-                                             float *xch = nullptr) {
+                                             float *xch = nullptr, uint32_t *isq = nullptr) {
     static_assert(PF == 0 || (!SRC_XR && !LSF), "PF: k_frame's MPEG-1 decode path only");
     const int f0 = seg * seg_len, f1 = min(F, f0 + seg_len);
     /* first frame decoded (warm-up frames below f0 leave state, no PCM) and
@@ -358,16 +381,20 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
     constexpr int MW = (int)(sizeof(UnitMeta) / 4); /* 14 words per unit */
 
     StreamState &S = st[s];
-    const int wa = tab->win_a[sb], wb = tab->win_b[sb];
     /* IMDCT overlap in output pairs ovp[i] = (ov[i], ov[17 - i]), with the
      * odd slots of odd subbands negated (the frequency inversion folded into
      * the window tables, SynShared::wp); state in and out as true values */
     f32x2 ovp[9];
     const float sgo = (sb & 1) ? -1.f : 1.f; /* slot sign of odd slots */
     const f32x2 sgp[2] = {(f32x2){1.f, sgo}, (f32x2){sgo, 1.f}}; /* pair i even / odd */
-    /* synthesis history: ha[k] = X_{k-14}[wa], hb[k] = X_{k-15}[wb] (slot
-     * index relative to the granule's first slot; fifo[t] = slot t - 15)  */
-    float ha[14], hb[15];
+    /* synthesis history as partial sums: the
+     * window terms of the NEXT granule's output slots t = 0 .. 14 that read
+     * this granule's matrixing outputs (slot t's taps i with t - 2 i < 0, or
+     * t - 2 i - 1 < 0), summed when this granule's X is at hand.  hp[tp] =
+     * (H_2tp, H_2tp+1) for lane (ch, j); H_15 = 0.  16 registers instead of
+     * the 29 raw X values (ha / hb) the window read them from before.
+     * StreamState.fifo[ch][t][j] holds H_t. */
+    f32x2 hp[8];
     constexpr int TAIL = (int)(sizeof(S.overlap) + sizeof(S.fifo)) / 4; /* floats per stream tail */
     if (from_state || (ch1_state && ch == 1)) {
         /* state in: StreamState, or the previous call's tail (the same
@@ -378,16 +405,14 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
         for (int i = 0; i < 9; i++)
             ovp[i] = (f32x2){ovi[(ch * 32 + sb) * 18 + i], ovi[(ch * 32 + sb) * 18 + 17 - i]} * sgp[i & 1];
 #pragma unroll
-        for (int k = 0; k < 14; k++) ha[k] = ffi[(ch * MP3D_FIFO_SLOTS + k + 1) * 32 + wa];
-#pragma unroll
-        for (int k = 0; k < 15; k++) hb[k] = ffi[(ch * MP3D_FIFO_SLOTS + k) * 32 + wb];
+        for (int tp = 0; tp < 8; tp++)
+            hp[tp] = (f32x2){ffi[(ch * MP3D_FIFO_SLOTS + 2 * tp) * 32 + sb],
+                             2 * tp + 1 < MP3D_FIFO_SLOTS ? ffi[(ch * MP3D_FIFO_SLOTS + 2 * tp + 1) * 32 + sb] : 0.f};
     } else {
 #pragma unroll
         for (int i = 0; i < 9; i++) ovp[i] = (f32x2){0.f, 0.f};
 #pragma unroll
-        for (int k = 0; k < 14; k++) ha[k] = 0.f;
-#pragma unroll
-        for (int k = 0; k < 15; k++) hb[k] = 0.f;
+        for (int tp = 0; tp < 8; tp++) hp[tp] = (f32x2){0.f, 0.f};
     }
 
     /* Per-stream buffer resources: every granule access below is a buffer
@@ -415,6 +440,11 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
      * loop-carried register directly; otherwise slot 0 = the current
      * granule, slot 1 the next, shifted after each prefetch. */
     constexpr bool PAR = !SRC_XR && !LSF && PF == 0;
+    /* PAR (the batch's MPEG-1 decode, 8-wave workgroups): the is[] words go
+     * by LDS-DMA (buffer_load ... lds) into the wave's isq area [ch][320]
+     * (256-B pieces; the fifth piece's upper half is padding) instead of
+     * ten registers held through phases I, M and W: the register budget
+     * of 4 waves per SIMD.  Otherwise into nis. */
     uint32_t nis[2][5], wm[2] = {0u, 0u}, wr[2] = {0u, 0u};
     constexpr int GSTEP = LSF ? 2 : 1; /* is[] granule slots per decoded granule */
     /* two unconditional loads; a lane outside a word range gets an offset
@@ -428,7 +458,50 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
         vm = __builtin_amdgcn_raw_buffer_load_b32(r_meta, om, g * 2 * (int)sizeof(UnitMeta), 0);
         vr = __builtin_amdgcn_raw_buffer_load_b32(r_rec, orr, (g >> 1) * (int)sizeof(FrameRec), 0);
     };
+    /* The LDS-DMA as inline asm, one block per channel: M0 = the channel's
+     * LDS area (saved and restored), the five 256-B pieces at instruction
+     * offsets 0 .. 1024 (the offset moves the memory AND the LDS address:
+     * LDS = M0 + offset + 4 lane, probed on the box, tools/dbg/
+     * lds_dma_probe.hip), and a descriptor per channel whose byte range is the
+     * row's nonzero prefix (2 nz_end bytes): every word at or past nz_end,
+     * and past the row, reads as 0, with no per-lane offset arithmetic.  As
+     * __builtin_amdgcn_raw_ptr_buffer_load_lds the compiler's wait-count
+     * pass, which cannot tell these LDS writes from the kernel's other LDS
+     * accesses, waited for the DMA (vmcnt) before every later LDS read --
+     * the prefetch turned synchronous.  Completion is the kernel's own
+     * vmcnt(0) before phase W (and after prefetch_full); the hardware counts
+     * these loads like any other, so the compiler's counted waits for its
+     * own loads can only over-wait. */
+    const uint64_t isb = (uint64_t)(uintptr_t)(is_buf + (size_t)s * F * 4 * 576);
+    auto dma_is = [&](int g, int nz0, int nz1) {
+        const int lo = opaque(lane * 4);
+        const uint32_t lds0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uintptr_t)(lds_cf32 *)(const float *)isq);
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            const uint64_t ra = isb + (uint64_t)(uint32_t)(g * gb + c * 1152);
+            const u32x4 rs = {(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)ra),
+                              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(ra >> 32)) & 0xFFFFu,
+                              (uint32_t)__builtin_amdgcn_readfirstlane(2 * (c ? nz1 : nz0)), 0x00020000u};
+            uint32_t keep;
+            __asm__ volatile("s_mov_b32 %0, m0\n\t"
+                             "s_mov_b32 m0, %2\n\t"
+                             "s_nop 0\n\t"
+                             "buffer_load_dword %1, %3, 0 offen lds\n\t"
+                             "buffer_load_dword %1, %3, 0 offen offset:256 lds\n\t"
+                             "buffer_load_dword %1, %3, 0 offen offset:512 lds\n\t"
+                             "buffer_load_dword %1, %3, 0 offen offset:768 lds\n\t"
+                             "buffer_load_dword %1, %3, 0 offen offset:1024 lds\n\t"
+                             "s_mov_b32 m0, %0"
+                             : "=&s"(keep)
+                             : "v"(lo), "s"(lds0 + 1280u * c), "s"(rs)
+                             : "memory");
+        }
+    };
     auto load_is = [&](int g, int nz0, int nz1) {
+        if (PAR) {
+            dma_is(g, nz0, nz1);
+            return;
+        }
         const int lo = opaque(lane * 4);
 #pragma unroll
         for (int c = 0; c < 2; c++) {
@@ -587,7 +660,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
 #pragma unroll
                 for (int c = 0; c < 2; c++)
 #pragma unroll
-                    for (int i = 0; i < 5; i++) cis[c][i] = nis[c][i];
+                    for (int i = 0; i < 5; i++) cis[c][i] = PAR ? isq[320 * c + 64 * i + lane] : nis[c][i];
                 /* UnitMeta into LDS for the (rare) intensity path; the common
                  * path reads the prefetched words straight from registers */
                 if (lane < nch * MW) ((uint32_t *)&Wd.m[0])[lane] = wm[cs]; /* lane / MW < nch, no division */
@@ -615,7 +688,10 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                 /* 2^(q/4) = ldexp(2^((q & 3) / 4), q >> 2): the mantissa from a
                  * 4-entry LDS table (as a select chain the compiler built
                  * divergent branches) */
-                const float msf = ms_fold ? isq : 1.f; /* uniform: one multiply, no select */
+                /* uniform: one multiply, no select; the select on integer
+                 * bits so it stays scalar (as a float select its constant was
+                 * held in a VGPR across the loop) */
+                const float msf = __int_as_float(__builtin_amdgcn_readfirstlane(ms_fold ? 0x3f3504f3 : 0x3f800000));
                 auto p2q = [&](int q) { return ldexpf(T.p2q[q & 3], q >> 2) * msf; };
                 if (var[0] == 0 && (nch == 1 || var[1] == 0)) {
                     /* long blocks in every coded channel (the common case): both
@@ -666,7 +742,6 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                                              (uint32_t)(uintptr_t)(lds_cf32 *)&Wd.scale[1][0]};
 #pragma unroll
                 for (int i = 0; i < 5; i++) {
-                    const int l0 = 2 * lane + 128 * i;
                     const bool ok = i < 4 || lane < 32;
 #pragma unroll
                     for (int c = 0; c < 2; c++) {
@@ -689,7 +764,6 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                      * stays branch-free and its LDS reads batch */
 #pragma unroll
                     for (int i = 0; i < 5; i++) {
-                        const int l0 = 2 * lane + 128 * i;
 #pragma unroll
                         for (int c = 0; c < 2; c++) {
 #pragma unroll
@@ -721,7 +795,6 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                     uint64_t nzR = 0;
 #pragma unroll
                     for (int i = 0; i < 5; i++) {
-                        const int l0 = 2 * lane + 128 * i;
                         const uint32_t tv2 = (i < 4 || lane < 32) ? lpair[var[1]][lane + 64 * i] : 0u;
                         if (fmaxf(fabsf(XV(1, 2 * i)), fabsf(XV(1, 2 * i + 1))) >= FLUSH)
                             nzR |= 1ull << ((tv2 >> 2) & 63u);
@@ -735,7 +808,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                         if (bt1 != 2 || (mx1 && lane < (LSF ? 6 : 8))) {
                             const int p = R.sf[lane == 21 ? 20 : lane];
                             const bool short_nz = (nzR >> 22) != 0ull;
-                            if (!short_nz && ((uint32_t)(nzR & 0x3FFFFFull) >> lane) == 0u && p < IS_ILLEGAL) ip = p;
+                            if (!short_nz && ((uint32_t)(nzR & 0x3FFFFFull) >> lane) == 0u && p < opaque(IS_ILLEGAL)) ip = p;
                         }
                     } else if (lane < 61 && bt1 == 2) {
                         const int b = (lane - 22) / 3, w = lane - 22 - 3 * b;
@@ -745,7 +818,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                             /* no nonzero line in window w at bands >= b */
                             uint64_t above = 0;
                             for (int bb = b; bb < 13; bb++) above |= 1ull << (22 + 3 * bb + w);
-                            if ((nzR & above) == 0ull && p < IS_ILLEGAL) ip = p;
+                            if ((nzR & above) == 0ull && p < opaque(IS_ILLEGAL)) ip = p;
                         }
                     }
                     /* LSF: ratio row by intensity_scale (UnitMeta.flags bit 1) */
@@ -754,7 +827,6 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                     wave_sync();
 #pragma unroll
                     for (int i = 0; i < 5; i++) {
-                        const int l0 = 2 * lane + 128 * i;
                         const uint32_t tv2 = (i < 4 || lane < 32) ? lpair[var[1]][lane + 64 * i] : 0u;
                         const int ipl = Wd.is[(tv2 >> 2) & 63u];
 #pragma unroll
@@ -762,8 +834,10 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                             const int k = 2 * i + e;
                             const float lv = XV(0, k), rv = XV(1, k);
                             if (ipl != 0xFF) {
-                                XV(0, k) = lv * T.isr[ipl][0];
-                                XV(1, k) = lv * T.isr[ipl][1];
+                                const f32x2 rr = *(const __attribute__((address_space(3))) f32x2 *)(uintptr_t)(uint32_t)(
+                                    opaque((int)(uintptr_t)(lds_cf32 *)&T.isr[0][0]) + 8 * ipl);
+                                XV(0, k) = lv * rr.x;
+                                XV(1, k) = lv * rr.y;
                             } else if (mext & 2) {
                                 XV(0, k) = (lv + rv) * isq;
                                 XV(1, k) = (lv - rv) * isq;
@@ -860,7 +934,11 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                      * from W[8 - i] = (w[8 - i], w[9 + i]) */
                     const f32x4 *wq = T.wp[sb & 1][bt == 2 ? 0 : bt];
                     f32x2 W[9];
-                    imdct36_wp(x, W, T.kc);
+                    /* the constants' LDS address from an opaque copy: the
+                     * reads then take immediate offsets from ONE register
+                     * (as absolute addresses the compiler held 8 of them live
+                     * across the loop) */
+                    imdct36_wp(x, W, (const f32x2 *)(uintptr_t)(uint32_t)opaque((int)(uintptr_t)(lds_cf32 *)(const float *)&T.kc[0]));
 #pragma unroll
                     for (int i = 0; i < 9; i++) {
                         const f32x4 q = wq[i];
@@ -870,6 +948,10 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                         nvp[i] = bc(W[8 - i].x) * (f32x2){q.z, q.w};
                     }
                 } else {
+                    /* the odd-slot sign of odd subbands, from the granule's
+                     * lane copy (held across the loop it spilled) */
+                    const float sgo = (sb & 1) ? -1.f : 1.f;
+                    const f32x2 sgp[2] = {(f32x2){1.f, sgo}, (f32x2){sgo, 1.f}};
                     /* z[6w+6+i] += y_w[i] * win12[i], w = 0..2, i = 0..11 */
                     float z[24]; /* z[6..29] */
 #pragma unroll
@@ -997,71 +1079,39 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
             if (PF == 2) { /* granule 0's synthesis history from the other wave */
                 __syncthreads();
 #pragma unroll
-                for (int k = 0; k < 14; k++) ha[k] = xch[(18 + k) * 64 + lane];
-#pragma unroll
-                for (int k = 0; k < 15; k++) hb[k] = xch[(32 + k) * 64 + lane];
+                for (int tp = 0; tp < 8; tp++)
+                    hp[tp] = (f32x2){xch[(18 + 2 * tp) * 64 + lane], xch[(19 + 2 * tp) * 64 + lane]};
             }
             {
-                float Dw[16];
+                /* the lane's X columns in buf (wa / wb of output j, ISO Annex
+                 * A matrixing folded to 32 outputs; X index k sits at (k & 1)
+                 * 16 + k / 2 of its row), one table read each: held across the
+                 * loop they spilled, recomputed they cost ~14 VALU a granule */
+                const int pa = T.xcol[0][lane], pb = T.xcol[1][lane];
+                /* loaded straight into the register pairs the packed FMAs
+                 * take: xap[m] = (xa[2m], xa[2m + 1]), xbp[m] = (xb[2m + 1],
+                 * xb[2m + 2]) (loaded as (xb[0], xb[1]), ... pairs, the odd
+                 * pairing cost a register copy per value and, at 128 VGPRs,
+                 * spills) */
+                f32x2 xap[9], xbp[8];
+                float xb0, xb17;
 #pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const float4 d = *(const float4 *)&T.dw[sb][4 * i];
-                    Dw[4 * i] = d.x; Dw[4 * i + 1] = d.y; Dw[4 * i + 2] = d.z; Dw[4 * i + 3] = d.w;
-                }
-                float xa[18], xb[18];
-                /* X index k sits at (k & 1) 16 + k / 2 of its row */
-                const int pa = opaque(18 * ch * XROW + (wa & 1) * 16 + (wa >> 1));
-                const int pb = opaque(18 * ch * XROW + (wb & 1) * 16 + (wb >> 1));
+                for (int m = 0; m < 9; m++) xap[m] = (f32x2){sBuf[pa + 2 * m * XROW], sBuf[pa + (2 * m + 1) * XROW]};
+#pragma unroll
+                for (int m = 0; m < 8; m++) xbp[m] = (f32x2){sBuf[pb + (2 * m + 1) * XROW], sBuf[pb + (2 * m + 2) * XROW]};
+                xb0 = sBuf[pb];
+                xb17 = sBuf[pb + 17 * XROW];
+                /* mono frame: channel 1 keeps its synthesis history.  Its
+                 * lanes park their partial sums in the channel-1 half of the
+                 * X buffer (rows 18..35, which only channel-1 lanes read, and
+                 * after their own reads) and take them back below */
+                const int park = opaque(18 * XROW + 16 * sb);
                 if (nch == 1) {
-                    /* mono frame: channel 1 keeps its synthesis history.  Its
-                     * lanes put the history back into the X slots it came from
-                     * (ha[k] = row k + 4 at wa, hb[k] = row k + 3 at wb; lanes
-                     * sharing a slot write the same value), so the plain
-                     * update below reloads it: no per-lane select on the
-                     * stereo path (a select there kept ~30 register copies
-                     * per granule alive: -45 VALU / granule, A/B NOSEL) */
                     if (ch == 1) {
 #pragma unroll
-                        for (int k = 0; k < 14; k++) sBuf[pa + (k + 4) * XROW] = ha[k];
-#pragma unroll
-                        for (int k = 0; k < 15; k++) sBuf[pb + (k + 3) * XROW] = hb[k];
-                    }
-                    wave_sync();
-                }
-#pragma unroll
-                for (int t = 0; t < 18; t++) {
-                    xa[t] = sBuf[pa + t * XROW];
-                    xb[t] = sBuf[pb + t * XROW];
-                }
-                /* output slots in pairs (t0, t1): lanes 0-31 hold L, lanes
-                 * 32-63 R; one half-wave swap leaves lane j with (L, R) of
-                 * slot t0 and lane 32 + j with (L, R) of slot t1 */
-                /* two output slots (2 tp, 2 tp + 1) at once: packed FMAs
-                 * (v_pk_fma_f32, tap broadcast), half the VALU issues of the
-                 * scalar form; the same fma order per slot, so bit-identical */
-                /* all 9 slot pairs accumulate side by side (tap i outer, slot
-                 * pair inner): 9 independent packed-FMA chains.  Written as one
-                 * chain per slot pair, the compiler emitted them back to back
-                 * into one register pair -- a 144-long dependent chain per
-                 * granule.  Same fma order per slot, so bit-identical. */
-                f32x2 acc[9];
-#pragma unroll
-                for (int tp = 0; tp < 9; tp++) acc[tp] = (f32x2){0.f, 0.f};
-#pragma unroll
-                for (int i = 0; i < 8; i++) {
-#pragma unroll
-                    for (int tp = 0; tp < 9; tp++) {
-                        const int ka = 2 * tp - 2 * i, kb = ka - 1;
-                        f32x2 va, vb;
-                        va.x = ka >= 0 ? xa[ka] : ha[ka + 14];
-                        va.y = ka + 1 >= 0 ? xa[ka + 1] : ha[ka + 15];
-                        vb.x = kb >= 0 ? xb[kb] : hb[kb + 15];
-                        vb.y = kb + 1 >= 0 ? xb[kb + 1] : hb[kb + 16];
-                        acc[tp] = __builtin_elementwise_fma((f32x2){Dw[2 * i], Dw[2 * i]}, va, acc[tp]);
-                        acc[tp] = __builtin_elementwise_fma((f32x2){Dw[2 * i + 1], Dw[2 * i + 1]}, vb, acc[tp]);
+                        for (int tp = 0; tp < 8; tp++) *(f32x2 *)&sBuf[park + 2 * tp] = hp[tp];
                     }
                 }
-                auto out2 = [&](int tp) { return acc[tp]; };
                 /* int16 sinks (taps pre-scaled by 32768): clamp(floor(x + 0.5)),
                  * FFmpeg's fixed-point rounding (round_sample: add half, shift),
                  * by one v_cvt_rpi_i32_f32 per sample: floor of the exact x + 0.5,
@@ -1071,66 +1121,125 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                     __asm__("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(v));
                     return r;
                 };
-                auto to_pcm = [&](float v) { return min(max(to_i32(v), -32768), 32767); }; /* v_med3_i32 */
                 const int so = f * 2304 * PB + gr * 576 * nch * PB;
-                if (f < f0) {
-                    /* warm-up frame: state only, no PCM */
-                } else if (F32) {
-                    /* float sink: the same sums, unscaled and unclipped (FFmpeg's
-                     * float decoder convention); (L, R) = 8 B per lane and slot */
-                    if (nch == 2) {
-                        const int vo = opaque((sb + 32 * ch) * 8);
-#pragma unroll
-                        for (int tp = 0; tp < 9; tp++) {
-                            const f32x2 o = out2(tp);
+                /* output slots (2 tp, 2 tp + 1): lanes 0-31 hold L, lanes 32-63
+                 * R; one half-wave swap leaves lane j with (L, R) of slot 2 tp
+                 * and lane 32 + j with (L, R) of slot 2 tp + 1 */
+                /* STEREO: a stereo frame past the warm-up (the common case):
+                 * branch-free stores, so the window loop below is one basic
+                 * block; otherwise the general sink (mono lanes, warm-up) */
+                /* the lane's PCM byte offsets, once per granule (in the
+                 * stores they were recomputed at each slot pair) */
+                const int vo_st = opaque((sb + 32 * ch) * (F32 ? 8 : 4)), vo_mo = opaque(sb * (F32 ? 4 : 2));
+                auto emit = [&](auto stereo, int tp, f32x2 o) {
+                    if (decltype(stereo)::value) {
+                        if (F32) {
+                            /* float sink: the same sums, unscaled and unclipped
+                             * (FFmpeg's float decoder convention); (L, R) = 8 B
+                             * per lane and slot */
+                            const int vo = vo_st;
                             const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(o.x), __float_as_uint(o.y),
                                                                             false, false);
                             __builtin_amdgcn_raw_buffer_store_b64((u32x2){r[0], r[1]}, r_pcm, vo + 512 * tp, so, 0);
+                        } else {
+                            /* floor(x + 0.5) -> int32, then v_cvt_pk_i16_i32
+                             * saturates to int16 and packs (L, R): 4 VALU per
+                             * slot pair */
+                            const int vo = vo_st;
+                            const int p0 = to_i32(o.x), p1 = to_i32(o.y);
+                            const auto r = __builtin_amdgcn_permlane32_swap(p0, p1, false, false);
+                            __builtin_amdgcn_raw_buffer_store_b32(
+                                __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16((int)r[0], (int)r[1])), r_pcm,
+                                vo + 256 * tp, so, 0);
                         }
-                    } else {
-                        const int vo = opaque(sb * 4);
-#pragma unroll
-                        for (int tp = 0; tp < 9; tp++) {
-                            const f32x2 o = out2(tp);
-                            if (active) {
-                                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o.x), r_pcm, vo + 256 * tp, so, 0);
-                                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o.y), r_pcm, vo + 256 * tp + 128, so, 0);
-                            }
+                    } else if (f < f0) {
+                        /* warm-up frame: state only, no PCM */
+                    } else if (nch == 2) { /* (stereo frames take the other copy) */
+                    } else if (active) {
+                        if (F32) {
+                            const int vo = vo_mo;
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o.x), r_pcm, vo + 256 * tp, so, 0);
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o.y), r_pcm, vo + 256 * tp + 128, so, 0);
+                        } else {
+                            /* saturated by v_cvt_pk_i16_i32 (a v_med3 clamp held its
+                             * 0x7fff bound in a VGPR across the loop) */
+                            const int vo = vo_mo;
+                            const uint32_t pk =
+                                __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16(to_i32(o.x), to_i32(o.y)));
+                            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)pk, r_pcm, vo + 128 * tp, so, 0);
+                            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(pk >> 16), r_pcm, vo + 128 * tp + 64, so, 0);
                         }
                     }
-                } else if (nch == 2) {
-                    const int vo = opaque((sb + 32 * ch) * 4);
-                    /* floor(x + 0.5) -> int32, then v_cvt_pk_i16_i32 saturates to
-                     * int16 and packs (L, R): 4 VALU per slot pair */
+                };
+                /* The 512-tap window (ISO Annex A: 16 taps per output sample,
+                 * alternately on columns wa and wb of the X FIFO), two output
+                 * slots at a time with packed FMAs (v_pk_fma_f32, the tap
+                 * broadcast).  Slot t = sum_i D[2i] A(t - 2i) + D[2i+1] B(t - 2i
+                 * - 1) with A / B this granule's X (index >= 0) or the previous
+                 * granule's (< 0).  Per slot ONE fma chain: the previous
+                 * granule's terms (hp, taps i ascending) first, then this
+                 * granule's (taps i ascending).  Step i (taps 2i, 2i + 1, read
+                 * from LDS at the step) advances the slot pairs tp >= i and
+                 * completes pair i (stored at once), and sums this granule's
+                 * terms of the NEXT granule's pairs tp < i into hp (pair i
+                 * starts there): at every step 9 pairs (18 registers) are live,
+                 * and the 9 chains are independent. */
+                auto window = [&](auto stereo) {
+                    f32x2 acc[9];
 #pragma unroll
-                    for (int tp = 0; tp < 9; tp++) {
-                        const f32x2 o = out2(tp);
-                        const int p0 = to_i32(o.x), p1 = to_i32(o.y);
-                        const auto r = __builtin_amdgcn_permlane32_swap(p0, p1, false, false);
-                        __builtin_amdgcn_raw_buffer_store_b32(
-                            __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16((int)r[0], (int)r[1])), r_pcm,
-                            vo + 256 * tp, so, 0);
-                    }
-                } else {
-                    const int vo = opaque(sb * 2);
+                    for (int tp = 0; tp < 8; tp++) acc[tp] = hp[tp];
+                    acc[8] = (f32x2){0.f, 0.f};
+                    const int dwo = opaque(sb);
+                    /* the taps of step i + 1 are read at the start of step i
+                     * (one step ahead, 2 registers): read at their own step,
+                     * each step waited for its LDS read */
+                    f32x2 dn = (&T.dwp[0][0])[dwo];
 #pragma unroll
-                    for (int tp = 0; tp < 9; tp++) {
-                        const f32x2 o = out2(tp);
-                        if (active) {
-                            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)to_pcm(o.x), r_pcm, vo + 128 * tp, so, 0);
-                            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)to_pcm(o.y), r_pcm, vo + 128 * tp + 64, so, 0);
+                    for (int i = 0; i < 8; i++) {
+                        const f32x2 d = dn;
+                        if (i < 7) dn = (&T.dwp[0][0])[dwo + 32 * (i + 1)];
+#pragma unroll
+                        for (int tp = i; tp < 9; tp++) {
+                            /* A = (xa[k], xa[k + 1]), B = (xb[k - 1], xb[k]), k = 2 (tp - i) */
+                            acc[tp] = pfma(bc(d.x), xap[tp - i], acc[tp]);
+                            if (tp > i)
+                                acc[tp] = pfma(bc(d.y), xbp[tp - i - 1], acc[tp]);
+                            else /* slot 2 tp + 1's B(0); slot 2 tp's B(-1) is in hp */
+                                acc[tp].y = fmaf(d.y, xb0, acc[tp].y);
                         }
+                        emit(stereo, i, acc[i]);
+                        hp[i] = (f32x2){d.y * xb17, 0.f}; /* H_2i: B(-1) = this X_17 */
+#pragma unroll
+                        for (int tp = 0; tp < i; tp++) {
+                            /* k = 2 (tp - i) + 18: A = xap[k / 2], B = xbp[k / 2 - 1] */
+                            hp[tp] = pfma(bc(d.x), xap[tp - i + 9], hp[tp]);
+                            hp[tp] = pfma(bc(d.y), xbp[tp - i + 8], hp[tp]);
+                        }
+                        /* one scheduling region per step: hoisted across the
+                         * steps, the tap reads and chains spilled at 128 VGPRs */
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                    emit(stereo, 8, acc[8]);
+                };
+                if (nch == 2 && f >= f0)
+                    window(BoolC<true>{});
+                else
+                    window(BoolC<false>{});
+                if (nch == 1) {
+                    wave_sync();
+#pragma unroll
+                    for (int tp = 0; tp < 8; tp++) {
+                        const f32x2 v = *(const f32x2 *)&sBuf[park + 2 * tp];
+                        hp[tp].x = lane_sel(amask, v.x, hp[tp].x);
+                        hp[tp].y = lane_sel(amask, v.y, hp[tp].y);
                     }
                 }
-#pragma unroll
-                for (int k = 0; k < 14; k++) ha[k] = xa[k + 4]; /* mono: channel 1 reloaded its own (above) */
-#pragma unroll
-                for (int k = 0; k < 15; k++) hb[k] = xb[k + 3];
                 if (PF == 1) {
 #pragma unroll
-                    for (int k = 0; k < 14; k++) xch[(18 + k) * 64 + lane] = ha[k];
-#pragma unroll
-                    for (int k = 0; k < 15; k++) xch[(32 + k) * 64 + lane] = hb[k];
+                    for (int tp = 0; tp < 8; tp++) {
+                        xch[(18 + 2 * tp) * 64 + lane] = hp[tp].x;
+                        xch[(19 + 2 * tp) * 64 + lane] = hp[tp].y;
+                    }
                     __syncthreads();
                 }
             }
@@ -1143,6 +1252,10 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
      * synth-only call reads it from there (st_tail_in), any other use of the
      * handle first copies it into StreamState (mp3d_host.cpp flush_tail). */
     if (f1 == F && PF != 1) {
+        const int lane = opaque((int)(threadIdx.x & 63)); /* lane values re-derived: not held across the loop */
+        const int ch = lane >> 5, sb = lane & 31;
+        const float sgo = (sb & 1) ? -1.f : 1.f;
+        const f32x2 sgp[2] = {(f32x2){1.f, sgo}, (f32x2){sgo, 1.f}};
         float *ovo = st_tail ? st_tail + (size_t)s * TAIL : &S.overlap[0][0][0];
         float *ffo = ovo + sizeof(S.overlap) / 4;
 #pragma unroll
@@ -1152,11 +1265,21 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
             ovo[(ch * 32 + sb) * 18 + 17 - i] = t.y;
         }
 #pragma unroll
-        for (int k = 0; k < 14; k++) ffo[(ch * MP3D_FIFO_SLOTS + k + 1) * 32 + wa] = ha[k];
-#pragma unroll
-        for (int k = 0; k < 15; k++) ffo[(ch * MP3D_FIFO_SLOTS + k) * 32 + wb] = hb[k];
+        for (int tp = 0; tp < 8; tp++) {
+            ffo[(ch * MP3D_FIFO_SLOTS + 2 * tp) * 32 + sb] = hp[tp].x;
+            if (2 * tp + 1 < MP3D_FIFO_SLOTS) ffo[(ch * MP3D_FIFO_SLOTS + 2 * tp + 1) * 32 + sb] = hp[tp].y;
+        }
     }
 }
+
+/* streams (waves) per k_synth workgroup: the MPEG-1 decode runs 8 (two
+ * workgroups = 4 waves per SIMD, the tables shared by 8 waves leave LDS for
+ * the is[] prefetch areas); the synth-only and LSF variants run 4 at 3 waves
+ * per SIMD */
+template <bool SRC_XR, bool LSF> struct SynCfg {
+    static constexpr bool DMA = !SRC_XR && !LSF;
+    static constexpr int WAVES = DMA ? 8 : 4;
+};
 
 template <bool SRC_XR, bool F32, bool LSF>
 /* 3 waves / SIMD (168 VGPRs).  The synth-only entry would fit 4 waves /
@@ -1164,14 +1287,17 @@ template <bool SRC_XR, bool F32, bool LSF>
  * one-granule-ahead prefetch at 3 waves is worth -13 % (A/B XPF3 vs XPF4,
  * profiles/r02_ab.txt): a wave's exposed load latency costs more than a
  * fourth wave hides. */
-__global__ void __launch_bounds__(64 * SYN_WAVES) __attribute__((amdgpu_waves_per_eu(3, 8)))
+__global__ void __launch_bounds__((64 * SynCfg<SRC_XR, LSF>::WAVES))
+    __attribute__((amdgpu_waves_per_eu(SynCfg<SRC_XR, LSF>::DMA ? 4 : 3, 8)))
 k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, const UnitMeta *__restrict__ meta,
         const float *__restrict__ xr_in, const uint8_t *__restrict__ xr_bt, const uint8_t *__restrict__ xr_mixed,
         const DevTables *__restrict__ tab, StreamState *__restrict__ st, void *__restrict__ pcm, int n_streams,
         int F, int xr_nch, int xr_sr, int seg_len, float *__restrict__ st_tail,
         const float *__restrict__ st_tail_in) {
+    constexpr int SYN_WAVES = SynCfg<SRC_XR, LSF>::WAVES;
     __shared__ __attribute__((aligned(16))) SynShared<LSF> T;
     __shared__ SynWave Wv[SYN_WAVES];
+    __shared__ __attribute__((aligned(16))) uint32_t s_isq[SynCfg<SRC_XR, LSF>::DMA ? SYN_WAVES : 1][2 * 320];
     if (!SRC_XR) {
         /* one variant per MPEG family (StreamState.kind, fixed by k_demux):
          * MPEG-1 takes kinds 0 / 1, LSF kind 2.  A workgroup holding no
@@ -1195,7 +1321,8 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
     const int s = vs / nseg, seg = vs - s * nseg;
     if (!SRC_XR && (st[s].kind == 2) != LSF) return; /* the other variant's stream */
     synth_stream<SRC_XR, F32, LSF>(rec, is_buf, meta, xr_in, xr_bt, xr_mixed, tab, st, pcm, F, xr_nch, xr_sr, seg_len,
-                                   st_tail, st_tail_in, T, Wv[wid], s, seg, nseg);
+                                   st_tail, st_tail_in, T, Wv[wid], s, seg, nseg, nullptr,
+                                   SynCfg<SRC_XR, LSF>::DMA ? s_isq[SynCfg<SRC_XR, LSF>::DMA ? wid : 0] : nullptr);
 }
 /* ------------------------------------------------------------------------ */
 /* k_gather_frames: segmented long-stream decode (mp3d_batch_decode_long).  */
@@ -1373,15 +1500,17 @@ void launch_synth(const FrameRec *rec, const int16_t *is_buf, const UnitMeta *me
                   StreamState *st, void *pcm, bool f32, int n_streams, int F, int kinds, int seg_len, float *st_tail,
                   const float *st_tail_in, hipStream_t strm) {
     const int waves = n_streams * ((F + seg_len - 1) / seg_len);
-    const dim3 grid((waves + SYN_WAVES - 1) / SYN_WAVES), block(64 * SYN_WAVES);
     /* the family variants in `kinds` (bit 0 MPEG-1, bit 1 LSF; a batch
      * launches both); a workgroup without a stream of its variant exits
-     * after SYN_WAVES scalar loads (the LSF launch on an all-MPEG-1 batch
+     * after its streams' scalar loads (the LSF launch on an all-MPEG-1 batch
      * costs only its workgroup dispatch) */
-#define MP3D_SYNTH_LAUNCH(F32_, LSF_)                                                                            \
-    hipLaunchKernelGGL((k_synth<false, F32_, LSF_>), grid, block, 0, strm, rec, is_buf, meta, (const float *)nullptr, \
-                       (const uint8_t *)nullptr, (const uint8_t *)nullptr, tab, st, pcm, n_streams, F, 2, 0, seg_len, \
-                       st_tail, st_tail_in)
+#define MP3D_SYNTH_LAUNCH(F32_, LSF_)                                                                              \
+    do {                                                                                                           \
+        constexpr int NW = SynCfg<false, LSF_>::WAVES;                                                             \
+        hipLaunchKernelGGL((k_synth<false, F32_, LSF_>), dim3((waves + NW - 1) / NW), dim3(64 * NW), 0, strm, rec,  \
+                           is_buf, meta, (const float *)nullptr, (const uint8_t *)nullptr, (const uint8_t *)nullptr, \
+                           tab, st, pcm, n_streams, F, 2, 0, seg_len, st_tail, st_tail_in);                        \
+    } while (0)
     if (f32) {
         if (kinds & 1) MP3D_SYNTH_LAUNCH(true, false);
         if (kinds & 2) MP3D_SYNTH_LAUNCH(true, true);
@@ -1398,7 +1527,8 @@ void launch_synth_xr(const float *xr, const uint8_t *bt, const uint8_t *mixed, c
                      int16_t *pcm, int n_streams, int F, int nch, int sr, int seg_len, float *st_tail,
                      const float *st_tail_in, hipStream_t strm) {
     const int waves = n_streams * ((F + seg_len - 1) / seg_len);
-    hipLaunchKernelGGL((k_synth<true, false, false>), dim3((waves + SYN_WAVES - 1) / SYN_WAVES), dim3(64 * SYN_WAVES), 0,
+    constexpr int NW = SynCfg<true, false>::WAVES;
+    hipLaunchKernelGGL((k_synth<true, false, false>), dim3((waves + NW - 1) / NW), dim3(64 * NW), 0,
                        strm, (const FrameRec *)nullptr, (const int16_t *)nullptr, (const UnitMeta *)nullptr, xr, bt,
                        mixed, tab, st, (void *)pcm, n_streams, F, nch, sr, seg_len, st_tail, st_tail_in);
 }

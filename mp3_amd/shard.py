@@ -58,14 +58,23 @@ def gather_to_root(t: torch.Tensor, root: int = 0, async_op: bool = False, out=N
     preallocated receive list on root (reused across steps), else allocated."""
     world, rank = dist.get_world_size(), dist.get_rank()
     src = t.contiguous()
-    if dist.get_backend() == "gloo":
+    gloo = dist.get_backend() == "gloo"
+    if gloo:
         src = src.cpu()  # gloo gathers host tensors
-        if src.dtype in (torch.int16, torch.uint8, torch.int8):
-            src = src.view(torch.int32)
+    # wire type: RCCL / NCCL has no int16 ("Unconvertible NCCL type Short"),
+    # so PCM travels as bytes there (bit-exact, the receive buffers viewed
+    # the same way); gloo has no 8/16-bit gather: int32 words
+    wire = None
+    if src.dtype in (torch.int16, torch.uint8, torch.int8):
+        wire = torch.int32 if gloo else (torch.uint8 if src.dtype == torch.int16 else None)
+    if wire is not None:
+        src = src.view(wire)
     if rank != root:
         out = None
-    elif out is None or dist.get_backend() == "gloo":
+    elif out is None or gloo:
         out = [torch.empty_like(src) for _ in range(world)]
+    else:  # preallocated receive list (device): gather straight into it
+        out = [o.view(src.dtype) for o in out]
     work = dist.gather(src, out, dst=root, async_op=async_op)
     if out is not None:
         out = [o.view(t.dtype) for o in out]

@@ -46,7 +46,9 @@ def _full_size_properties(cfg, base):
     n, F = 65536, 32
     buf, offs, sizes = _gen.batch(cfg, base, n, F, threads=16)
     d_in = torch.from_numpy(buf).cuda()
-    pcm = torch.empty((n, F, 2304), dtype=torch.int16, device="cuda")
+    # zeroed sinks: a mono frame fills only the first half of its row and the
+    # decoder leaves the rest of a device sink as it was
+    pcm = torch.zeros((n, F, 2304), dtype=torch.int16, device="cuda")
     inf = torch.zeros((n, F, 6), dtype=torch.int32, device="cuda")
     dec = mp3_amd.BatchDecoder(n, F)  # >= 256 streams: the wide k_walk + k_mdcopy demux
     dec.decode(d_in, offs, sizes, F, pcm=pcm, infos=inf)
@@ -58,8 +60,8 @@ def _full_size_properties(cfg, base):
     infs = inf.cpu().numpy()
     first = infs[:, : F // 2, 0].astype(np.int64).sum(1)  # bytes of frames 0 .. 15
     half = mp3_amd.BatchDecoder(n, F // 2)
-    pa = torch.empty((n, F // 2, 2304), dtype=torch.int16, device="cuda")
-    pb = torch.empty_like(pa)
+    pa = torch.zeros((n, F // 2, 2304), dtype=torch.int16, device="cuda")
+    pb = torch.zeros_like(pa)
     half.decode(d_in, offs, first.astype(np.uint32), F // 2, pcm=pa)
     half.decode(d_in, offs + first.astype(np.uint64), (sizes - first).astype(np.uint32), F // 2, pcm=pb)
     torch.cuda.synchronize()
