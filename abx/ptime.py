@@ -21,6 +21,7 @@ S = "    /* state out: the stream's last segment.  With several segments the"
 
 def main():
     src = open("mp3_amd/csrc/mp3d_synth.hip").read()
+    mark = os.environ.get("PT_MARK", "")
     reps = [
         ("namespace mp3d {\n", "namespace mp3d {\n__device__ unsigned long long g_ptime[8];\n"),
         ("    for (int f = fw; f < f1; f++) {\n",
@@ -33,22 +34,37 @@ def main():
         (E, E + "\n            tl_ = __builtin_amdgcn_s_memtime(); pt_[3] += tl_ - tw_;"),
         (S, "    if ((threadIdx.x & 63) == 0 && !SRC_XR && PF == 0)\n"
             "        for (int k = 0; k < 8; k++) atomicAdd(&g_ptime[k], pt_[k]);\n" + S),
+    ]
+    if mark == "w":
+        # slots 5, 6 split phase W instead: its vmcnt(0) drain, then the X /
+        # tap loads (up to their lgkmcnt(0)); the rest of W = window + stores
+        reps += [
+            ("            if (!SRC_XR) WAIT_VMCNT0();\n",
+             "            if (!SRC_XR) WAIT_VMCNT0();\n"
+             "            unsigned long long tw1_ = __builtin_amdgcn_s_memtime(); pt_[5] += tw1_ - tw_;\n"),
+            ("                xb17 = sBuf[pb + 17 * XROW];\n",
+             "                xb17 = sBuf[pb + 17 * XROW];\n"
+             "                __builtin_amdgcn_s_waitcnt(0xC07F);\n"
+             "                unsigned long long tw2_ = __builtin_amdgcn_s_memtime(); pt_[6] += tw2_ - tw1_;\n"),
+        ]
+    else:
         # phase Q sub-marks (decode path): after the band scales, after the
         # requantise loop, after escapes + stereo (the rest of Q = scatter)
-        ("                (void)m12a;\n",
-         "                (void)m12a;\n                unsigned long long tq1_ = __builtin_amdgcn_s_memtime(); pt_[5] += tq1_ - tq_;\n"),
-        ("                if (__ballot((bigacc & 0xF800F800u) != 0u)) {\n",
-         "                unsigned long long tq2_ = __builtin_amdgcn_s_memtime(); pt_[6] += tq2_ - tq1_;\n"
-         "                if (__ballot((bigacc & 0xF800F800u) != 0u)) {\n"),
-    ] + ([  # PT_MARK=prefetch: the last Q sub-mark after the next granule's prefetch is issued
-        ("                /* scatter in (short-block reordered) position; M/S-only frames\n",
-         "                pt_[7] += __builtin_amdgcn_s_memtime() - tq2_;\n"
-         "                /* scatter in (short-block reordered) position; M/S-only frames\n"),
-    ] if os.environ.get("PT_MARK") == "prefetch" else [
-        ("                /* the next granule's loads fly during phases I, M, W (issued\n",
-         "                pt_[7] += __builtin_amdgcn_s_memtime() - tq2_;\n"
-         "                /* the next granule's loads fly during phases I, M, W (issued\n"),
-    ])
+        reps += [
+            ("                (void)m12a;\n",
+             "                (void)m12a;\n                unsigned long long tq1_ = __builtin_amdgcn_s_memtime(); pt_[5] += tq1_ - tq_;\n"),
+            ("                if (__ballot((bigacc & 0xF800F800u) != 0u)) {\n",
+             "                unsigned long long tq2_ = __builtin_amdgcn_s_memtime(); pt_[6] += tq2_ - tq1_;\n"
+             "                if (__ballot((bigacc & 0xF800F800u) != 0u)) {\n"),
+        ]
+        if mark == "prefetch":  # the last Q sub-mark after the next granule's prefetch is issued
+            reps.append(("                /* scatter in (short-block reordered) position; M/S-only frames\n",
+                         "                pt_[7] += __builtin_amdgcn_s_memtime() - tq2_;\n"
+                         "                /* scatter in (short-block reordered) position; M/S-only frames\n"))
+        else:
+            reps.append(("                /* the next granule's loads fly during phases I, M, W (issued\n",
+                         "                pt_[7] += __builtin_amdgcn_s_memtime() - tq2_;\n"
+                         "                /* the next granule's loads fly during phases I, M, W (issued\n"))
     for a, b in reps:
         assert src.count(a) == 1, a
         src = src.replace(a, b)
@@ -70,7 +86,7 @@ def main():
     open(d + "/mp3d_host.cpp", "w").write(host)
     os.makedirs(d + "/../../include", exist_ok=True)
     shutil.copy("include/mp3d.h", d + "/../../include/")
-    out = "build_ab/PT2.so" if os.environ.get("PT_MARK") == "prefetch" else "build_ab/PT.so"
+    out = {"prefetch": "build_ab/PT2.so", "w": "build_ab/PTW.so"}.get(mark, "build_ab/PT.so")
     _build.compile_hip(d, out, d + "/obj")
     print(out)
 

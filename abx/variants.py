@@ -368,6 +368,24 @@ VARS["H4"] = [("#define HUFF_WAVES 16", "#define HUFF_WAVES 4"),
 VARS["NODMA"] = [("        if (PAR) {\n            dma_is(g, nz0, nz1);", "        if (false) {\n            dma_is(g, nz0, nz1);"),
                  ("cis[c][i] = PAR ? isq[320 * c + 64 * i + lane] : nis[c][i];", "cis[c][i] = nis[c][i];")]
 
+# round 4: phase W's pair i stored after step i's history updates (its convert / swap chain overlaps them)
+VARS["EMITLATE"] = [("""                        emit(stereo, i, acc[i]);
+                        hp[i] = (f32x2){d.y * xb17, 0.f}; /* H_2i: B(-1) = this X_17 */
+#pragma unroll
+                        for (int tp = 0; tp < i; tp++) {
+                            /* k = 2 (tp - i) + 18: A = xap[k / 2], B = xbp[k / 2 - 1] */
+                            hp[tp] = pfma(bc(d.x), xap[tp - i + 9], hp[tp]);
+                            hp[tp] = pfma(bc(d.y), xbp[tp - i + 8], hp[tp]);
+                        }""", """                        const f32x2 done = acc[i];
+                        hp[i] = (f32x2){d.y * xb17, 0.f}; /* H_2i: B(-1) = this X_17 */
+#pragma unroll
+                        for (int tp = 0; tp < i; tp++) {
+                            /* k = 2 (tp - i) + 18: A = xap[k / 2], B = xbp[k / 2 - 1] */
+                            hp[tp] = pfma(bc(d.x), xap[tp - i + 9], hp[tp]);
+                            hp[tp] = pfma(bc(d.y), xbp[tp - i + 8], hp[tp]);
+                        }
+                        emit(stereo, i, done);""")]
+
 VARS["PAD128"] = _pad(128)
 VARS["PAD64"] = _pad(64)
 

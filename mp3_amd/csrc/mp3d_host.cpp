@@ -391,11 +391,13 @@ static int grow(void **p, size_t *cap, size_t need) {
 /* Frames per k_synth segment for n streams x F frames: few streams leave
  * the chip idle (one wave walks one stream), so each stream is split into
  * frame-parallel segments (one wave each, warm-up frames before; k_synth)
- * until ~2 rounds of resident waves (3 per SIMD) are in the grid, keeping
- * segments >= min_len frames.  MP3D_SEG_FRAMES overrides (0 = never split). */
+ * until one round of resident waves (3 per SIMD) is in the grid, keeping
+ * segments >= min_len frames (C2, 1 024 x 64: 3 segments of 22 frames;
+ * 2 rounds of 11 frames measured 4 % slower, tools/dbg/job_c2_seg.sh).
+ * MP3D_SEG_FRAMES overrides (0 = never split). */
 static int seg_frames(int n, int F, int n_cu, int min_len) {
     int seg_len = F;
-    const long long want = 2LL * 3 * 4 * n_cu;
+    const long long want = 3LL * 4 * n_cu;
     if ((long long)n < want && F >= 2 * min_len) {
         const int nseg = (int)std::min<long long>((want + n - 1) / n, F / min_len);
         seg_len = (F + nseg - 1) / nseg;

@@ -4,20 +4,22 @@
  * groups) and the big_values / count1 Huffman decode of every unit into
  * is[576] + UnitMeta.  Pipeline overview: mp3d_device.h.
  */
+#include <algorithm>
+
 #include "mp3d_huffman_dev.h"
 
 namespace mp3d {
 
 /* k_huffman: one lane per unit (its layout constants and helpers: mp3d_huffman_dev.h) */
-/* work: the handle's super-chunk counter; this launch's tickets start at
- * ticket0 (every wave takes tickets until one is past the last super-chunk,
- * so a launch consumes n_super + its wave count: the host advances its copy) */
+/* work: the handle's work-item counter; this launch's tickets start at
+ * ticket0 (every wave takes tickets until one is past the last unit);
+ * n_big: how many tickets are whole super-chunks (the rest single rounds) */
 __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restrict__ md, const uint64_t *__restrict__ md_off,
                                                         const FrameRec *__restrict__ rec,
                                                         const uint64_t *__restrict__ sideu,
                                                         const DevTables *__restrict__ tab, int16_t *__restrict__ is_buf,
                                                         UnitMeta *__restrict__ meta, int n_units, int F,
-                                                        uint32_t *__restrict__ work, uint32_t ticket0) {
+                                                        uint32_t *__restrict__ work, uint32_t ticket0, int n_big) {
     __shared__ __attribute__((aligned(16))) uint16_t s_lut[MP3D_LUT_MAX];
     /* per-wave staging areas after a 4-word guard: win64g / win32g read the
      * word below a window that starts on a word boundary */
@@ -50,19 +52,24 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
     const int qb1 = tab->lut_hdr.bits1[MP3D_LUT_TABLES - 1];
     /* count1 table B: after the zero table (huff_tables_lane) */
     const uint32_t c1b_base = ((qbase + (1u << qb1) + 1u) & ~1u) + MP3D_C1B_OFF;
-    const int n_super = (n_units + HUFF_SUPER - 1) / HUFF_SUPER;
-
+    /* work items: tickets below n_big are super-chunks of HUFF_SUPER units
+     * (HUFF_ROUNDS rounds), the rest single rounds of 64 units covering the
+     * last units: the waves' finishing times then differ by a round, not by
+     * a super-chunk (the tail of a persistent launch) */
+    const int big_units = n_big * HUFF_SUPER;
     for (;;) {
         uint32_t t = 0u;
         if (lane == 0) t = atomicAdd(work, 1u) - ticket0;
         const int sc = (int)__builtin_amdgcn_readfirstlane(t);
-        if ((uint32_t)sc >= (uint32_t)n_super) break;
-        /* ---- order the super-chunk's units by big_values (counting sort in
+        const bool big = sc < n_big;
+        const int ubase = big ? sc * HUFF_SUPER : big_units + (sc - n_big) * 64;
+        const int nr = big ? HUFF_ROUNDS : 1;
+        if (ubase >= n_units) break;
+        /* ---- order the work item's units by big_values (counting sort in
          * LDS: histogram by ds_add_rtn, wave scan), so each 64-unit round
          * holds units of similar length -- the big_values loop runs
          * max-over-lanes iterations.  The order (u16) lives past the
          * staging area, the histogram in it. */
-        const int ubase = sc * HUFF_SUPER;
         uint16_t *order16 = (uint16_t *)(bits + HUFF_STAGEW + 4);
         wave_sync();
         for (int i = lane; i < 320; i += 64) bits[i] = 0u;
@@ -73,7 +80,8 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
             const int u = ubase + 64 * j + lane;
             bvk[j] = u < n_units ? (uint32_t)(sideu[u] >> 43) & 0x1FFu : 0u;
             bvk[j] = bvk[j] < 320u ? bvk[j] : 319u;
-            slot[j] = atomicAdd(&bits[bvk[j]], 1u);
+            slot[j] = 0u;
+            if (j < nr) slot[j] = atomicAdd(&bits[bvk[j]], 1u);
         }
         wave_sync();
         {   /* exclusive prefix over the 320 bins: lane owns bins 5 lane .. +4 */
@@ -93,10 +101,11 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
         }
         wave_sync();
 #pragma unroll
-        for (int j = 0; j < HUFF_ROUNDS; j++) order16[bits[bvk[j]] + slot[j]] = (uint16_t)(64 * j + lane);
+        for (int j = 0; j < HUFF_ROUNDS; j++)
+            if (j < nr) order16[bits[bvk[j]] + slot[j]] = (uint16_t)(64 * j + lane);
         wave_sync();
 
-        for (int rd = 0; rd < HUFF_ROUNDS; rd++) {
+        for (int rd = 0; rd < nr; rd++) {
             const int u = ubase + (int)order16[64 * rd + lane];
             const int fr = u >> 2, gr = (u >> 1) & 1, ch = u & 1;
             bool valid = u < n_units;
@@ -234,10 +243,11 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                             const uint32_t i1 = tb + (hi >> s1);
                             const uint32_t e1 = s_lut[i1];
                             /* second level, branch-free: i2 = i1 for a leaf */
-                            const uint32_t nb = (e1 >> 11) & 15u;
+                            const uint32_t nb = __builtin_amdgcn_ubfe(e1, 11, 4);
                             /* the nb bits after the first level's b1 = 32 - s1: (hi << b1) >> (32 - nb); a
-                             * zero-width field (leaf, nb = 0) extracts 0 */
-                            const uint32_t sub = ((e1 & 0x7FFu) << 2) + __builtin_amdgcn_ubfe(hi, s1 - nb, nb);
+                             * zero-width field (leaf, nb = 0) extracts 0.  The base by v_bfe + v_lshl_add
+                             * (as (e1 & 0x7FF) << 2 the compiler spent three ops) */
+                            const uint32_t sub = (__builtin_amdgcn_ubfe(e1, 0, 11) << 2) + __builtin_amdgcn_ubfe(hi, s1 - nb, nb);
                             const uint32_t i2 = (e1 & 0x8000u) ? sub : i1;
                             const uint32_t e = s_lut[i2];
                             const uint32_t x = (e >> 4) & 15u, y = e & 15u, len_c = (e >> 8) & 31u;
@@ -399,6 +409,9 @@ void launch_huffman(const uint8_t *md, const uint64_t *md_off, const FrameRec *r
      * counter as they finish, so uneven super-chunks balance themselves */
     int blocks = (supers + HUFF_WAVES - 1) / HUFF_WAVES;
     blocks = blocks < n_cu ? (blocks > 0 ? blocks : 1) : n_cu;
+    /* the last ~2 rounds per wave as single-round work items (k_huffman) */
+    const int small_units = std::min(n_units, 2 * blocks * HUFF_WAVES * 64);
+    const int n_big = (n_units - small_units) / HUFF_SUPER;
     if (wave) {
         hipLaunchKernelGGL(k_huffman_wave, dim3((n_units + HW_UNITS - 1) / HW_UNITS), dim3(64 * HW_UNITS), 0, strm, md,
                            md_off, rec, sideu, tab, is_buf, meta, n_units, F);
@@ -408,7 +421,7 @@ void launch_huffman(const uint8_t *md, const uint64_t *md_off, const FrameRec *r
      * us): a launch that failed can never leave the next one's tickets off */
     (void)hipMemsetAsync(work, 0, sizeof(uint32_t), strm);
     hipLaunchKernelGGL(k_huffman, dim3(blocks), dim3(HUFF_BLOCK), 0, strm, md, md_off, rec, sideu, tab, is_buf, meta,
-                       n_units, F, work, 0u);
+                       n_units, F, work, 0u, n_big);
     (void)base;
 }
 

@@ -1215,9 +1215,6 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                             hp[tp] = pfma(bc(d.x), xap[tp - i + 9], hp[tp]);
                             hp[tp] = pfma(bc(d.y), xbp[tp - i + 8], hp[tp]);
                         }
-                        /* one scheduling region per step: hoisted across the
-                         * steps, the tap reads and chains spilled at 128 VGPRs */
-                        __builtin_amdgcn_sched_barrier(0);
                     }
                     emit(stereo, 8, acc[8]);
                 };
