@@ -389,6 +389,20 @@ VARS["EMITLATE"] = [("""                        emit(stereo, i, acc[i]);
 VARS["PAD128"] = _pad(128)
 VARS["PAD64"] = _pad(64)
 
+# r04: the synth-only (C2) variant at 4 waves / SIMD with its register prefetch (spills 40 B):
+# 8-wave workgroups (XS4) or 4-wave (XS4b)
+_XWPE = ("amdgpu_waves_per_eu(SynCfg<SRC_XR, LSF>::DMA ? 4 : 3, 8)", "amdgpu_waves_per_eu(!LSF ? 4 : 3, 8)")
+VARS["XS4"] = [_XWPE, ("static constexpr int WAVES = DMA ? 8 : 4;", "static constexpr int WAVES = !LSF ? 8 : 4;")]
+VARS["XS4b"] = [_XWPE]
+
+# XS4M: XS4 with the next granule's spectra loads issued at phase M (after phase I's register peak)
+_XQ = ("                if (f + 1 < f1 || gr == 0) load_xr(2 * f + gr + 1); /* next granule, in flight through I, M, W */\n", "")
+_XM = ("            /* ---------------- phase M: matrixing on the matrix cores ------- */\n",
+       "            /* ---------------- phase M: matrixing on the matrix cores ------- */\n"
+       "            if (SRC_XR && (f + 1 < f1 || gr == 0)) load_xr(2 * f + gr + 1);\n")
+VARS["XS4M"] = VARS["XS4"] + [_XQ, _XM]
+VARS["XS4Mb"] = VARS["XS4b"] + [_XQ, _XM]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])

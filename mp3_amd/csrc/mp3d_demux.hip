@@ -170,7 +170,8 @@ __device__ __forceinline__ bool walk_crc_ok(const LaneWin &W, uint32_t side_byte
 __global__ void __launch_bounds__(64) k_walk(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
                                              const uint32_t *__restrict__ in_len, StreamState *__restrict__ st,
                                              FrameRec *__restrict__ rec, uint64_t *__restrict__ sideu,
-                                             DevInfo *__restrict__ infos, int n_streams, int F, int opts) {
+                                             DevInfo *__restrict__ infos, int n_streams, int F, int opts,
+                                             uint32_t *__restrict__ fam, uint32_t seq) {
     __shared__ uint32_t s_win[64 * WALK_WORDS];
     /* frame words and sample rates in LDS: a constant-table read per frame
      * from L2 was a round trip on the frame chain */
@@ -341,6 +342,9 @@ __global__ void __launch_bounds__(64) k_walk(const uint8_t *__restrict__ in, con
     if ((uint32_t)c > P) c = (int)P;
     S.frames += decoded;
     S.kind = kind;
+    /* the batch holds an LSF stream: tag the family word with this call's
+     * seq (lanes store the same value; k_synth's LSF variant reads it) */
+    if (fam && kind == 2) *fam = seq;
     S.pad_[0] = (int32_t)P; /* md end, for k_mdcopy */
     S.pad_[1] = c;          /* next carry length   */
 }
@@ -476,10 +480,10 @@ hipError_t upload_demux_constants(const uint16_t *frame_bytes) { return upload_d
  * per stream (fewer launches: the per-frame decoder, small batches) */
 void launch_demux(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len, uint8_t *md,
                   const uint64_t *md_off, StreamState *st, FrameRec *rec, uint64_t *sideu, void *infos, int n_streams,
-                  int F, int opts, bool wide, hipStream_t strm) {
+                  int F, int opts, bool wide, uint32_t *fam, uint32_t seq, hipStream_t strm) {
     if (wide) {
-        hipLaunchKernelGGL(k_walk, dim3((n_streams + WALK_LANES - 1) / WALK_LANES), dim3(64), 0, strm, in, in_off, in_len, st, rec, sideu,
-                           (DevInfo *)infos, n_streams, F, opts);
+        hipLaunchKernelGGL(k_walk, dim3((n_streams + WALK_LANES - 1) / WALK_LANES), dim3(64), 0, strm, in, in_off,
+                           in_len, st, rec, sideu, (DevInfo *)infos, n_streams, F, opts, fam, seq);
         hipLaunchKernelGGL(k_mdcopy, dim3((n_streams + MDC_WAVES - 1) / MDC_WAVES), dim3(64 * MDC_WAVES), 0, strm, in,
                            md, md_off, st, (const FrameRec *)rec, n_streams, F);
         return;

@@ -27,11 +27,11 @@ namespace mp3d {
 hipError_t upload_synth_constants(const float *, const float *, const float *, const float *);
 hipError_t upload_demux_constants(const uint16_t *);
 void launch_demux(const uint8_t *, const uint64_t *, const uint32_t *, uint8_t *, const uint64_t *, StreamState *,
-                  FrameRec *, uint64_t *, void *, int, int, int, bool, hipStream_t);
+                  FrameRec *, uint64_t *, void *, int, int, int, bool, uint32_t *, uint32_t, hipStream_t);
 void launch_huffman(const uint8_t *, const uint64_t *, const FrameRec *, const uint64_t *, const DevTables *, int16_t *,
-                    UnitMeta *, int, int, int, bool, uint32_t *, uint32_t *, hipStream_t);
+                    UnitMeta *, int, int, int, bool, uint32_t *, hipStream_t);
 void launch_synth(const FrameRec *, const int16_t *, const UnitMeta *, const DevTables *, StreamState *, void *, bool, int,
-                  int, int, int, float *, const float *, hipStream_t);
+                  int, int, int, float *, const float *, const uint32_t *, uint32_t, hipStream_t);
 void launch_synth_xr(const float *, const uint8_t *, const uint8_t *, const DevTables *, StreamState *, int16_t *, int,
                      int, int, int, int, float *, const float *, hipStream_t);
 void launch_gather_frames(const void *, void *, const void *, void *, const int *, int, int, int, int, int,
@@ -335,10 +335,13 @@ struct mp3d_batch {
         uint32_t *in_len() const { return (uint32_t *)(d + 2 * (size_t)n); }
     } geo[2];
     int geo_i = 0;
-    /* k_huffman's super-chunk counter (device; reset by each launch's memset
-     * on the call's stream, and a handle's calls are ordered) */
+    /* d_work[0]: k_huffman's super-chunk counter (device; reset by each
+     * launch's memset on the call's stream, and a handle's calls are
+     * ordered).  d_work[1]: the family word, = call_seq when k_walk saw an
+     * LSF stream in this call (fam_ok: this call's demux was k_walk) */
     uint32_t *d_work = nullptr;
-    uint32_t work_base = 0; /* unused ticket base (launch_huffman signature) */
+    uint32_t call_seq = 0;
+    bool fam_ok = false;
     hipStream_t copy = nullptr;
     mp3d_frame_info *d_infos = nullptr;
     uint8_t *md = nullptr;
@@ -391,13 +394,14 @@ static int grow(void **p, size_t *cap, size_t need) {
 /* Frames per k_synth segment for n streams x F frames: few streams leave
  * the chip idle (one wave walks one stream), so each stream is split into
  * frame-parallel segments (one wave each, warm-up frames before; k_synth)
- * until one round of resident waves (3 per SIMD) is in the grid, keeping
- * segments >= min_len frames (C2, 1 024 x 64: 3 segments of 22 frames;
- * 2 rounds of 11 frames measured 4 % slower, tools/dbg/job_c2_seg.sh).
+ * until one round of resident waves (4 per SIMD) is in the grid, keeping
+ * segments >= min_len frames (C2, 1 024 x 64: 4 segments of 16 frames;
+ * at 3 waves per SIMD, 2 rounds of 11 frames measured 4 % slower than one
+ * of 22, tools/dbg/job_c2_seg.sh).
  * MP3D_SEG_FRAMES overrides (0 = never split). */
 static int seg_frames(int n, int F, int n_cu, int min_len) {
     int seg_len = F;
-    const long long want = 3LL * 4 * n_cu;
+    const long long want = 4LL * 4 * n_cu; /* one round at 4 waves per SIMD */
     if ((long long)n < want && F >= 2 * min_len) {
         const int nseg = (int)std::min<long long>((want + n - 1) / n, F / min_len);
         seg_len = (F + nseg - 1) / nseg;
@@ -717,11 +721,14 @@ static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offse
     if (b->timing) HIPCHK(hipEventRecord(b->ev[0], s));
     /* demux + main-data gather: lane-per-stream walk + payload copy for wide
      * batches, one wave per stream below MP3D_WIDE_STREAMS (fewer launches) */
+    const bool wide = demux_wide(n);
+    if (++b->call_seq == 0) b->call_seq = 1; /* (d_work[1] starts at 0) */
+    b->fam_ok = wide;
     launch_demux(din, g.in_off(), g.in_len(), b->md, g.md_off(), b->st, b->rec, b->sideu,
-                 dev_infos ? (void *)dev_infos : b->d_infos, n, F, b->opts, demux_wide(n), s);
+                 dev_infos ? (void *)dev_infos : b->d_infos, n, F, b->opts, wide, b->d_work + 1, b->call_seq, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[1], s));
     launch_huffman(b->md, g.md_off(), b->rec, b->sideu, dc.tables, b->is_buf, b->meta, n, F, dc.n_cu,
-                   huffman_wave(n * F * 4), b->d_work, &b->work_base, s);
+                   huffman_wave(n * F * 4), b->d_work, s);
     HIPCHK(hipEventRecord(g.freed, s)); /* the slot's last reader */
     b->geo[b->geo_i].fresh = true;
     if (b->timing) HIPCHK(hipEventRecord(b->ev[2], s));
@@ -769,7 +776,8 @@ static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *of
     TailPlan tp;
     r = tail_plan(b, n, F, seg_len, s, &tp);
     if (r) return r;
-    launch_synth(b->rec, b->is_buf, b->meta, dc.tables, b->st, dpcm, f32, n, F, kinds, seg_len, tp.out, tp.in, s);
+    launch_synth(b->rec, b->is_buf, b->meta, dc.tables, b->st, dpcm, f32, n, F, kinds, seg_len, tp.out, tp.in,
+                 b->fam_ok ? b->d_work + 1 : nullptr, b->call_seq, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[3], s));
     HIPCHK(hipGetLastError());
     tail_commit(b, n, F, seg_len, tp);

@@ -401,7 +401,7 @@ __global__ void __launch_bounds__(64 * HW_UNITS) k_huffman_wave(const uint8_t *_
 /* work: k_huffman's super-chunk counter (4 B of device memory per handle) */
 void launch_huffman(const uint8_t *md, const uint64_t *md_off, const FrameRec *rec, const uint64_t *sideu,
                     const DevTables *tab, int16_t *is_buf, UnitMeta *meta, int n_streams, int F, int n_cu, bool wave,
-                    uint32_t *work, uint32_t *base, hipStream_t strm) {
+                    uint32_t *work, hipStream_t strm) {
     int n_units = n_streams * F * 4;
     int supers = (n_units + HUFF_SUPER - 1) / HUFF_SUPER;
     /* one workgroup per CU (its LDS is the whole CU's), fewer when there
@@ -422,7 +422,6 @@ void launch_huffman(const uint8_t *md, const uint64_t *md_off, const FrameRec *r
     (void)hipMemsetAsync(work, 0, sizeof(uint32_t), strm);
     hipLaunchKernelGGL(k_huffman, dim3(blocks), dim3(HUFF_BLOCK), 0, strm, md, md_off, rec, sideu, tab, is_buf, meta,
                        n_units, F, work, 0u, n_big);
-    (void)base;
 }
 
 } // namespace mp3d

@@ -440,6 +440,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
      * loop-carried register directly; otherwise slot 0 = the current
      * granule, slot 1 the next, shifted after each prefetch. */
     constexpr bool PAR = !SRC_XR && !LSF && PF == 0;
+    constexpr bool XDMA = SRC_XR && !LSF && PF == 0;
     /* PAR (the batch's MPEG-1 decode, 8-wave workgroups): the is[] words go
      * by LDS-DMA (buffer_load ... lds) into the wave's isq area [ch][320]
      * (256-B pieces; the fifth piece's upper half is padding) instead of
@@ -556,10 +557,42 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
     const __amdgpu_buffer_rsrc_t r_xr = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(xr_in + (SRC_XR ? (size_t)s * F * 2 * xr_nch * 576 : 0)), 0, SRC_XR ? F * 2 * xr_nch * 2304 : 0,
         0x00020000);
+    /* XDMA (the synth-only entry at 4 waves / SIMD, 8-wave workgroups):
+     * channel 0's 576 floats go by LDS-DMA into the wave's isq area (nine
+     * 256-B pieces, the dma_is recipe; a granule past F reads 0), channel 1
+     * into nxr[1] -- 10 registers instead of 20 held through I, M and W */
+    auto dma_xr = [&](int g) {
+        const int lo = opaque(lane * 4);
+        const uint32_t lds0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uintptr_t)(lds_cf32 *)(const float *)isq);
+        const uint64_t ra = (uint64_t)(uintptr_t)(xr_in + (size_t)s * F * 2 * xr_nch * 576);
+        const u32x4 rs = {(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)ra),
+                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(ra >> 32)) & 0xFFFFu,
+                          (uint32_t)(F * 2 * xr_nch * 2304), 0x00020000u};
+        const int so = __builtin_amdgcn_readfirstlane(g * xr_nch * 2304);
+        uint32_t keep;
+        __asm__ volatile("s_waitcnt lgkmcnt(0)\n\t" /* this granule's reads of the area are done */
+                         "s_mov_b32 %0, m0\n\t"
+                         "s_mov_b32 m0, %2\n\t"
+                         "s_nop 0\n\t"
+                         "buffer_load_dword %1, %3, %4 offen lds\n\t"
+                         "buffer_load_dword %1, %3, %4 offen offset:256 lds\n\t"
+                         "buffer_load_dword %1, %3, %4 offen offset:512 lds\n\t"
+                         "buffer_load_dword %1, %3, %4 offen offset:768 lds\n\t"
+                         "buffer_load_dword %1, %3, %4 offen offset:1024 lds\n\t"
+                         "buffer_load_dword %1, %3, %4 offen offset:1280 lds\n\t"
+                         "buffer_load_dword %1, %3, %4 offen offset:1536 lds\n\t"
+                         "buffer_load_dword %1, %3, %4 offen offset:1792 lds\n\t"
+                         "buffer_load_dword %1, %3, %4 offen offset:2048 lds\n\t"
+                         "s_mov_b32 m0, %0"
+                         : "=&s"(keep)
+                         : "v"(lo), "s"(lds0), "s"(rs), "s"(so)
+                         : "memory");
+    };
     auto load_xr = [&](int g) {
         const int lo = opaque(lane * 8);
+        if (XDMA) dma_xr(g);
 #pragma unroll
-        for (int c = 0; c < 2; c++)
+        for (int c = XDMA ? 1 : 0; c < 2; c++)
 #pragma unroll
             for (int i = 0; i < 5; i++) {
                 nxr[c][i] = (f32x2){0.f, 0.f};
@@ -567,12 +600,20 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                     nxr[c][i] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(
                                                               r_xr, lo + 512 * i + 2304 * c, g * xr_nch * 2304, 0));
             }
-        const int q = lane & 1;
-        const size_t ux = ((size_t)s * F * 2 + g) * xr_nch + q;
-        nbt = 0u;
-        if (lane < 4 && q < xr_nch && g < 2 * F) nbt = lane < 2 ? xr_bt[ux] : xr_mixed[ux];
+        /* block type (lanes 0, 1) and mixed flag (lanes 2, 3) of channel
+         * lane & 1: two unconditional byte loads from the uniform array
+         * bases with 32-bit lane offsets (a per-lane 64-bit address was
+         * held across the loop and spilled) */
+        const int lq = opaque((int)(threadIdx.x & 63)), q = lq & 1;
+        const bool okq = lq < 4 && q < xr_nch && g < 2 * F;
+        const uint32_t ob = okq ? (uint32_t)(((s * F * 2) + g) * xr_nch + q) : 0u;
+        const uint32_t vb = xr_bt[ob], vm = xr_mixed[ob];
+        nbt = okq ? (lq < 2 ? vb : vm) : 0u;
     };
-    if (SRC_XR) load_xr(2 * fw);
+    if (SRC_XR) {
+        load_xr(2 * fw);
+        if (XDMA) WAIT_VMCNT0(); /* channel 0 lands in LDS before the first phase Q */
+    }
     if (!SRC_XR) {
         prefetch_full(2 * fw + (PF == 2 ? 1 : 0));
         /* explicit drain on the entry path, so the compiler's wait before
@@ -628,7 +669,9 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
 #pragma unroll
                 for (int c = 0; c < 2; c++)
 #pragma unroll
-                    for (int i = 0; i < 5; i++) cx[c][i] = nxr[c][i];
+                    for (int i = 0; i < 5; i++)
+                        cx[c][i] = XDMA && c == 0 ? *(const f32x2 *)((const float *)isq + 2 * lane + 128 * i)
+                                                  : nxr[c][i];
                 bt0 = __builtin_amdgcn_readlane((int)nbt, 0);
                 mx0 = bt0 == 2 ? __builtin_amdgcn_readlane((int)nbt, 2) : 0;
                 if (nch == 2) {
@@ -1075,7 +1118,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
              * pending the compiler needs no wait after the stores.  (Its
              * waitcnt pass treats loads and stores pending together as out of
              * order and would otherwise emit vmcnt(0) right after them.) */
-            if (!SRC_XR) WAIT_VMCNT0();
+            if (!SRC_XR || XDMA) WAIT_VMCNT0();
             if (PF == 2) { /* granule 0's synthesis history from the other wave */
                 __syncthreads();
 #pragma unroll
@@ -1274,28 +1317,33 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
  * the is[] prefetch areas); the synth-only and LSF variants run 4 at 3 waves
  * per SIMD */
 template <bool SRC_XR, bool LSF> struct SynCfg {
-    static constexpr bool DMA = !SRC_XR && !LSF;
+    static constexpr bool DMA = !LSF; /* is[] (decode) or channel-0 spectra (synth only) by LDS-DMA */
     static constexpr int WAVES = DMA ? 8 : 4;
 };
 
 template <bool SRC_XR, bool F32, bool LSF>
-/* 3 waves / SIMD (168 VGPRs).  The synth-only entry would fit 4 waves /
- * SIMD without its spectra prefetch (-3.4 % k_synth on C2, A/B XW4), but the
- * one-granule-ahead prefetch at 3 waves is worth -13 % (A/B XPF3 vs XPF4,
- * profiles/r02_ab.txt): a wave's exposed load latency costs more than a
- * fourth wave hides. */
+/* MPEG-1 decode and synth only: 4 waves / SIMD (<= 128 VGPRs), the next
+ * granule's is[] words or channel-0 spectra prefetched by LDS-DMA into the
+ * wave's isq area; LSF: 3 waves / SIMD (168 VGPRs).  (Round 2: without any
+ * prefetch the synth-only entry fitted 4 waves but was slower than 3 waves
+ * with it, A/B XPF3 / XPF4.) */
 __global__ void __launch_bounds__((64 * SynCfg<SRC_XR, LSF>::WAVES))
     __attribute__((amdgpu_waves_per_eu(SynCfg<SRC_XR, LSF>::DMA ? 4 : 3, 8)))
 k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, const UnitMeta *__restrict__ meta,
         const float *__restrict__ xr_in, const uint8_t *__restrict__ xr_bt, const uint8_t *__restrict__ xr_mixed,
         const DevTables *__restrict__ tab, StreamState *__restrict__ st, void *__restrict__ pcm, int n_streams,
         int F, int xr_nch, int xr_sr, int seg_len, float *__restrict__ st_tail,
-        const float *__restrict__ st_tail_in) {
+        const float *__restrict__ st_tail_in, const uint32_t *__restrict__ fam, uint32_t seq) {
     constexpr int SYN_WAVES = SynCfg<SRC_XR, LSF>::WAVES;
     __shared__ __attribute__((aligned(16))) SynShared<LSF> T;
     __shared__ SynWave Wv[SYN_WAVES];
     __shared__ __attribute__((aligned(16))) uint32_t s_isq[SynCfg<SRC_XR, LSF>::DMA ? SYN_WAVES : 1][2 * 320];
-    if (!SRC_XR) {
+    /* LSF variant of a batch decode (fam given): k_walk tagged the family
+     * word with this call's seq if any stream is LSF; otherwise the whole
+     * (small, persistent) grid leaves at once.  With LSF streams each
+     * workgroup walks blocks blockIdx.x, + gridDim.x, ... */
+    if (LSF && !SRC_XR && fam && *fam != seq) return;
+    if (!SRC_XR && !(LSF && fam)) {
         /* one variant per MPEG family (StreamState.kind, fixed by k_demux):
          * MPEG-1 takes kinds 0 / 1, LSF kind 2.  A workgroup holding no
          * stream of its variant leaves before staging any table (the same
@@ -1313,13 +1361,26 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
     __syncthreads();
     const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); /* wave-uniform (SGPR) */
     const int nseg = (F + seg_len - 1) / seg_len;
-    const int vs = blockIdx.x * SYN_WAVES + wid;
-    if (vs >= n_streams * nseg) return; /* after the only workgroup barrier */
-    const int s = vs / nseg, seg = vs - s * nseg;
-    if (!SRC_XR && (st[s].kind == 2) != LSF) return; /* the other variant's stream */
-    synth_stream<SRC_XR, F32, LSF>(rec, is_buf, meta, xr_in, xr_bt, xr_mixed, tab, st, pcm, F, xr_nch, xr_sr, seg_len,
-                                   st_tail, st_tail_in, T, Wv[wid], s, seg, nseg, nullptr,
-                                   SynCfg<SRC_XR, LSF>::DMA ? s_isq[SynCfg<SRC_XR, LSF>::DMA ? wid : 0] : nullptr);
+    const int nblk = (n_streams * nseg + SYN_WAVES - 1) / SYN_WAVES;
+    /* one block, or (LSF variant, persistent grid) blocks blockIdx.x +
+     * k gridDim.x; the loop only there: around the 4-wave variants' bodies
+     * it held loop-invariant addresses across the stream and spilled */
+    auto run = [&](int blk) {
+        const int vs = blk * SYN_WAVES + wid;
+        if (vs >= n_streams * nseg) return false; /* after the only workgroup barrier */
+        const int s = vs / nseg, seg = vs - s * nseg;
+        if (!SRC_XR && (st[s].kind == 2) != LSF) return true; /* the other variant's stream */
+        synth_stream<SRC_XR, F32, LSF>(rec, is_buf, meta, xr_in, xr_bt, xr_mixed, tab, st, pcm, F, xr_nch, xr_sr,
+                                       seg_len, st_tail, st_tail_in, T, Wv[wid], s, seg, nseg, nullptr,
+                                       SynCfg<SRC_XR, LSF>::DMA ? s_isq[SynCfg<SRC_XR, LSF>::DMA ? wid : 0] : nullptr);
+        return true;
+    };
+    if constexpr (LSF && !SRC_XR) {
+        for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x)
+            if (!run(blk)) break;
+    } else {
+        run(blockIdx.x);
+    }
 }
 /* ------------------------------------------------------------------------ */
 /* k_gather_frames: segmented long-stream decode (mp3d_batch_decode_long).  */
@@ -1495,18 +1556,23 @@ void launch_frame(const uint8_t *in_host, uint32_t in_have, const uint64_t *in_o
  * (st_tail_in, when given, holds the streams' state in place of st) */
 void launch_synth(const FrameRec *rec, const int16_t *is_buf, const UnitMeta *meta, const DevTables *tab,
                   StreamState *st, void *pcm, bool f32, int n_streams, int F, int kinds, int seg_len, float *st_tail,
-                  const float *st_tail_in, hipStream_t strm) {
+                  const float *st_tail_in, const uint32_t *fam, uint32_t seq, hipStream_t strm) {
     const int waves = n_streams * ((F + seg_len - 1) / seg_len);
     /* the family variants in `kinds` (bit 0 MPEG-1, bit 1 LSF; a batch
      * launches both); a workgroup without a stream of its variant exits
-     * after its streams' scalar loads (the LSF launch on an all-MPEG-1 batch
-     * costs only its workgroup dispatch) */
+     * after its streams' scalar loads.  With the family word (fam, seq; wide
+     * demux) the LSF variant runs a persistent grid of at most SYN_LSF_GRID
+     * workgroups that all leave at once on an all-MPEG-1 batch (its 16 384
+     * workgroups' dispatch and loads cost 39 us per C3 step) */
+#define SYN_LSF_GRID 1024
 #define MP3D_SYNTH_LAUNCH(F32_, LSF_)                                                                              \
     do {                                                                                                           \
         constexpr int NW = SynCfg<false, LSF_>::WAVES;                                                             \
-        hipLaunchKernelGGL((k_synth<false, F32_, LSF_>), dim3((waves + NW - 1) / NW), dim3(64 * NW), 0, strm, rec,  \
-                           is_buf, meta, (const float *)nullptr, (const uint8_t *)nullptr, (const uint8_t *)nullptr, \
-                           tab, st, pcm, n_streams, F, 2, 0, seg_len, st_tail, st_tail_in);                        \
+        int nb = (waves + NW - 1) / NW;                                                                            \
+        if (LSF_ && fam && nb > SYN_LSF_GRID) nb = SYN_LSF_GRID;                                                   \
+        hipLaunchKernelGGL((k_synth<false, F32_, LSF_>), dim3(nb), dim3(64 * NW), 0, strm, rec, is_buf, meta,       \
+                           (const float *)nullptr, (const uint8_t *)nullptr, (const uint8_t *)nullptr, tab, st, pcm,  \
+                           n_streams, F, 2, 0, seg_len, st_tail, st_tail_in, LSF_ ? fam : nullptr, seq);           \
     } while (0)
     if (f32) {
         if (kinds & 1) MP3D_SYNTH_LAUNCH(true, false);
@@ -1527,7 +1593,8 @@ void launch_synth_xr(const float *xr, const uint8_t *bt, const uint8_t *mixed, c
     constexpr int NW = SynCfg<true, false>::WAVES;
     hipLaunchKernelGGL((k_synth<true, false, false>), dim3((waves + NW - 1) / NW), dim3(64 * NW), 0,
                        strm, (const FrameRec *)nullptr, (const int16_t *)nullptr, (const UnitMeta *)nullptr, xr, bt,
-                       mixed, tab, st, (void *)pcm, n_streams, F, nch, sr, seg_len, st_tail, st_tail_in);
+                       mixed, tab, st, (void *)pcm, n_streams, F, nch, sr, seg_len, st_tail, st_tail_in,
+                       (const uint32_t *)nullptr, 0u);
 }
 
 void launch_gather_frames(const void *src, void *dst, const void *isrc, void *idst, const int *a, int L, int F, int k0,

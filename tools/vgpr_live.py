@@ -42,13 +42,15 @@ def parse(asm, kernel):
         if m:
             files[m.group(1)] = (m.group(3) or m.group(2)).split("/")[-1]
     start = next(i for i, l in enumerate(lines) if l.startswith(kernel) and re.match(r"^\S+:", l))
-    insts, labels, loc = [], {}, ("?", 0)
+    insts, labels, loc, chain = [], {}, ("?", 0), ()
     for l in lines[start + 1:]:
         if l.startswith(".Lfunc_end"):
             break
         m = re.match(r"\s*\.loc\s+(\d+)\s+(\d+)", l)
         if m:
             loc = (files.get(m.group(1), "?"), int(m.group(2)))
+            # the inlined-at chain in the comment: every (file, line) from the innermost out
+            chain = tuple((f.split("/")[-1], int(n)) for f, n in re.findall(r"([\w./-]+):(\d+):\d+", l.split(";", 1)[-1]))
             continue
         m = re.match(r"^(\.LBB\w+):", l)
         if m:
@@ -57,14 +59,14 @@ def parse(asm, kernel):
         s = l.split(";")[0].strip()
         if not s or s.startswith(".") or s.endswith(":"):
             continue
-        insts.append((s, loc))
+        insts.append((s, loc, chain))
     return insts, labels
 
 
 def analyse(insts, labels):
     n = len(insts)
     defs, uses, succ = [], [], []
-    for i, (s, _) in enumerate(insts):
+    for i, (s, _, _) in enumerate(insts):
         op, _, rest = s.partition(" ")
         ops = [o.strip() for o in rest.split(",")] if rest else []
         d, u = set(), set()
@@ -116,6 +118,9 @@ def main():
     ap.add_argument("--flags", default="-fno-slp-vectorize")
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--asm", default=None, help="use this .s instead of compiling")
+    ap.add_argument("--phases", default="",
+                    help="NAME:FIRST-LAST,... source line ranges of --src: the largest live count of the "
+                         "instructions whose inlined-at chain passes through each range")
     ap.add_argument("--why", type=int, default=0,
                     help="at the hottest instruction of this source line: the live VGPRs by the source line of "
                          "their nearest preceding def")
@@ -130,11 +135,19 @@ def main():
     insts, labels = parse(asm, args.kernel)
     live, defs = analyse(insts, labels)
     per_line = collections.defaultdict(int)
-    for (s, loc), lv in zip(insts, live):
+    for (s, loc, _), lv in zip(insts, live):
         per_line[loc] = max(per_line[loc], len(lv))
     print("instructions %d, max live VGPRs %d" % (len(insts), max(len(x) for x in live)))
+    if args.phases:
+        src = os.path.basename(args.src)
+        for ph in args.phases.split(","):
+            name, rng = ph.split(":")
+            a, b = (int(x) for x in rng.split("-"))
+            sel = [len(lv) for (_, loc, ch), lv in zip(insts, live)
+                   if any(f == src and a <= n <= b for f, n in (loc,) + ch)]
+            print("phase %-4s lines %4d-%4d: %5d instructions, max live %3d" % (name, a, b, len(sel), max(sel or [0])))
     if args.why:
-        cand = [i for i, (_, loc) in enumerate(insts) if loc[1] == args.why]
+        cand = [i for i, (_, loc, _) in enumerate(insts) if loc[1] == args.why]
         i0 = max(cand, key=lambda i: len(live[i]))
         by = collections.Counter()
         for r in live[i0]:
