@@ -31,7 +31,7 @@ void launch_demux(const uint8_t *, const uint64_t *, const uint32_t *, uint8_t *
 void launch_huffman(const uint8_t *, const uint64_t *, const FrameRec *, const uint64_t *, const DevTables *, int16_t *,
                     UnitMeta *, int, int, int, bool, uint32_t *, hipStream_t);
 void launch_synth(const FrameRec *, const int16_t *, const UnitMeta *, const DevTables *, StreamState *, void *, bool, int,
-                  int, int, int, float *, const float *, const uint32_t *, uint32_t, hipStream_t);
+                  int, int, int, float *, const float *, const uint32_t *, uint32_t, int, hipStream_t);
 void launch_synth_xr(const float *, const uint8_t *, const uint8_t *, const DevTables *, StreamState *, int16_t *, int,
                      int, int, int, int, float *, const float *, hipStream_t);
 void launch_gather_frames(const void *, void *, const void *, void *, const int *, int, int, int, int, int,
@@ -777,7 +777,7 @@ static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *of
     r = tail_plan(b, n, F, seg_len, s, &tp);
     if (r) return r;
     launch_synth(b->rec, b->is_buf, b->meta, dc.tables, b->st, dpcm, f32, n, F, kinds, seg_len, tp.out, tp.in,
-                 b->fam_ok ? b->d_work + 1 : nullptr, b->call_seq, s);
+                 b->fam_ok ? b->d_work + 1 : nullptr, b->call_seq, dc.n_cu, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[3], s));
     HIPCHK(hipGetLastError());
     tail_commit(b, n, F, seg_len, tp);

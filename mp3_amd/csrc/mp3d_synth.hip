@@ -699,11 +699,29 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                     }
                 }
             } else {
+                /* nz_end per channel (UnitMeta word 12, uniform): the 128-line
+                 * chunks i at or past max(nz_end) are all zero, so their
+                 * words are not read and their lines not requantised.  Three
+                 * straight-line copies (2, 3 or 5 live chunks; C3 granules
+                 * mostly end below line 256 or 384), each keeping its LDS
+                 * reads batched -- a branch per chunk made every chunk wait
+                 * out its own reads. */
+                const int nzq0 = __builtin_amdgcn_readlane((int)wm[cs], 12) & 0xFFFF;
+                const int nzq1 = nch == 2 ? __builtin_amdgcn_readlane((int)wm[cs], MW + 12) & 0xFFFF : 0;
+                const int nzmax = nzq0 > nzq1 ? nzq0 : nzq1;
+                const int nlive = nzmax <= 256 ? 2 : (nzmax <= 384 ? 3 : 5); /* uniform */
                 uint32_t cis[2][5];
+                auto read_cis = [&](auto nic) {
+                    constexpr int NI = decltype(nic)::value;
 #pragma unroll
-                for (int c = 0; c < 2; c++)
+                    for (int c = 0; c < 2; c++)
 #pragma unroll
-                    for (int i = 0; i < 5; i++) cis[c][i] = PAR ? isq[320 * c + 64 * i + lane] : nis[c][i];
+                        for (int i = 0; i < 5; i++)
+                            cis[c][i] = i < NI ? (PAR ? isq[320 * c + 64 * i + lane] : nis[c][i]) : 0u;
+                };
+                if (nlive == 2) read_cis(std::integral_constant<int, 2>{});
+                else if (nlive == 3) read_cis(std::integral_constant<int, 3>{});
+                else read_cis(std::integral_constant<int, 5>{});
                 /* UnitMeta into LDS for the (rare) intensity path; the common
                  * path reads the prefetched words straight from registers */
                 if (lane < nch * MW) ((uint32_t *)&Wd.m[0])[lane] = wm[cs]; /* lane / MW < nch, no division */
@@ -783,11 +801,18 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                 __asm__ volatile("" : "+s"(k1024));
                 const uint32_t sc_base[2] = {(uint32_t)(uintptr_t)(lds_cf32 *)&Wd.scale[0][0],
                                              (uint32_t)(uintptr_t)(lds_cf32 *)&Wd.scale[1][0]};
+                auto requant = [&](auto nic) {
+                constexpr int NI = decltype(nic)::value;
 #pragma unroll
                 for (int i = 0; i < 5; i++) {
                     const bool ok = i < 4 || lane < 32;
 #pragma unroll
                     for (int c = 0; c < 2; c++) {
+                        if (i >= NI) {
+                            XV(c, 2 * i) = 0.f;
+                            XV(c, 2 * i + 1) = 0.f;
+                            continue;
+                        }
                         const uint32_t tv2 = ok ? lpair[var[c]][lane + 64 * i] : 0u;
                         /* lines >= nz_end arrive as 0 (load_is_masked) */
                         /* one v_pk_mad_u16: 4 v + 1024 in both halves (as C the
@@ -801,6 +826,10 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                         XV(c, 2 * i + 1) = *(const float *)(p43b + ((t >> 16) & 0x7FCu)) * sc;
                     }
                 }
+                };
+                if (nlive == 2) requant(std::integral_constant<int, 2>{});
+                else if (nlive == 3) requant(std::integral_constant<int, 3>{});
+                else requant(std::integral_constant<int, 5>{});
                 if (__ballot((bigacc & 0xF800F800u) != 0u)) {
                     /* rare path (escapes |is| >= 256): patch those lines with
                      * the in-register |is|^(4/3); one block, so the loop above
@@ -1556,20 +1585,21 @@ void launch_frame(const uint8_t *in_host, uint32_t in_have, const uint64_t *in_o
  * (st_tail_in, when given, holds the streams' state in place of st) */
 void launch_synth(const FrameRec *rec, const int16_t *is_buf, const UnitMeta *meta, const DevTables *tab,
                   StreamState *st, void *pcm, bool f32, int n_streams, int F, int kinds, int seg_len, float *st_tail,
-                  const float *st_tail_in, const uint32_t *fam, uint32_t seq, hipStream_t strm) {
+                  const float *st_tail_in, const uint32_t *fam, uint32_t seq, int n_cu, hipStream_t strm) {
     const int waves = n_streams * ((F + seg_len - 1) / seg_len);
     /* the family variants in `kinds` (bit 0 MPEG-1, bit 1 LSF; a batch
      * launches both); a workgroup without a stream of its variant exits
      * after its streams' scalar loads.  With the family word (fam, seq; wide
-     * demux) the LSF variant runs a persistent grid of at most SYN_LSF_GRID
-     * workgroups that all leave at once on an all-MPEG-1 batch (its 16 384
-     * workgroups' dispatch and loads cost 39 us per C3 step) */
-#define SYN_LSF_GRID 1024
+     * demux) the LSF variant runs a persistent grid of one resident round
+     * (3 workgroups of 4 waves per CU at 3 waves / SIMD) that all leave at
+     * once on an all-MPEG-1 batch (its 16 384 workgroups' dispatch and loads
+     * cost 39 us per C3 step) */
+    const int lsf_grid = 3 * (n_cu > 0 ? n_cu : 256);
 #define MP3D_SYNTH_LAUNCH(F32_, LSF_)                                                                              \
     do {                                                                                                           \
         constexpr int NW = SynCfg<false, LSF_>::WAVES;                                                             \
         int nb = (waves + NW - 1) / NW;                                                                            \
-        if (LSF_ && fam && nb > SYN_LSF_GRID) nb = SYN_LSF_GRID;                                                   \
+        if (LSF_ && fam && nb > lsf_grid) nb = lsf_grid;                                                           \
         hipLaunchKernelGGL((k_synth<false, F32_, LSF_>), dim3(nb), dim3(64 * NW), 0, strm, rec, is_buf, meta,       \
                            (const float *)nullptr, (const uint8_t *)nullptr, (const uint8_t *)nullptr, tab, st, pcm,  \
                            n_streams, F, 2, 0, seg_len, st_tail, st_tail_in, LSF_ ? fam : nullptr, seq);           \
