@@ -477,8 +477,6 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
     auto dma_is = [&](int g, int nz0, int nz1) {
         const int lo = opaque(lane * 4);
         const uint32_t lds0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uintptr_t)(lds_cf32 *)(const float *)isq);
-        const int nzm = __builtin_amdgcn_readfirstlane(nz0 > nz1 ? nz0 : nz1);
-        const int np = nzm <= 256 ? 2 : (nzm <= 384 ? 3 : 5);
 #pragma unroll
         for (int c = 0; c < 2; c++) {
             const uint64_t ra = isb + (uint64_t)(uint32_t)(g * gb + c * 1152);
@@ -486,23 +484,18 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                               (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(ra >> 32)) & 0xFFFFu,
                               (uint32_t)__builtin_amdgcn_readfirstlane(2 * (c ? nz1 : nz0)), 0x00020000u};
             uint32_t keep;
-            /* only the pieces phase Q reads: its live chunks (i < 2, 3 or 5
-             * by max(nz_end), the same rule as its requantiser copies) */
-#define SYN_DMA_HEAD "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t" \
-                     "buffer_load_dword %1, %3, 0 offen lds\n\tbuffer_load_dword %1, %3, 0 offen offset:256 lds\n\t"
-#define SYN_DMA_ARGS : "=&s"(keep) : "v"(lo), "s"(lds0 + 1280u * c), "s"(rs) : "memory"
-            if (np == 2)
-                __asm__ volatile(SYN_DMA_HEAD "s_mov_b32 m0, %0" SYN_DMA_ARGS);
-            else if (np == 3)
-                __asm__ volatile(SYN_DMA_HEAD "buffer_load_dword %1, %3, 0 offen offset:512 lds\n\t"
-                                              "s_mov_b32 m0, %0" SYN_DMA_ARGS);
-            else
-                __asm__ volatile(SYN_DMA_HEAD "buffer_load_dword %1, %3, 0 offen offset:512 lds\n\t"
-                                              "buffer_load_dword %1, %3, 0 offen offset:768 lds\n\t"
-                                              "buffer_load_dword %1, %3, 0 offen offset:1024 lds\n\t"
-                                              "s_mov_b32 m0, %0" SYN_DMA_ARGS);
-#undef SYN_DMA_HEAD
-#undef SYN_DMA_ARGS
+            __asm__ volatile("s_mov_b32 %0, m0\n\t"
+                             "s_mov_b32 m0, %2\n\t"
+                             "s_nop 0\n\t"
+                             "buffer_load_dword %1, %3, 0 offen lds\n\t"
+                             "buffer_load_dword %1, %3, 0 offen offset:256 lds\n\t"
+                             "buffer_load_dword %1, %3, 0 offen offset:512 lds\n\t"
+                             "buffer_load_dword %1, %3, 0 offen offset:768 lds\n\t"
+                             "buffer_load_dword %1, %3, 0 offen offset:1024 lds\n\t"
+                             "s_mov_b32 m0, %0"
+                             : "=&s"(keep)
+                             : "v"(lo), "s"(lds0 + 1280u * c), "s"(rs)
+                             : "memory");
         }
     };
     auto load_is = [&](int g, int nz0, int nz1) {
