@@ -662,6 +662,35 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
              * the other waves' VALU phases; A/B SP2: -2 % k_synth on C3; the
              * synth-only entry measured within noise, so it stays at 0) */
             if (!SRC_XR) __builtin_amdgcn_s_setprio(1);
+            bool fusedq = false; /* phase Q's fused requantiser ran */
+            /* phase I's input: lane (ch, sb)'s 18 lines and the alias
+             * neighbours up[k] = x_{sb-1}[17 - k], dn[k] = x_{sb+1}[k] */
+            float xf[18], up[8], dn[8];
+            /* ... read back from the xr scatter (after the wave's LDS stores
+             * land), at the end of each scatter path of phase Q (as one
+             * read after the paths merge, the fused path's xf was held
+             * across the scatter paths' registers and spilled) */
+            auto xin = [&]() {
+                wave_sync();
+                const int lx = opaque((int)(threadIdx.x & 63));
+                const int base = (lx >> 5) * 576 + 18 * (lx & 31), sbx = lx & 31;
+#pragma unroll
+                for (int i = 0; i < 9; i++) {
+                    const float2 v = *(const float2 *)&sBuf[base + 2 * i];
+                    xf[2 * i] = v.x;
+                    xf[2 * i + 1] = v.y;
+                }
+                const int pb = sbx ? base - 8 : base, nb = sbx < 31 ? base + 18 : base;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const float2 p = *(const float2 *)&sBuf[pb + 2 * i];
+                    const float2 n = *(const float2 *)&sBuf[nb + 2 * i];
+                    up[7 - 2 * i] = p.x;
+                    up[6 - 2 * i] = p.y;
+                    dn[2 * i] = n.x;
+                    dn[2 * i + 1] = n.y;
+                }
+            };
             /* ---------------- phase Q: requantise + stereo -> LDS ---------- */
             if (SRC_XR) {
                 (void)fr;
@@ -698,6 +727,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                         }
                     }
                 }
+                xin();
             } else {
                 /* nz_end per channel (UnitMeta word 12, uniform): the 128-line
                  * chunks i at or past max(nz_end) are all zero, so their
@@ -719,9 +749,6 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                         for (int i = 0; i < 5; i++)
                             cis[c][i] = i < NI ? (PAR ? isq[320 * c + 64 * i + lane] : nis[c][i]) : 0u;
                 };
-                if (nlive == 2) read_cis(std::integral_constant<int, 2>{});
-                else if (nlive == 3) read_cis(std::integral_constant<int, 3>{});
-                else read_cis(std::integral_constant<int, 5>{});
                 /* UnitMeta into LDS for the (rare) intensity path; the common
                  * path reads the prefetched words straight from registers */
                 if (lane < nch * MW) ((uint32_t *)&Wd.m[0])[lane] = wm[cs]; /* lane / MW < nch, no division */
@@ -742,7 +769,14 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                 const int var[2] = {bt0 == 2 ? (mx0 ? 2 : 1) : 0, bt1 == 2 ? (mx1 ? 2 : 1) : 0};
                 const bool is_on = mode == 1 && nch == 2 && (mext & 1);
                 const bool ms_fold = mode == 1 && nch == 2 && mext == 2; /* M/S only: 1/sqrt2 in the scale */
-                const float isq = 0.70710678118654752f;
+                /* fused requantiser: MPEG-1 decode, long blocks in every
+                 * channel, neither intensity nor M/S (uniform).  With M/S a
+                 * lane pairs its lines with lane +- 32's (v_permlane32_swap
+                 * of a line with itself, then one FMA: bit-exact), but the 36
+                 * VALU per granule cost more than the LDS round trip saved
+                 * (A/B FQ: C3 +2 % k_synth) */
+                fusedq = PAR && var[0] == 0 && var[1] == 0 && !is_on && !ms_fold;
+                const float rsq2 = 0.70710678118654752f;
                 /* per-band scale 2^(q/4), lane = band idx (long b | 22 + 3 b + w);
                  * the lane's scalefactor byte comes from the prefetched meta
                  * words by one cross-lane read per channel */
@@ -801,6 +835,60 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                 __asm__ volatile("" : "+s"(k1024));
                 const uint32_t sc_base[2] = {(uint32_t)(uintptr_t)(lds_cf32 *)&Wd.scale[0][0],
                                              (uint32_t)(uintptr_t)(lds_cf32 *)&Wd.scale[1][0]};
+                const uint8_t *p43b = (const uint8_t *)T.p43s;
+                if (fusedq) {
+                    /* lane (ch, sb) requantises its own subband's 18 lines
+                     * (is[] words 9 sb .. 9 sb + 8 of its channel's prefetch
+                     * area, stride 9: conflict-free) straight into phase I's
+                     * registers: no xr scatter through LDS and no reads back;
+                     * phase I takes the alias neighbours by DPP lane shifts */
+                    const int lq = opaque((int)(threadIdx.x & 63));
+                    const int fc = lq >> 5, fsb = lq & 31;
+                    const uint32_t *iw = isq + 320 * fc + 9 * fsb;
+                    const uint32_t *lpw = &lpair[0][9 * fsb];
+                    const uint32_t scb = fc ? sc_base[1] : sc_base[0];
+                    uint32_t bigf = 0u;
+#pragma unroll
+                    for (int m = 0; m < 9; m++) {
+                        const uint32_t tv2 = lpw[m];
+                        uint32_t t;
+                        __asm__("v_pk_mad_u16 %0, %1, 4, %2 op_sel_hi:[1,0,0]" : "=v"(t) : "v"(iw[m]), "s"(k1024));
+                        bigf |= t;
+                        const float sc = *(lds_cf32 *)(uintptr_t)(scb | (tv2 & 0xFCu));
+                        xf[2 * m] = *(const float *)(p43b + (t & 0x7FCu)) * sc;
+                        xf[2 * m + 1] = *(const float *)(p43b + ((t >> 16) & 0x7FCu)) * sc;
+                    }
+                    if (__ballot((bigf & 0xF800F800u) != 0u)) {
+                        /* rare: escapes (|is| >= 256), the words read again */
+#pragma unroll
+                        for (int m = 0; m < 9; m++) {
+                            const uint32_t w = iw[m];
+#pragma unroll
+                            for (int e = 0; e < 2; e++) {
+                                const int v = (int)(int16_t)(e ? (w >> 16) : (w & 0xFFFFu));
+                                const int a = v < 0 ? -v : v;
+                                if ((uint32_t)(v + 256) >= 512u) {
+                                    const float mag = pow43_big(a) * *(lds_cf32 *)(uintptr_t)(scb | (lpw[m] & 0xFCu));
+                                    xf[2 * m + e] = v < 0 ? -mag : mag;
+                                }
+                            }
+                        }
+                    }
+                    if (PF == 0 && (gr == 0 || f + 1 < f1)) prefetch(2 * f + gr + 1, cs);
+                    /* the alias neighbours by DPP whole-wave shifts: lane
+                     * i - 1 (wave_shr) and i + 1 (wave_shl); across the
+                     * channel boundary (sb 31 | 0) they are not used */
+#pragma unroll
+                    for (int k = 0; k < 8; k++) {
+                        up[k] = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(xf[17 - k]), 0x138, 0xF, 0xF, false));
+                        dn[k] = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(xf[k]), 0x130, 0xF, 0xF, false));
+                    }
+                } else {
+                /* (read here, not before the band scales: read early, the
+                 * words were held through the fused path and spilled) */
+                if (nlive == 2) read_cis(std::integral_constant<int, 2>{});
+                else if (nlive == 3) read_cis(std::integral_constant<int, 3>{});
+                else read_cis(std::integral_constant<int, 5>{});
                 auto requant = [&](auto nic) {
                 constexpr int NI = decltype(nic)::value;
 #pragma unroll
@@ -821,7 +909,6 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                         __asm__("v_pk_mad_u16 %0, %1, 4, %2 op_sel_hi:[1,0,0]" : "=v"(t) : "v"(cis[c][i]), "s"(k1024));
                         bigacc |= t;
                         const float sc = *(lds_cf32 *)(uintptr_t)(sc_base[c] | (tv2 & 0xFCu));
-                        const uint8_t *p43b = (const uint8_t *)T.p43s;
                         XV(c, 2 * i) = *(const float *)(p43b + (t & 0x7FCu)) * sc;
                         XV(c, 2 * i + 1) = *(const float *)(p43b + ((t >> 16) & 0x7FCu)) * sc;
                     }
@@ -911,8 +998,8 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                                 XV(0, k) = lv * rr.x;
                                 XV(1, k) = lv * rr.y;
                             } else if (mext & 2) {
-                                XV(0, k) = (lv + rv) * isq;
-                                XV(1, k) = (lv - rv) * isq;
+                                XV(0, k) = (lv + rv) * rsq2;
+                                XV(1, k) = (lv - rv) * rsq2;
                             }
                         }
                     }
@@ -949,6 +1036,8 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                                 if (c < nch) scatter(i, c, xp[c][i]);
                         }
                 }
+                xin();
+                } /* !fusedq */
             }
             wave_sync();
 #undef XV
@@ -964,23 +1053,11 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
             f32x2 nvp[9]; /* the next overlap (folded sign convention) */
             {
                 const int base = ch * 576 + 18 * sb;
-                float x[18], up[8], dn[8];
-#pragma unroll
-                for (int i = 0; i < 9; i++) {
-                    const float2 v = *(const float2 *)&sBuf[base + 2 * i];
-                    x[2 * i] = v.x;
-                    x[2 * i + 1] = v.y;
-                }
-                const int pb = sb ? base - 8 : base, nb = sb < 31 ? base + 18 : base;
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const float2 p = *(const float2 *)&sBuf[pb + 2 * i];
-                    const float2 n = *(const float2 *)&sBuf[nb + 2 * i];
-                    up[7 - 2 * i] = p.x; /* up[k] = x_{sb-1}[17 - k] */
-                    up[6 - 2 * i] = p.y;
-                    dn[2 * i] = n.x;     /* dn[k] = x_{sb+1}[k]      */
-                    dn[2 * i + 1] = n.y;
-                }
+                /* the subband's lines and its neighbours' alias inputs,
+                 * defined at the end of every phase-Q path (xin / the fused
+                 * requantiser): one set of registers, no merge copies */
+                float(&x)[18] = xf;
+                (void)base;
                 /* alias reduction (ISO 2.4.3.4): all 31 boundaries (long),
                  * the first one (mixed), none (short) */
                 const bool upper = (bt != 2 && sb >= 1) || (bt == 2 && mixed && sb == 1);
