@@ -247,7 +247,9 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                             /* the nb bits after the first level's b1 = 32 - s1: (hi << b1) >> (32 - nb); a
                              * zero-width field (leaf, nb = 0) extracts 0.  The base by v_bfe + v_lshl_add
                              * (as (e1 & 0x7FF) << 2 the compiler spent three ops) */
-                            const uint32_t sub = (__builtin_amdgcn_ubfe(e1, 0, 11) << 2) + __builtin_amdgcn_ubfe(hi, s1 - nb, nb);
+                            uint32_t b11 = __builtin_amdgcn_ubfe(e1, 0, 11);
+                            __asm__("" : "+v"(b11)); /* one v_lshl_add below, not a shift + mask + add */
+                            const uint32_t sub = (b11 << 2) + __builtin_amdgcn_ubfe(hi, s1 - nb, nb);
                             const uint32_t i2 = (e1 & 0x8000u) ? sub : i1;
                             const uint32_t e = s_lut[i2];
                             const uint32_t x = (e >> 4) & 15u, y = e & 15u, len_c = (e >> 8) & 31u;

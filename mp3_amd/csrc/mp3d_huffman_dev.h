@@ -76,7 +76,10 @@ __device__ __forceinline__ uint32_t win32(const uint32_t *bits, uint32_t pos) {
 /* No index clamp: k_huffman reads only while pos is inside the lane's staged
  * segment (pos <= the unit end + 47 bits < its 2-word margin). */
 __device__ __forceinline__ void win64g(const uint32_t *bits, uint32_t pos, uint32_t &hi, uint32_t &lo) {
-    const uint32_t w = (pos + 31u) >> 5;
+    /* (the barrier keeps the word index whole, so its byte address is one
+     * v_lshl_add; combined, the compiler spent a shift, a mask and an add) */
+    uint32_t w = (pos + 31u) >> 5;
+    __asm__("" : "+v"(w));
     const uint32_t w0 = bits[(int)w - 1], w1 = bits[w], w2 = bits[w + 1];
     hi = __builtin_amdgcn_alignbit(w0, w1, 0u - pos);
     lo = __builtin_amdgcn_alignbit(w1, w2, 0u - pos);
