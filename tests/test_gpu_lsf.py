@@ -74,6 +74,52 @@ def test_mixed_family_batch():
         assert np.abs(got.astype(np.int32) - o.astype(np.int32)).max() <= 1, s
 
 
+def test_mixed_family_wide_batch_persistent_lsf_grid():
+    """A wide batch (k_walk demux) with 2 048 LSF streams among 4 096: k_walk
+    tags the family word, and the LSF k_synth variant runs its persistent
+    grid (one resident round, fewer workgroups than blocks, so each walks
+    several).  Bit-identical to the wave-per-stream demux path, which leaves
+    the family word out and launches one workgroup per block; a stride
+    sample within 1 LSB of the oracle; then an all-MPEG-1 call on the same
+    decoder (family word of an older call: the LSF grid leaves at once)."""
+    import os
+    n, F = 4096, 2
+    b1, o1, s1 = _gen.batch(_gen.C3, 611, n // 2, F, threads=8)
+    b2, o2, s2 = _gen.batch(LSF, 612, n // 2, F, threads=8)
+    buf = np.concatenate([b1, b2])
+    offs = np.empty(n, np.uint64)
+    sizes = np.empty(n, np.uint32)
+    offs[0::2], sizes[0::2] = o1, s1
+    offs[1::2], sizes[1::2] = o2 + len(b1), s2
+    dec = mp3_amd.BatchDecoder(n, F)
+    pcm_w, inf_w = dec.decode(buf, offs, sizes, F)
+    pcm_w, inf_w = pcm_w.copy(), inf_w.copy()
+    os.environ["MP3D_DEMUX"] = "wave"
+    try:
+        ref = mp3_amd.BatchDecoder(n, F)
+        pcm_v, inf_v = ref.decode(buf, offs, sizes, F)
+    finally:
+        os.environ.pop("MP3D_DEMUX", None)
+    assert np.array_equal(inf_w, inf_v)
+    assert np.array_equal(pcm_w, pcm_v)
+    for s in range(1, n, 258):  # odd slots: LSF
+        assert (inf_w[s]["samples"] == 576).all(), s
+        o = oracle_pcm16(bytes(buf[offs[s]:offs[s] + sizes[s]]))
+        got = mp3_amd.pcm_to_planar(pcm_w[s], inf_w[s])
+        assert np.abs(got.astype(np.int32) - o.astype(np.int32)).max() <= 1, s
+    # the next call: MPEG-1 streams only, fresh states
+    b3, o3, s3 = _gen.batch(_gen.C3, 613, n, F, threads=8)
+    dec2 = mp3_amd.BatchDecoder(n, F)
+    dec2.decode(buf, offs, sizes, F)           # tags the family word
+    dec2.reset()
+    pcm3, inf3 = dec2.decode(b3, o3, s3, F)    # no LSF stream: the LSF grid leaves
+    assert (inf3["samples"] == 1152).all()
+    for s in range(0, n, 511):
+        o = oracle_pcm16(bytes(b3[o3[s]:o3[s] + s3[s]]))
+        got = mp3_amd.pcm_to_planar(pcm3[s], inf3[s])
+        assert np.abs(got.astype(np.int32) - o.astype(np.int32)).max() <= 1, s
+
+
 def test_lsf_state_carries_across_calls():
     """Two calls of 4 frames == one call of 8 (reservoir, overlap, FIFO and
     the MPEG-family lock resident in HBM between calls)."""
