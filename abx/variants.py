@@ -403,6 +403,27 @@ _XM = ("            /* ---------------- phase M: matrixing on the matrix cores -
 VARS["XS4M"] = VARS["XS4"] + [_XQ, _XM]
 VARS["XS4Mb"] = VARS["XS4b"] + [_XQ, _XM]
 
+# r04: phase-Q wave priority off (SP0)
+VARS["SP0"] = [("            if (!SRC_XR) __builtin_amdgcn_s_setprio(1);\n            bool fusedq",
+                "            bool fusedq")]
+
+# r04: xin takes the alias neighbours by DPP wave shifts, not 8 LDS reads (XDPP)
+VARS["XDPP"] = [("""                const int pb = sbx ? base - 8 : base, nb = sbx < 31 ? base + 18 : base;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const float2 p = *(const float2 *)&sBuf[pb + 2 * i];
+                    const float2 n = *(const float2 *)&sBuf[nb + 2 * i];
+                    up[7 - 2 * i] = p.x;
+                    up[6 - 2 * i] = p.y;
+                    dn[2 * i] = n.x;
+                    dn[2 * i + 1] = n.y;
+                }""", """                (void)sbx;
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    up[k] = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(xf[17 - k]), 0x138, 0xF, 0xF, false));
+                    dn[k] = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(xf[k]), 0x130, 0xF, 0xF, false));
+                }""")]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
