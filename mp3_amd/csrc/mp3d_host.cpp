@@ -300,6 +300,10 @@ static int device_init(int device) {
     }
     HIPCHK(hipMalloc(&c.tables, sizeof(DevTables)));
     HIPCHK(hipMemcpy(c.tables, &host_tables, sizeof(DevTables), hipMemcpyHostToDevice));
+    /* the uploads above run on the null stream, and every handle's kernels
+     * on non-blocking streams, which do not order after it: complete them
+     * here, once per device */
+    HIPCHK(hipDeviceSynchronize());
     (void)hipDeviceGetAttribute(&c.n_cu, hipDeviceAttributeMultiprocessorCount, device);
     c.ready = true;
     return MP3D_OK;
@@ -550,8 +554,12 @@ extern "C" int mp3d_batch_create(int device, int max_streams, int max_frames, mp
         return MP3D_E_HIP;
     }
     for (int i = 0; i < 4; i++) (void)hipEventCreate(&b->ev[i]);
-    if (hipMemset(b->st, 0, sizeof(StreamState) * max_streams) != hipSuccess ||
-        hipMemset(b->d_work, 0, 256) != hipSuccess) {
+    /* zeroed on the handle's own stream and waited for: a null-stream
+     * hipMemset is asynchronous for device memory and does not order before
+     * kernels on non-blocking streams (a first call could read the previous
+     * owner's bytes as its streams' state) */
+    if (hipMemsetAsync(b->st, 0, sizeof(StreamState) * max_streams, b->own) != hipSuccess ||
+        hipMemsetAsync(b->d_work, 0, 256, b->own) != hipSuccess || hipStreamSynchronize(b->own) != hipSuccess) {
         mp3d_batch_destroy(b);
         return MP3D_E_HIP;
     }
