@@ -587,6 +587,19 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                          : "=&s"(keep)
                          : "v"(lo), "s"(lds0), "s"(rs), "s"(so)
                          : "memory");
+        /* and channel 1's last chunk (lines 512 .. 575, lanes < 32 only:
+         * half the lanes of a register pair) into the area's last 256 B */
+        if (xr_nch == 2) {
+            uint32_t keep1;
+            __asm__ volatile("s_mov_b32 %0, m0\n\t"
+                             "s_mov_b32 m0, %2\n\t"
+                             "s_nop 0\n\t"
+                             "buffer_load_dword %1, %3, %4 offen lds\n\t"
+                             "s_mov_b32 m0, %0"
+                             : "=&s"(keep1)
+                             : "v"(lo), "s"(lds0 + 2304u), "s"(rs), "s"(so + 2304 + 2048)
+                             : "memory");
+        }
     };
     auto load_xr = [&](int g) {
         const int lo = opaque(lane * 8);
@@ -594,7 +607,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
 #pragma unroll
         for (int c = XDMA ? 1 : 0; c < 2; c++)
 #pragma unroll
-            for (int i = 0; i < 5; i++) {
+            for (int i = 0; i < (XDMA ? 4 : 5); i++) { /* XDMA: channel 1's chunk 4 by DMA */
                 nxr[c][i] = (f32x2){0.f, 0.f};
                 if (c < xr_nch && (i < 4 || lane < 32))
                     nxr[c][i] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(
@@ -645,8 +658,10 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
             mode = (int)(r5 >> 22) & 3;
             mext = (int)(r5 >> 20) & 3;
         }
-        const bool active = ch < nch;
-        const uint64_t amask = __ballot(active); /* lanes of coded channels */
+        /* lanes of coded channels: channel 0's half, or all -- from nch
+         * alone, no lane id (held across the loop for a ballot, the lane id
+         * was the synth-only variant's last spill) */
+        const uint64_t amask = nch == 2 ? ~0ull : 0xFFFFFFFFull;
         const uint32_t(*lpair)[288] = T.lpair[sr];
 #pragma unroll /* the words' slot (cs) is then a constant per copy */
         for (int gr = PF == 2 ? 1 : 0; gr < (LSF || PF == 1 ? 1 : 2); gr++) { /* LSF: one granule per frame */
@@ -699,8 +714,11 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                 for (int c = 0; c < 2; c++)
 #pragma unroll
                     for (int i = 0; i < 5; i++)
-                        cx[c][i] = XDMA && c == 0 ? *(const f32x2 *)((const float *)isq + 2 * lane + 128 * i)
-                                                  : nxr[c][i];
+                        cx[c][i] = XDMA && (c == 0 || i == 4)
+                                       ? (c == 0 || (nch == 2 && lane < 32)
+                                              ? *(const f32x2 *)((const float *)isq + 576 * c + 2 * lane + 128 * i - 512 * c)
+                                              : (f32x2){0.f, 0.f})
+                                       : nxr[c][i];
                 bt0 = __builtin_amdgcn_readlane((int)nbt, 0);
                 mx0 = bt0 == 2 ? __builtin_amdgcn_readlane((int)nbt, 2) : 0;
                 if (nch == 2) {
@@ -1304,7 +1322,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                     } else if (f < f0) {
                         /* warm-up frame: state only, no PCM */
                     } else if (nch == 2) { /* (stereo frames take the other copy) */
-                    } else if (active) {
+                    } else if (ch == 0) { /* mono: channel 0's lanes */
                         if (F32) {
                             const int vo = vo_mo;
                             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o.x), r_pcm, vo + 256 * tp, so, 0);
