@@ -892,7 +892,6 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                             }
                         }
                     }
-                    if (PF == 0 && (gr == 0 || f + 1 < f1)) prefetch(2 * f + gr + 1, cs);
                     /* the alias neighbours by DPP whole-wave shifts: lane
                      * i - 1 (wave_shr) and i + 1 (wave_shl); across the
                      * channel boundary (sb 31 | 0) they are not used */
@@ -1022,9 +1021,6 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                         }
                     }
                 }
-                /* the next granule's loads fly during phases I, M, W (issued
-                 * after cis is consumed: fewer live registers in phase Q) */
-                if (PF == 0 && (LSF ? f + 1 < f1 : (gr == 0 || f + 1 < f1))) prefetch(LSF ? 2 * f + 2 : 2 * f + gr + 1, cs);
                 /* scatter in (short-block reordered) position; M/S-only frames
                  * store (L + R, L - R) from their own copy of the loop (as an
                  * in-place update before one scatter, the branch merge cost a
@@ -1056,6 +1052,12 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                 }
                 xin();
                 } /* !fusedq */
+                /* the next granule's loads fly during phases I, M, W (issued
+                 * after phase Q read this granule's words), from ONE call
+                 * site: issued in both requantiser paths, the loaded words
+                 * merged at the join with a register copy, i.e. a vmcnt(0)
+                 * wait that made the prefetch synchronous */
+                if (PF == 0 && (LSF ? f + 1 < f1 : (gr == 0 || f + 1 < f1))) prefetch(LSF ? 2 * f + 2 : 2 * f + gr + 1, cs);
             }
             wave_sync();
 #undef XV
