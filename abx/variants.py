@@ -424,6 +424,10 @@ VARS["XDPP"] = [("""                const int pb = sbx ? base - 8 : base, nb = s
                     dn[k] = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(xf[k]), 0x130, 0xF, 0xF, false));
                 }""")]
 
+# r04 timing probe (wrong output): k_walk's header chain alone, no side info / reservoir / record work (WCH)
+VARS["WCH"] = [("            if (cur + (uint32_t)fb <= len || cur + need <= len) {",
+                "            if (cur + (uint32_t)fb <= len) {\n                cur += (uint32_t)fb;\n            } else if (false) {")]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
