@@ -428,6 +428,12 @@ VARS["XDPP"] = [("""                const int pb = sbx ? base - 8 : base, nb = s
 VARS["WCH"] = [("            if (cur + (uint32_t)fb <= len || cur + need <= len) {",
                 "            if (cur + (uint32_t)fb <= len) {\n                cur += (uint32_t)fb;\n            } else if (false) {")]
 
+# r04: 2 ranking rounds per super-chunk (R2)
+VARS["R2"] = [("#define HUFF_ROUNDS 4", "#define HUFF_ROUNDS 2")]
+
+VARS["R6"] = [("#define HUFF_ROUNDS 4", "#define HUFF_ROUNDS 6")]
+VARS["R8b"] = [("#define HUFF_ROUNDS 4", "#define HUFF_ROUNDS 8")]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
