@@ -434,6 +434,9 @@ VARS["R2"] = [("#define HUFF_ROUNDS 4", "#define HUFF_ROUNDS 2")]
 VARS["R6"] = [("#define HUFF_ROUNDS 4", "#define HUFF_ROUNDS 6")]
 VARS["R8b"] = [("#define HUFF_ROUNDS 4", "#define HUFF_ROUNDS 8")]
 
+# r04: k_synth MPEG-1 / synth-only in one 16-wave workgroup per CU (W16)
+VARS["W16"] = [("    static constexpr int WAVES = DMA ? 8 : 4;", "    static constexpr int WAVES = DMA ? 16 : 4;")]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
