@@ -437,6 +437,36 @@ VARS["R8b"] = [("#define HUFF_ROUNDS 4", "#define HUFF_ROUNDS 8")]
 # r04: k_synth MPEG-1 / synth-only in one 16-wave workgroup per CU (W16)
 VARS["W16"] = [("    static constexpr int WAVES = DMA ? 8 : 4;", "    static constexpr int WAVES = DMA ? 16 : 4;")]
 
+# r04: persistent MPEG-1 k_synth (one resident round of workgroups, each wave walks blocks) (PST)
+VARS["PST"] = [
+    ("    if (!SRC_XR && !(LSF && fam)) {", "    if (!SRC_XR && LSF && !fam) {"),
+    ("""    if constexpr (LSF && !SRC_XR) {
+        for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x)
+            if (!run(blk)) break;
+    } else {
+        run(blockIdx.x);
+    }""", """    if constexpr (!SRC_XR) {
+        for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x)
+            if (!run(blk)) break;
+    } else {
+        run(blockIdx.x);
+    }"""),
+    ("        if (LSF_ && fam && nb > lsf_grid) nb = lsf_grid;                                                           \\",
+     "        if (LSF_ && fam && nb > lsf_grid) nb = lsf_grid;                                                           \\\n        if (!LSF_ && nb > 2 * (n_cu > 0 ? n_cu : 256)) nb = 2 * (n_cu > 0 ? n_cu : 256);                            \\"),
+]
+
+VARS["PST2"] = VARS["PST"] + [
+    ("""        synth_stream<SRC_XR, F32, LSF>(rec, is_buf, meta, xr_in, xr_bt, xr_mixed, tab, st, pcm, F, xr_nch, xr_sr,
+                                       seg_len, st_tail, st_tail_in, T, Wv[wid], s, seg, nseg, nullptr,
+                                       SynCfg<SRC_XR, LSF>::DMA ? s_isq[SynCfg<SRC_XR, LSF>::DMA ? wid : 0] : nullptr);""",
+     """        int z = blk;
+        __asm__("" : "+s"(z));
+        z -= blk; /* 0, unknown to the optimizer: the LDS bases are re-derived per stream, not hoisted */
+        synth_stream<SRC_XR, F32, LSF>(rec, is_buf, meta, xr_in, xr_bt, xr_mixed, tab, st, pcm, F, xr_nch, xr_sr,
+                                       seg_len, st_tail, st_tail_in, *(&T + z), Wv[wid + z], s, seg, nseg, nullptr,
+                                       SynCfg<SRC_XR, LSF>::DMA ? s_isq[(SynCfg<SRC_XR, LSF>::DMA ? wid : 0) + z] : nullptr);"""),
+]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
