@@ -467,6 +467,9 @@ VARS["PST2"] = VARS["PST"] + [
                                        SynCfg<SRC_XR, LSF>::DMA ? s_isq[(SynCfg<SRC_XR, LSF>::DMA ? wid : 0) + z] : nullptr);"""),
 ]
 
+VARS["NOSLPALL"] = [("FLAGS", "-fno-slp-vectorize")]
+VARS["UNR"] = [("FLAGS", "-mllvm"), ("FLAGS", "-unroll-threshold=400")]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
