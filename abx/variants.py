@@ -143,7 +143,7 @@ VARS = {
             ("    const uint32_t w0 = bits[w], w1 = bits[w + 1];",
              "    const uint32_t ln = " + LID + "; (void)w;\n    const uint32_t w0 = bits[ln], w1 = bits[ln + 64];")],
     "LUT0": [("const uint32_t e1 = s_lut[i1];", "const uint32_t e1 = s_lut[(i1 & ~63u) + (uint32_t)lane];"),
-             ("const uint32_t e = s_lut[i2];", "const uint32_t e = s_lut[(i2 & ~63u) + (uint32_t)lane];")],
+             ("const uint32_t e = s_lut[i2];", "const uint32_t e = s_lut[(i2 & ~63u) + (uint32_t)lane_now()];")],
     # k_huffman row stores: suppressed (compute kept) / coalesced into one
     # contiguous 1 KB per wave instruction (output wrong; timing only)
     "NS1": [("                        *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);",
@@ -172,6 +172,18 @@ VARS = {
     # r03: big_values groups wholly past the lane's big_values not stored (count1 or nothing reads them) (BVZ)
     "BVZ": [("                        *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);",
              "                        if (k < bv2) *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);")],
+    # round 5: big_values group stores only up to the end of the 128-B line holding the lane's last pair (BVL)
+    "BVL": [("                        *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);",
+             "                        if (k < ((bv2 + 63) & ~63)) *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);")],
+    # round 5 LDS bank-conflict diagnosis (output wrong; counters only): each read class made conflict-free
+    "CFW": [("    const uint32_t w0 = bits[(int)w - 1], w1 = bits[w], w2 = bits[w + 1];",
+             "    const int ln = lane_now();\n    const uint32_t w0 = bits[ln], w1 = bits[ln + 64], w2 = bits[ln + 128]; (void)w;")],
+    "CFL1": [("const uint32_t e1 = s_lut[i1];", "const uint32_t e1 = s_lut[(i1 & ~63u) + (uint32_t)lane_now()];")],
+    "CFL2": [("const uint32_t e = s_lut[i2];", "const uint32_t e = s_lut[(i2 & ~63u) + (uint32_t)lane_now()];")],
+    "CFC": [("                        const uint32_t e = s_lut[c1base + (hw >> c1sh)];",
+             "                        const uint32_t e = s_lut[((c1base + (hw >> c1sh)) & ~63u) + (uint32_t)lane];"),
+            ("                        se = s_c1s[(v << 4) | ((hw << lq) >> 28)];",
+             "                        se = s_c1s[(((v << 4) | ((hw << lq) >> 28)) & ~63u) + (uint32_t)lane];")],
     # timing only (C3 holds no LSF stream): the LSF k_synth launch skipped on int16 batches (NL)
     "NL": [("        if (kinds & 2) MP3D_SYNTH_LAUNCH(false, true);", "")],
     # r03: k_mdcopy quadruples by one unaligned 16-B load each instead of 16 + 4 B and four funnel shifts (UA1)

@@ -35,7 +35,9 @@
 extern "C" {
 #endif
 
-#define MP3D_ABI_VERSION 4
+/* 5: the state blob's synthesis history is partial window sums in float
+ *    units, with a format stamp (blobs of v4 are refused by set_state) */
+#define MP3D_ABI_VERSION 5
 
 #if defined(__GNUC__) || defined(__clang__)
 #define MP3D_API __attribute__((visibility("default")))
@@ -207,10 +209,12 @@ MP3D_API int mp3d_long_plan(const uint8_t *data, size_t bytes, int L, long long 
 /* ---- per-stream state save / restore (ABI v4) --------------------------- *
  * A stream's decoder state -- bit-reservoir carry, IMDCT overlap, synthesis
  * history, MPEG family, Xing/LAME tag, frame count -- is an opaque blob of
- * mp3d_state_bytes() bytes, valid for handles of the same ABI version.
+ * mp3d_state_bytes() bytes, valid for handles of the same ABI version and
+ * for either PCM sink (a stream may switch between int16 and float calls).
  * batch_get_state copies the state of streams [first, first + n) out of the
  * handle into buf; batch_set_state writes it into those slots (of this or
- * another handle).  A player seeks by saving the state at a frame boundary
+ * another handle) and fails with MP3D_E_ARG, writing nothing, when a blob
+ * lacks this version's format stamp (e.g. one saved by an ABI v4 build).  A player seeks by saving the state at a frame boundary
  * and restoring it before decoding from that frame's bytes again; a server
  * moves a stream between batches or GPUs the same way.  buf: host or device
  * memory.  Both order after the handle's last call and return when done.  */

@@ -385,6 +385,15 @@ static hipEvent_t end_event(mp3d_batch *b) {
     return b->ev_done;
 }
 
+/* StreamState slots [0, n) zeroed with their format stamp, on stream s (the
+ * caller orders / waits) */
+static hipError_t state_clear(StreamState *st, int n, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(st, 0, sizeof(StreamState) * (size_t)n, s);
+    if (e == hipSuccess)
+        e = hipMemset2DAsync(&st[0].fmt, sizeof(StreamState), MP3D_STATE_FMT_BYTE, sizeof(uint32_t), (size_t)n, s);
+    return e;
+}
+
 static int grow(void **p, size_t *cap, size_t need) {
     if (need <= *cap) return MP3D_OK;
     if (*p) HIPCHK(hipFree(*p));
@@ -558,7 +567,7 @@ extern "C" int mp3d_batch_create(int device, int max_streams, int max_frames, mp
      * hipMemset is asynchronous for device memory and does not order before
      * kernels on non-blocking streams (a first call could read the previous
      * owner's bytes as its streams' state) */
-    if (hipMemsetAsync(b->st, 0, sizeof(StreamState) * max_streams, b->own) != hipSuccess ||
+    if (state_clear(b->st, max_streams, b->own) != hipSuccess ||
         hipMemsetAsync(b->d_work, 0, 256, b->own) != hipSuccess || hipStreamSynchronize(b->own) != hipSuccess) {
         mp3d_batch_destroy(b);
         return MP3D_E_HIP;
@@ -596,7 +605,7 @@ extern "C" int mp3d_batch_reset(mp3d_batch *b) {
     int r = own_after_last(b);
     if (r) return r;
     b->tail_live = -1; /* the state is zeroed whole */
-    HIPCHK(hipMemsetAsync(b->st, 0, sizeof(StreamState) * b->max_streams, b->own));
+    HIPCHK(state_clear(b->st, b->max_streams, b->own));
     HIPCHK(hipStreamSynchronize(b->own));
     return MP3D_OK;
 }
@@ -690,8 +699,14 @@ static int prepare_geometry(mp3d_batch *b, const uint64_t *offsets, const uint32
     memcpy(g.h, offsets, sizeof(uint64_t) * n);
     memcpy(g.h + 2 * (size_t)n, sizes, sizeof(uint32_t) * n);
     /* growing md frees the old region: hipFree waits for the device */
+    const size_t md_was = b->md_cap;
     int r = grow((void **)&b->md, &b->md_cap, o + 8192);
     if (r) return r;
+    /* a new region starts zeroed: the Huffman staging reads whole words up
+     * to 2 past a unit's end, and a corrupt unit may decode past its
+     * payload -- those bits then read as zeros (FFmpeg's buffer padding),
+     * never as a previous allocation's bytes */
+    if (b->md_cap != md_was) HIPCHK(hipMemsetAsync(b->md, 0, b->md_cap, s));
     /* after the call that last read this slot */
     HIPCHK(hipStreamWaitEvent(b->copy, g.fresh ? g.freed : end_event(b), 0));
     HIPCHK(hipMemcpyAsync(g.d, g.h, 20 * (size_t)n, hipMemcpyHostToDevice, b->copy));
@@ -1073,7 +1088,7 @@ extern "C" int mp3d_batch_decode_long(mp3d_batch *b, const uint8_t *data, size_t
             ss[i] = (uint32_t)((e < N ? off[e] : bytes) - so[i]);
         }
         /* fresh decoder state for every virtual stream */
-        LCHK(hipMemsetAsync(b->st, 0, sizeof(StreamState) * ns, s));
+        LCHK(state_clear(b->st, ns, s));
         b->tail_live = -1; /* fresh states: no tail of the previous chunk */
         rc = batch_decode(b, din, so.data(), ss.data(), ns, F, seg_pcm, f32 != 0, nullptr, s, false);
         if (rc) goto done;
@@ -1492,6 +1507,21 @@ static int state_copy(mp3d_batch *b, int first, int n, void *dst, const void *sr
     if (r) return r;
     r = flush_tail(b, s);
     if (r) return r;
+    if (!out) {
+        /* every blob must carry this build's format stamp (StreamState.fmt):
+         * a blob of another state format would decode with wrong history */
+        std::vector<uint32_t> fmt((size_t)n);
+        const uint8_t *f0 = (const uint8_t *)src + offsetof(StreamState, fmt);
+        if (ptr_kind(src, b->device) == PTR_HOST) {
+            for (int i = 0; i < n; i++) memcpy(&fmt[i], f0 + sizeof(StreamState) * (size_t)i, sizeof(uint32_t));
+        } else {
+            HIPCHK(hipMemcpy2DAsync(fmt.data(), sizeof(uint32_t), f0, sizeof(StreamState), sizeof(uint32_t), (size_t)n,
+                                    hipMemcpyDefault, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+        for (int i = 0; i < n; i++)
+            if (fmt[i] != MP3D_STATE_FMT) return MP3D_E_ARG;
+    }
     StreamState *at = b->st + first;
     HIPCHK(hipMemcpyAsync(out ? dst : (void *)at, out ? (const void *)at : src, sizeof(StreamState) * (size_t)n,
                           hipMemcpyDefault, s));

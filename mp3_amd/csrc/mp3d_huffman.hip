@@ -410,7 +410,8 @@ void launch_huffman(const uint8_t *md, const uint64_t *md_off, const FrameRec *r
      * are fewer super-chunks than waves; the waves take super-chunks from the
      * counter as they finish, so uneven super-chunks balance themselves */
     int blocks = (supers + HUFF_WAVES - 1) / HUFF_WAVES;
-    blocks = blocks < n_cu ? (blocks > 0 ? blocks : 1) : n_cu;
+    const int cus = n_cu > 0 ? n_cu : 256; /* (device_init's attribute query failed) */
+    blocks = blocks < cus ? (blocks > 0 ? blocks : 1) : cus;
     /* the last ~2 rounds per wave as single-round work items (k_huffman) */
     const int small_units = std::min(n_units, 2 * blocks * HUFF_WAVES * 64);
     const int n_big = (n_units - small_units) / HUFF_SUPER;

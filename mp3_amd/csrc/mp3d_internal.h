@@ -82,10 +82,23 @@ struct StreamState {
      * 0 none yet, 1 MPEG-1, 2 MPEG-2 / 2.5 LSF.  Headers of the other
      * family are skipped as junk; k_synth runs one variant per family. */
     int32_t kind;
-    int32_t pad_[3];
-    float overlap[2][32][18];              /* IMDCT overlap                  */
-    float fifo[2][MP3D_FIFO_SLOTS][32];    /* last 15 matrixing outputs X    */
+    int32_t pad_[2];                       /* k_walk -> k_mdcopy: md end, next carry */
+    /* state format stamp, MP3D_STATE_FMT in every handle's slots (written by
+     * the host at create / reset, never by a kernel): set_state refuses a
+     * blob without it, e.g. one saved by a build whose fifo meant raw X */
+    uint32_t fmt;
+    float overlap[2][32][18];              /* IMDCT overlap (true values)    */
+    /* synthesis history as partial window sums (round 4): fifo[ch][t][j] =
+     * the terms of the NEXT granule's output slot t (< 15) that read this
+     * granule's matrixing outputs, in float-sink units (full scale 1.0):
+     * the int16 variant scales by 2^-15 on the way out and 2^15 on the way
+     * in (exact), so a stream may switch sinks between calls */
+    float fifo[2][MP3D_FIFO_SLOTS][32];
 };
+/* 0x05 in every byte: one hipMemset2D per slot array; 5 = the format of
+ * ABI v5 (fifo = partial sums in float units) */
+#define MP3D_STATE_FMT 0x05050505u
+#define MP3D_STATE_FMT_BYTE 0x05
 
 /* Huffman LUT layout (u16 entries, two levels, first level <= 8 bits):
  * leaf:    bit15 = 0, bits 8..12 code length, bits 4..7 x, bits 0..3 y,

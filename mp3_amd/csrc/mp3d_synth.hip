@@ -404,10 +404,14 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
 #pragma unroll
         for (int i = 0; i < 9; i++)
             ovp[i] = (f32x2){ovi[(ch * 32 + sb) * 18 + i], ovi[(ch * 32 + sb) * 18 + 17 - i]} * sgp[i & 1];
+        /* the state holds H_t in float-sink units: int16 sinks run the
+         * window in PCM units (taps x 2^15), so x 2^15 in (exact) */
+        const f32x2 hsc = bc(F32 ? 1.0f : 32768.0f);
 #pragma unroll
         for (int tp = 0; tp < 8; tp++)
             hp[tp] = (f32x2){ffi[(ch * MP3D_FIFO_SLOTS + 2 * tp) * 32 + sb],
-                             2 * tp + 1 < MP3D_FIFO_SLOTS ? ffi[(ch * MP3D_FIFO_SLOTS + 2 * tp + 1) * 32 + sb] : 0.f};
+                             2 * tp + 1 < MP3D_FIFO_SLOTS ? ffi[(ch * MP3D_FIFO_SLOTS + 2 * tp + 1) * 32 + sb] : 0.f} *
+                     hsc;
     } else {
 #pragma unroll
         for (int i = 0; i < 9; i++) ovp[i] = (f32x2){0.f, 0.f};
@@ -484,7 +488,11 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                               (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(ra >> 32)) & 0xFFFFu,
                               (uint32_t)__builtin_amdgcn_readfirstlane(2 * (c ? nz1 : nz0)), 0x00020000u};
             uint32_t keep;
-            __asm__ volatile("s_mov_b32 %0, m0\n\t"
+            /* lgkmcnt(0) first: this granule's LDS reads of the area (the
+             * fused requantiser's iw[] words may be waited on only where they
+             * are used, which the compiler can place after this block) */
+            __asm__ volatile("s_waitcnt lgkmcnt(0)\n\t"
+                             "s_mov_b32 %0, m0\n\t"
                              "s_mov_b32 m0, %2\n\t"
                              "s_nop 0\n\t"
                              "buffer_load_dword %1, %3, 0 offen lds\n\t"
@@ -1430,10 +1438,11 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
             ovo[(ch * 32 + sb) * 18 + i] = t.x;
             ovo[(ch * 32 + sb) * 18 + 17 - i] = t.y;
         }
+        const float hsc = F32 ? 1.0f : 1.0f / 32768.0f; /* to float-sink units (exact) */
 #pragma unroll
         for (int tp = 0; tp < 8; tp++) {
-            ffo[(ch * MP3D_FIFO_SLOTS + 2 * tp) * 32 + sb] = hp[tp].x;
-            if (2 * tp + 1 < MP3D_FIFO_SLOTS) ffo[(ch * MP3D_FIFO_SLOTS + 2 * tp + 1) * 32 + sb] = hp[tp].y;
+            ffo[(ch * MP3D_FIFO_SLOTS + 2 * tp) * 32 + sb] = hp[tp].x * hsc;
+            if (2 * tp + 1 < MP3D_FIFO_SLOTS) ffo[(ch * MP3D_FIFO_SLOTS + 2 * tp + 1) * 32 + sb] = hp[tp].y * hsc;
         }
     }
 }

@@ -26,7 +26,7 @@ def test_library_exports_all_declared_symbols():
     L = ctypes.CDLL(str(mp3_amd.LIB_PATH))
     for n in declared():
         assert hasattr(L, n), n
-    assert L.mp3d_abi_version() == 4
+    assert L.mp3d_abi_version() == 5
     assert mp3_amd.state_bytes() > 8000  # the opaque per-stream state blob
 
 

@@ -57,7 +57,10 @@ def test_calls_on_changing_streams_and_destroyed_stream():
     assert torch.equal(torch.cat(parts, 1), p_ref)
     assert np.array_equal(_state_view(st), _state_view(st_ref))
     dec.reset()
-    assert not dec.get_state(0, n).any()
+    z = dec.get_state(0, n)
+    assert (z[:, 540:544].copy().view(np.uint32) == 0x05050505).all()  # StreamState.fmt, the format stamp
+    z[:, 540:544] = 0
+    assert not z.any()
 
 
 def test_state_buffer_size_checks():
