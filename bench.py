@@ -337,17 +337,26 @@ def run_per_frame(args):
     import _golden
     import mp3_amd
     data, _ = _golden.case("keypress_128k_js")
-    L = mp3_amd.lib()
+    # the call through a pointer into the file (no per-call copy of the rest
+    # of the buffer, which Python's slicing would add to every call's time)
+    L = ctypes.CDLL(str(mp3_amd.LIB_PATH))
+    L.mp3d_decode_frame.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                    ctypes.POINTER(mp3_amd.FrameInfo)]
+    mp3_amd.lib()
     d = mp3_amd.Decoder(device=0)
+    data_np = np.frombuffer(data, np.uint8)
+    base = data_np.ctypes.data
     pcm = np.zeros(2304, np.int16)
+    pcm_p = pcm.ctypes.data
     info = mp3_amd.FrameInfo()
+    info_p = ctypes.byref(info)
 
     def one_pass():
         d.reset()
         pos, nf, lat = 0, 0, []
         while pos < len(data):
             t = time.perf_counter()
-            n = L.mp3d_decode_frame(d._h, data[pos:], len(data) - pos, pcm.ctypes.data, ctypes.byref(info))
+            n = L.mp3d_decode_frame(d._h, base + pos, len(data) - pos, pcm_p, info_p)
             lat.append(time.perf_counter() - t)
             if n < 0 or info.frame_bytes <= 0:
                 break
@@ -365,6 +374,54 @@ def run_per_frame(args):
         lats += lat
     dt = time.perf_counter() - t0
     lat_us = np.array(lats) * 1e6
+    # steady state of a long stream (the player's case: the read-ahead's
+    # next run decodes behind the served calls): a 512-frame 128 kbps golden
+    # stream, one call per frame, every call's latency; the first call of a
+    # pass (cold: nothing read ahead yet) reported apart
+    long_data, _ = _golden.case("long_c3_512")
+    long_np = np.frombuffer(long_data, np.uint8)
+    lbase = long_np.ctypes.data
+    sl, first = [], []
+    for _ in range(max(1, args.steps // 4)):
+        d.reset()
+        pos, k = 0, 0
+        while pos < len(long_data):
+            t = time.perf_counter()
+            n = L.mp3d_decode_frame(d._h, lbase + pos, len(long_data) - pos, pcm_p, info_p)
+            el = time.perf_counter() - t
+            if n < 0 or info.frame_bytes <= 0:
+                break
+            (first if k == 0 else sl).append(el)
+            pos += info.frame_bytes
+            k += 1
+    sl_us, first_us = np.array(sl) * 1e6, np.array(first) * 1e6
+    # the same with the calls paced (a busy wait between calls, as a player
+    # slower than the GPU's single-stream decode makes them): the next run
+    # then completes behind the served calls and no call waits for a refill
+    pace_us = 40.0
+    pl = []
+    d.reset()
+    pos, k = 0, 0
+    while pos < len(long_data):
+        t = time.perf_counter()
+        n = L.mp3d_decode_frame(d._h, lbase + pos, len(long_data) - pos, pcm_p, info_p)
+        el = time.perf_counter() - t
+        if n < 0 or info.frame_bytes <= 0:
+            break
+        if k:
+            pl.append(el)
+        pos += info.frame_bytes
+        k += 1
+        while time.perf_counter() - t < pace_us * 1e-6:
+            pass
+    pl_us = np.array(pl) * 1e6
+    steady = {"stream": "tests/golden/long_c3_512.mp3 (512 frames, 128 kbps 44.1 kHz joint stereo)",
+              "calls": int(sl_us.size), "median": float(np.median(sl_us)), "p90": float(np.percentile(sl_us, 90)),
+              "p99": float(np.percentile(sl_us, 99)), "max": float(sl_us.max()), "mean": float(sl_us.mean()),
+              "first_call_median": float(np.median(first_us)),
+              "frames_per_s": float(sl_us.size / (sl_us.sum() * 1e-6)),
+              "paced": {"pace_us": pace_us, "calls": int(pl_us.size), "median": float(np.median(pl_us)),
+                        "p99": float(np.percentile(pl_us, 99)), "max": float(pl_us.max())}}
     L32, _ = _oracle_libs()
     out = np.zeros((2, 64 * 1152), np.float32)
     nch, hz = ctypes.c_int(), ctypes.c_int()
@@ -382,10 +439,13 @@ def run_per_frame(args):
                        "streams_per_gpu": 1, "parallelism": "none (per-frame player call)"},
             "latency_us": {"median": float(np.median(lat_us)), "p90": float(np.percentile(lat_us, 90)),
                            "p99": float(np.percentile(lat_us, 99)), "mean": float(lat_us.mean())},
-            "readahead_frames": int(os.environ.get("MP3D_PF_READAHEAD", 16)),
+            "steady_latency_us": steady,
+            "readahead_frames": int(os.environ.get("MP3D_PF_READAHEAD", 32)),
             "note": "one call per frame as a player's loop makes them, the rest of the file passed each time: the "
                     "decoder reads up to readahead_frames frames ahead in one batch call and serves the next calls "
-                    "from it (MP3D_PF_READAHEAD=0: every call decodes its own frame)",
+                    "from it, while the run after it decodes behind them (MP3D_PF_READAHEAD=0: every call decodes "
+                    "its own frame).  latency_us: every call of the 22-frame file, each pass from reset, so one "
+                    "call in 22 is a cold start; steady_latency_us: a 512-frame stream, its first call apart",
             "roofline": None, "cpu_baseline": cpu}
 
 
@@ -403,6 +463,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true",
                     help="also time an RCCL PCM gather to rank 0 overlapped with the next step (reported apart)")
+    ap.add_argument("--gather-priority", default="normal", choices=("high", "normal"),
+                    help="stream priority of the process group's collectives (the gather); measured at world 1: "
+                         "neither overlaps the decode, whose kernels fill every CU's VGPRs (DESIGN §6)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse the "
                          "multi-rank path, e.g. several ranks on one GPU)")
@@ -460,7 +523,15 @@ def main():
             os.environ.setdefault("RANK", str(rank))
             os.environ.setdefault("WORLD_SIZE", str(world))
             torch.cuda.set_device(c.gpu)
-            dist.init_process_group("nccl", device_id=c.dev)
+            # the group's collectives on a high-priority stream (--gather-priority):
+            # the gather's RCCL kernels then take a CU as soon as one frees up,
+            # instead of queueing behind the decode's workgroups
+            opts = None
+            if args.gather_priority == "high":
+                from torch.distributed import ProcessGroupNCCL
+                opts = ProcessGroupNCCL.Options()
+                opts.is_high_priority_stream = True
+            dist.init_process_group("nccl", device_id=c.dev, pg_options=opts)
         else:
             if c.gpu is not None:
                 torch.cuda.set_device(c.gpu)
@@ -582,6 +653,7 @@ def main():
     # --- optional RCCL PCM gather, overlapped with the next step ----------
     gather = None
     if args.gather and use_group:
+        c.ms_decode = ms_per_step
         gather = time_gather(c, args, dist, shard, torch, sync)
 
     setup_all = shard.all_ranks(c.setup_s, c.dev)  # collective: every rank takes part
@@ -653,8 +725,19 @@ def time_gather(c, args, dist, shard, torch, sync):
     sync()
     dist.barrier()
     dt = shard.max_over_ranks(time.perf_counter() - t0, c.dev)
-    return {"ms_alone": alone * 1e3, "bytes_per_step": nbytes * c.world,
+    # rank 0's xGMI ingress bounds the gather at world > 1: it receives the
+    # world - 1 other shards over its 7 links.  XGMI_INGRESS is the nominal
+    # 7 x 153.6 GB/s; if that figure counts both directions, the
+    # one-way ingress and this bound are half of it
+    xgmi_bytes = nbytes * (c.world - 1)
+    bound = c.n * c.F * c.world / (xgmi_bytes / XGMI_INGRESS) if xgmi_bytes else None
+    return {"ms_alone": alone * 1e3, "bytes_per_step": nbytes * c.world, "xgmi_bytes_per_step": xgmi_bytes,
+            "xgmi_ingress_bound_frames_per_s": bound, "xgmi_ingress_assumed_bytes_per_s": XGMI_INGRESS,
+            "priority": args.gather_priority,
             "ms_per_step_decode_plus_gather": dt / args.steps * 1e3,
+            # the share of the gather hidden behind the decode: (decode + gather
+            # alone - both overlapped) / gather alone
+            "hidden_fraction": (c.ms_decode + alone * 1e3 - dt / args.steps * 1e3) / (alone * 1e3) if alone > 0 else None,
             "frames_per_s_with_gather": c.n * c.F * c.world * args.steps / dt,
             "overlapped": dist.get_backend() != "gloo",
             "world": c.world, "backend": dist.get_backend(),
@@ -665,6 +748,9 @@ def time_gather(c, args, dist, shard, torch, sync):
                         "; world 1: a one-rank RCCL group gathers rank 0's PCM to itself (device copy, no xGMI), "
                         "which runs the same init / async gather / wait code an 8-GPU run takes" if c.world == 1
                         else "")}
+
+
+XGMI_INGRESS = 7 * 153.6e9  # bytes/s into one MI355X over its 7 xGMI links (nominal)
 
 
 def decoder_bytes(n, F):

@@ -478,6 +478,189 @@ hipError_t upload_demux_constants(const uint16_t *frame_bytes) { return upload_d
 
 /* wide: k_walk + k_mdcopy (batches of many streams); else one k_demux wave
  * per stream (fewer launches: the per-frame decoder, small batches) */
+/* ------------------------------------------------------------------------ */
+/* k_demux_fp: one stream's run of pre-located, complete frames (the per-  */
+/* frame decoder's read-ahead runs, mp3d_host.cpp ra_fill: the host has     */
+/* found every frame, fo[f] = its header offset in the run's bytes, which  */
+/* the kernel reads from the mapped host buffer) demuxed frame-parallel in  */
+/* ONE workgroup, with the same results as k_demux: the waves parse the     */
+/* frames' headers and side info side by side (parse_frame), one wave runs  */
+/* the bit-reservoir map over them in order (resolve_frame, the only serial */
+/* step), then the waves write the records and copy the payloads in        */
+/* parallel.  It also does the run's state book-keeping that would         */
+/* otherwise be separate copies: the previous run's synthesis tail into     */
+/* StreamState (tail_in, may be null) and then the snapshot of the state   */
+/* before the run (snap) that a settle restores.                           */
+/* ------------------------------------------------------------------------ */
+#define FP_WAVES 16
+#define FP_MAX 64   /* frames per run (MP3D_PF_READAHEAD <= 64) */
+#define FP_PER 4    /* frames per wave */
+static_assert(FP_WAVES * FP_PER == FP_MAX, "k_demux_fp: frame slots");
+struct FpRes {      /* what the serial resolve needs of a parsed frame */
+    int fb, plen, mdb;
+    uint32_t need;
+    int p00, p01, p10, p11;
+    uint32_t flags; /* bit 0 lsf, 1 bad, 2 tag, 3 two channels */
+};
+struct FpOut {      /* what it decides */
+    uint32_t payload_md, md_bit, lens; /* lens: payload_len | payload_avail << 16 */
+    uint32_t gr_samples;              /* first_gr | samples << 8 */
+};
+__global__ void __launch_bounds__(64 * FP_WAVES)
+k_demux_fp(const uint8_t *__restrict__ in, uint32_t len, const uint32_t *__restrict__ fo, uint8_t *__restrict__ md,
+           StreamState *__restrict__ st, const float *__restrict__ tail_in, StreamState *__restrict__ snap,
+           FrameRec *__restrict__ rec, uint64_t *__restrict__ sideu, DevInfo *__restrict__ infos, int F, int opts) {
+    __shared__ FpRes s_res[FP_MAX];
+    __shared__ FpOut s_out[FP_MAX];
+    __shared__ uint32_t s_h1[FP_MAX];
+    __shared__ int s_fin[3];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    StreamState &S = st[0];
+    /* the previous run's final overlap + history (a segmented synthesis
+     * leaves them in the handle's tail) into the state, then the snapshot */
+    constexpr int TAILW = (int)(sizeof(S.overlap) + sizeof(S.fifo)) / 4;
+    if (tail_in)
+        for (int i = tid; i < TAILW; i += 64 * FP_WAVES) (&S.overlap[0][0][0])[i] = tail_in[i];
+    __syncthreads();
+    for (int i = tid; i < (int)(sizeof(StreamState) / 4); i += 64 * FP_WAVES)
+        ((uint32_t *)snap)[i] = ((const uint32_t *)&S)[i];
+    __syncthreads(); /* every read of the state before the run is done (the tag write below) */
+    const uint8_t *p0 = in;
+    uint8_t *dst = md;
+    const int carry_in = __builtin_amdgcn_readfirstlane(S.res_len);
+    const bool stream_start = __builtin_amdgcn_readfirstlane((int)S.frames) == 0;
+    if (wv == 0)
+        for (int i = lane; i < (carry_in + 3) / 4; i += 64) ((uint32_t *)dst)[i] = ((const uint32_t *)S.res)[i];
+    /* the wave's frames' header windows, all in flight together */
+    HdrWin w[FP_PER];
+#pragma unroll
+    for (int j = 0; j < FP_PER; j++) {
+        const int f = wv + FP_WAVES * j;
+        if (f < F) w[j] = load_win<SrcGlobal>(p0, len, fo[f], lane);
+    }
+    FrameRec r[FP_PER];
+    DevInfo inf[FP_PER];
+    uint32_t need[FP_PER];
+    bool has[FP_PER];
+#pragma unroll
+    for (int j = 0; j < FP_PER; j++) {
+        const int f = wv + FP_WAVES * j;
+        has[j] = false;
+        need[j] = 0u;
+        rec_init(r[j], 0u, inf[j]);
+        if (f >= F) continue;
+        const uint32_t cur = fo[f];
+        /* (the family was checked on the host: every frame's header is of
+         * the stream's family) */
+        const int fb = hdr_frame_bytes(win_byte(w[j], 1), win_byte(w[j], 2), 0);
+        FrameParse fp;
+        fp.fb = 0;
+        fp.sw = 0;
+        fp.h1 = 0u; /* stays 0: no header found (a valid one has h1 >= 0xE0) */
+        if (fb > 0) parse_frame<SrcGlobal>(w[j], p0, 0, cur, len, fb, stream_start && f == 0, opts, S, fp, r[j], inf[j], lane);
+        has[j] = fp.fb != 0;
+        need[j] = fp.need;
+        if (lane < 4) sideu[(size_t)f * 4 + lane] = fp.fb ? fp.sw : 0ull;
+        if (lane == 0) {
+            FpRes q;
+            q.fb = fp.fb; q.plen = fp.plen; q.mdb = fp.mdb; q.need = fp.need;
+            q.p00 = fp.p00; q.p01 = fp.p01; q.p10 = fp.p10; q.p11 = fp.p11;
+            q.flags = (fp.lsf ? 1u : 0u) | (fp.bad ? 2u : 0u) | (fp.tag ? 4u : 0u) | (fp.nch == 2 ? 8u : 0u);
+            s_res[f] = q;
+            s_h1[f] = fp.h1;
+        }
+    }
+    __syncthreads();
+    /* the bit-reservoir map, in stream order (one wave, uniform) */
+    if (wv == 0) {
+        uint32_t P = (uint32_t)carry_in;
+        int avail = carry_in, decoded = 0;
+        for (int f = 0; f < F; f++) {
+            const FpRes q = s_res[f];
+            FrameParse fp;
+            fp.fb = q.fb; fp.plen = q.plen; fp.mdb = q.mdb; fp.need = q.need;
+            fp.p00 = q.p00; fp.p01 = q.p01; fp.p10 = q.p10; fp.p11 = q.p11;
+            fp.lsf = q.flags & 1u; fp.bad = (q.flags >> 1) & 1u; fp.tag = (q.flags >> 2) & 1u;
+            fp.nch = (q.flags & 8u) ? 2 : 1;
+            fp.ngr = fp.lsf ? 1 : 2;
+            fp.have = (uint32_t)q.fb; /* complete frames */
+            FrameRec rr;
+            DevInfo ii;
+            rec_init(rr, P, ii);
+            rr.payload_len = (uint16_t)(q.plen > 0 ? q.plen : 0);
+            if (q.fb) {
+                decoded += resolve_frame(fp, P, avail, rr, ii);
+                (void)frame_body(fp, rr);
+            }
+            if (lane == 0) {
+                FpOut o;
+                o.payload_md = rr.payload_md;
+                o.md_bit = rr.md_bit;
+                o.lens = (uint32_t)rr.payload_len | (uint32_t)rr.payload_avail << 16;
+                o.gr_samples = (uint32_t)rr.first_gr | (uint32_t)ii.samples << 8;
+                s_out[f] = o;
+            }
+        }
+        if (lane == 0) {
+            s_fin[0] = (int)P;
+            s_fin[1] = avail;
+            s_fin[2] = decoded;
+        }
+    }
+    __syncthreads();
+    /* records and payloads, the wave's own frames (their parse results still
+     * in registers) */
+#pragma unroll
+    for (int j = 0; j < FP_PER; j++) {
+        const int f = wv + FP_WAVES * j;
+        if (f >= F) continue;
+        const FpOut o = s_out[f];
+        r[j].payload_md = o.payload_md;
+        if (has[j]) {
+            r[j].md_bit = o.md_bit;
+            r[j].payload_len = (uint16_t)(o.lens & 0xFFFFu);
+            r[j].payload_avail = (uint16_t)(o.lens >> 16);
+            r[j].first_gr = (uint8_t)(o.gr_samples & 0xFFu);
+            inf[j].samples = (int)(o.gr_samples >> 8);
+        }
+        if (lane == 0) {
+            rec[f] = r[j];
+            if (infos) infos[f] = inf[j];
+        }
+        if (has[j] && !(r[j].first_gr & REC_TAG)) {
+            const uint32_t body = (r[j].first_gr & REC_DROP) ? 4u : need[j];
+            copy_payload<SrcGlobal>(p0, dst, r[j], fo[f] + body, fo[f], lane);
+        }
+    }
+    __syncthreads(); /* every wave's md stores before the carry is read back */
+    if (wv == 0) {
+        const uint32_t P = (uint32_t)s_fin[0];
+        const int avail = s_fin[1];
+        int c = avail < MP3D_RES_BYTES ? avail : MP3D_RES_BYTES;
+        if ((uint32_t)c > P) c = (int)P;
+        for (int i = lane; i < c; i += 64) S.res[i] = dst[P - c + i];
+        /* the family of the last frame found (k_demux: of every frame) */
+        int kind = __builtin_amdgcn_readfirstlane(S.kind);
+        for (int f = 0; f < F; f++)
+            if (s_h1[f]) kind = hdr_kind(s_h1[f]);
+        if (lane == 0) {
+            S.res_len = c;
+            S.frames += s_fin[2];
+            S.kind = kind;
+        }
+    }
+}
+
+/* one pre-located run (k_demux_fp): in = its bytes (len), fo = its frame
+ * offsets, md = the handle's md region (stream 0 at offset 0) */
+void launch_demux_fp(const uint8_t *in, uint32_t len, const uint32_t *fo, uint8_t *md, StreamState *st,
+                     const float *tail_in, StreamState *snap, FrameRec *rec, uint64_t *sideu, void *infos, int F,
+                     int opts, hipStream_t strm) {
+    hipLaunchKernelGGL(k_demux_fp, dim3(1), dim3(64 * FP_WAVES), 0, strm, in, len, fo, md, st, tail_in, snap, rec,
+                       sideu, (DevInfo *)infos, F, opts);
+}
+
 void launch_demux(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len, uint8_t *md,
                   const uint64_t *md_off, StreamState *st, FrameRec *rec, uint64_t *sideu, void *infos, int n_streams,
                   int F, int opts, bool wide, uint32_t *fam, uint32_t seq, hipStream_t strm) {

@@ -190,6 +190,230 @@ template <class P> __device__ uint32_t parse_info_tag(P t, uint32_t n, uint32_t 
     return info;
 }
 
+/* One frame's header and side info, parsed from the header window at its
+ * sync position (ISO 2.4.1.3 / 2.4.1.7; 13818-3 for LSF): everything about
+ * the frame that does not depend on the frames before it.  The bit-reservoir
+ * map (resolve_frame) is the only serial step of a stream's demux: k_demux
+ * runs parse / resolve / emit frame by frame in one wave, k_demux_fp parses
+ * and emits the frames of a pre-located run in parallel around one serial
+ * resolve.  Uniform fields; sw is per lane (lane q < 4: unit q's side word). */
+struct FrameParse {
+    int fb;               /* frame bytes; 0: no frame (cut too short)         */
+    int nch, crc, side_bytes, ngr, plen, mdb;
+    uint32_t h1, h2, h3, have, need;
+    int p00, p01, p10, p11; /* part2_3_length of unit (gr, ch), by select     */
+    bool lsf, bad, tag;
+    uint64_t sw;
+    __device__ __forceinline__ int p23(int gr, int ch) const { return gr ? (ch ? p11 : p10) : (ch ? p01 : p00); }
+};
+
+/* parse the frame of fb bytes whose header is at stream offset cur (window
+ * w at cur); f0 = the stream's first frame of the stream's first call (the
+ * Xing/Info tag check); r / inf get the frame's fields.  The tag's LAME
+ * fields go to S (lane 0). */
+template <class M>
+__device__ __forceinline__ void parse_frame(const HdrWin &w, typename M::u8 *p0, uint64_t base, uint32_t cur,
+                                            uint32_t len, int fb, bool f0, int opts, StreamState &S, FrameParse &fp,
+                                            FrameRec &r, DevInfo &inf, int lane) {
+    fp.fb = 0;
+    fp.sw = 0;
+    fp.bad = fp.tag = false;
+    const uint32_t h1 = win_byte(w, 1), h2 = win_byte(w, 2), h3 = win_byte(w, 3);
+    const int nch = (h3 >> 6) == 3 ? 1 : 2;
+    const int crc = (h1 & 1) ? 0 : 2;
+    const bool lsf = hdr_kind(h1) == 2;
+    const int ngr = lsf ? 1 : 2;
+    const int side_bytes = lsf ? (nch == 1 ? 9 : 17) : (nch == 1 ? 17 : 32);
+    const uint32_t need = 4u + (uint32_t)crc + (uint32_t)side_bytes;
+    fp.h1 = h1; fp.h2 = h2; fp.h3 = h3;
+    fp.nch = nch; fp.crc = crc; fp.lsf = lsf; fp.ngr = ngr; fp.side_bytes = side_bytes; fp.need = need;
+    /* a final frame cut short still decodes (FFmpeg: the missing bytes read
+     * as zeros) once its header and side info are present */
+    if (!(cur + (uint32_t)fb <= len || cur + need <= len)) return;
+    const uint32_t have = min(len - cur, (uint32_t)fb);
+    const int plen = fb - 4 - crc - side_bytes;
+    fp.fb = fb; fp.have = have; fp.plen = plen;
+    r.frame_off = base + cur;
+    r.frame_bytes = (uint16_t)fb;
+    r.payload_len = (uint16_t)(plen > 0 ? plen : 0);
+    r.hdr1 = (uint8_t)h1; r.hdr2 = (uint8_t)h2; r.hdr3 = (uint8_t)h3;
+    r.nch = (uint8_t)nch;
+    r.side_off = (uint8_t)(4 + crc);
+    r.sr_idx = (uint8_t)hdr_sr_idx(h1, h2);
+    r.lsf = (uint8_t)lsf;
+    inf.frame_bytes = fb; inf.channels = nch; inf.hz = (int)MP3D_SAMPLE_RATE[r.sr_idx];
+    inf.layer = 3; inf.bitrate_kbps = (int)(c_frame_word[r.sr_idx][h2 >> 4] >> 16);
+    /* side info: bit offsets relative to the window's dword base */
+    const uint32_t sbit = 8u * (w.mis + 4u + (uint32_t)crc);
+    fp.mdb = (int)(win_bits64(w, sbit) >> (lsf ? 56 : 55));
+    const int q = lane & 3, qgr = q >> 1, qch = q & 1;
+    const uint32_t ub = sbit + side_unit_bit(nch, qgr, qch, lsf);
+    const bool unit_ok = lane < 4 && qch < nch && qgr < ngr;
+    uint64_t v59;
+    uint32_t low5; /* side word bits 4..0: scfsi << 1 (MPEG-1) | scalefac_compress >> 4 (LSF) */
+    if (lsf) {
+        /* 63-bit LSF unit (13818-3 2.4.1.7): part2_3 12, big_values 9,
+         * global_gain 8, scalefac_compress 9, window switching 1 + 22,
+         * scalefac_scale 1, count1table 1 -> the MPEG-1 layout with
+         * scalefac_compress bits 0..3 in its 4-bit slot, the
+         * intensity-right-channel flag in the preflag slot, bits 4..8 in the
+         * side word's low 5 bits */
+        const uint64_t v63 = win_bits64(w, ub) >> 1;
+        const uint32_t sfc9 = (uint32_t)(v63 >> 25) & 511u;
+        const uint64_t low25 = v63 & 0x1FFFFFFull;
+        const bool is_right = (h3 >> 6) == 1 && ((h3 >> 4) & 1) && qch == 1;
+        v59 = ((v63 >> 34) << 30) | ((uint64_t)(sfc9 & 15u) << 26) | ((low25 >> 2) << 3) | ((uint64_t)is_right << 2) |
+              (low25 & 3u);
+        low5 = sfc9 >> 4;
+    } else {
+        v59 = win_bits64(w, ub) >> 5;
+        low5 = (uint32_t)(win_bits64(w, sbit + 9 + (nch == 1 ? 5 : 3) + 4 * qch) >> 60) << 1;
+    }
+    const uint32_t myp23 = unit_ok ? (uint32_t)(v59 >> 47) : 0u;
+    /* FFmpeg drops the frame: big_values > 288, or window
+     * switching with the reserved block_type 0 */
+    const bool mybad = unit_ok && (((v59 >> 38) & 0x1FFu) > 288u || (v59 & (7ull << 23)) == (4ull << 23));
+    fp.sw = unit_ok ? (v59 << 5) | low5 : 0ull;
+    fp.p00 = __builtin_amdgcn_readlane((int)myp23, 0);
+    fp.p01 = __builtin_amdgcn_readlane((int)myp23, 1);
+    fp.p10 = __builtin_amdgcn_readlane((int)myp23, 2);
+    fp.p11 = __builtin_amdgcn_readlane((int)myp23, 3);
+    /* MP3D_OPT_CRC_CHECK: a protected frame whose CRC-16 mismatches is
+     * dropped like a bad one (FFmpeg handle_crc + explode) */
+    const bool crc_bad = (opts & MP3D_OPT_CRC_CHECK) && crc && !crc16_ok(w, (uint32_t)side_bytes, lane);
+    fp.bad = plen < 0 || __ballot(mybad) != 0ull || crc_bad;
+    const uint32_t tgo = 4u + (uint32_t)crc + (uint32_t)side_bytes;
+    fp.tag = f0 && plen >= 4 && have == (uint32_t)fb &&
+             ((win_byte(w, tgo) == 'X' && win_byte(w, tgo + 1) == 'i' && win_byte(w, tgo + 2) == 'n' &&
+               win_byte(w, tgo + 3) == 'g') ||
+              (win_byte(w, tgo) == 'I' && win_byte(w, tgo + 1) == 'n' && win_byte(w, tgo + 2) == 'f' &&
+               win_byte(w, tgo + 3) == 'o'));
+    if (fp.tag && lane == 0) S.tag_info = parse_info_tag(p0 + cur + tgo, (uint32_t)fb - tgo, S.tag_frames);
+}
+
+/* The serial step: the bit-reservoir map of a parsed frame (ISO 2.4.3.4
+ * main_data_begin; FFmpeg's underflow and drop rules).  P = md position of
+ * the next payload, avail = md bytes after the previous main-data end (both
+ * updated); sets r.first_gr, md_bit, payload_md, the dropped frame's
+ * payload_len, and inf.samples; returns 1 for a frame with audio. */
+__device__ __forceinline__ int resolve_frame(const FrameParse &fp, uint32_t &P, int &avail, FrameRec &r,
+                                             DevInfo &inf) {
+    r.payload_md = P;
+    if (fp.tag) {
+        r.first_gr = REC_TAG;
+        return 0;
+    }
+    if (fp.bad) {
+        /* FFmpeg drops the frame; its reservoir restarts as the frame's last
+         * min(512, bytes - 4) post-header bytes (mp_decode_frame) */
+        r.first_gr = REC_DROP;
+        r.payload_len = (uint16_t)(fp.fb - 4);
+        avail = fp.fb - 4 < MP3D_RES_BYTES ? fp.fb - 4 : MP3D_RES_BYTES;
+        P += (uint32_t)r.payload_len;
+        return 0;
+    }
+    int gr0 = 0;
+    uint32_t mdbit;
+    if (fp.mdb <= avail) {
+        mdbit = (P - (uint32_t)fp.mdb) * 8u;
+    } else {
+        uint32_t bits = (uint32_t)avail * 8u;
+        while (gr0 < fp.ngr && (int)(bits >> 3) < fp.mdb) {
+            for (int ch = 0; ch < fp.nch; ch++) bits += (uint32_t)fp.p23(gr0, ch);
+            gr0++;
+        }
+        mdbit = (P - (uint32_t)avail) * 8u + bits - 8u * (uint32_t)fp.mdb;
+    }
+    uint32_t end = mdbit;
+    for (int gr = gr0; gr < 2; gr++)
+        for (int ch = 0; ch < fp.nch; ch++) end += (uint32_t)fp.p23(gr, ch);
+    r.md_bit = mdbit;
+    r.first_gr = (uint8_t)gr0;
+    P += (uint32_t)fp.plen;
+    const int64_t after = (int64_t)P - (int64_t)((end + 7u) >> 3);
+    avail = after < 0 ? 0 : (int)after;
+    inf.samples = fp.lsf ? 576 : 1152;
+    return 1;
+}
+
+/* A resolved frame's payload bytes [L, payload_len) zero (cut short), then
+ * [0, L) from the stream at src_off into md at r.payload_md, in aligned
+ * words built by v_alignbit and the <= 3 edge bytes as bytes.  frame_at =
+ * the frame's header position (always in the stream). */
+template <class M>
+__device__ __forceinline__ void copy_payload(typename M::u8 *p0, uint8_t *__restrict__ dst, const FrameRec &r,
+                                             uint32_t src_off, uint32_t frame_at, int lane) {
+    typename M::u8 *src = p0 + src_off;
+    const uint32_t Pm = r.payload_md, L = r.payload_avail;
+    for (uint32_t i = L + lane; i < r.payload_len; i += 64) dst[Pm + i] = 0; /* cut-short final frame */
+    const uint32_t h = min((4u - (Pm & 3u)) & 3u, L);     /* head bytes up to an aligned word */
+    const uint32_t wb = (Pm + h) >> 2, we = (Pm + L) >> 2; /* whole words [wb, we)           */
+    /* tail bytes [t0, L) after the last whole word -- or after the head when
+     * there is none (an LSF payload can be < 8 bytes) */
+    const uint32_t t0 = 4u * we > Pm + h ? 4u * we - Pm : h; /* h <= t0 <= L */
+    /* edge-byte loads first, stored after the words' loads: every load of
+     * the payload is in flight before the first store waits (unconditional:
+     * lanes without an edge byte re-read the frame's first header byte, which
+     * is always in the stream) */
+    typename M::u8 *hb0 = p0 + frame_at;
+    const uint8_t hbv = *((uint32_t)lane < h ? src + lane : hb0);
+    const uint8_t tbv = *((uint32_t)lane < L - t0 ? src + t0 + lane : hb0);
+    if (wb < we) {
+        /* pointer arithmetic, not an integer round trip: the loads stay
+         * global_load (a flat load waits on lgkmcnt too) */
+        typename M::u8 *sb = src + (4u * wb - Pm);
+        const uint32_t mis = (uint32_t)((uintptr_t)sb & 3u);
+        const uint32_t sh = mis * 8u;
+        typename M::u32 *swd = (typename M::u32 *)(sb - mis);
+        /* all words in flight before the first store (straight-line, so no
+         * loop-header wait drains them early): one load latency per frame
+         * instead of one per 64-word round.  A payload is at most 1437 B
+         * (1441-B frame) = 360 words < 6 x 64.  Loads are unconditional
+         * (lanes past the payload re-read word 0) and the shift is
+         * branch-free (alignbit by 0 = lo): with a load under a branch the
+         * compiler's waitcnt pass loses track at the join and drains vmcnt
+         * before every store.  The high word is read only for a misaligned
+         * source (index select, not a branch): it then still holds payload
+         * bytes.  Both words are aligned dwords holding at least one payload
+         * byte, so no load leaves the pages of the caller's buffer. */
+        const uint32_t nwd = we - wb;
+        uint32_t v[6];
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+            const uint32_t k = 64u * j + (uint32_t)lane;
+            const uint32_t kk = k < nwd ? k : 0u;
+            v[j] = __builtin_amdgcn_alignbit(swd[sh ? kk + 1 : kk], swd[kk], sh);
+        }
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+            const uint32_t k = 64u * j + (uint32_t)lane;
+            if (k < nwd) ((uint32_t *)dst)[wb + k] = v[j];
+        }
+        for (uint32_t k = 384u + (uint32_t)lane; k < nwd; k += 64) { /* not reached (see above) */
+            const uint32_t l = swd[k];
+            ((uint32_t *)dst)[wb + k] = sh ? __builtin_amdgcn_alignbit(swd[k + 1], l, sh) : l;
+        }
+    }
+    if ((uint32_t)lane < h) dst[Pm + lane] = hbv;
+    if ((uint32_t)lane < L - t0) dst[Pm + t0 + lane] = tbv;
+}
+
+/* a resolved frame's payload_avail and copy source (the body after the
+ * header and side info; a dropped frame's after the header) */
+__device__ __forceinline__ uint32_t frame_body(const FrameParse &fp, FrameRec &r) {
+    const uint32_t body = (r.first_gr & REC_DROP) ? 4u : fp.need;
+    const uint32_t av = fp.have > body ? fp.have - body : 0u;
+    r.payload_avail = (uint16_t)(av < r.payload_len ? av : r.payload_len);
+    return body;
+}
+
+__device__ __forceinline__ void rec_init(FrameRec &r, uint32_t P, DevInfo &inf) {
+    r.frame_off = 0; r.md_bit = 0; r.payload_md = P; r.frame_bytes = 0; r.payload_len = 0;
+    r.hdr1 = r.hdr2 = r.hdr3 = 0; r.nch = 0; r.side_off = 4; r.first_gr = 0; r.sr_idx = 0; r.lsf = 0;
+    r.payload_avail = 0;
+    inf = {0, 0, 0, 0, 0, 0};
+}
+
 /* one stream's demux (k_demux's wave; also the per-frame k_frame's first
  * phase): stream s, lane 0..63 of the calling wave, its bytes [0, len) at p0
  * (global memory or LDS, M), base = their offset in the call's input (the
@@ -240,125 +464,24 @@ __device__ __forceinline__ void demux_stream(typename M::u8 *p0, uint64_t base, 
             if (fb > 0) break;
         }
         FrameRec r;
-        r.frame_off = 0; r.md_bit = 0; r.payload_md = P; r.frame_bytes = 0; r.payload_len = 0;
-        r.hdr1 = r.hdr2 = r.hdr3 = 0; r.nch = 0; r.side_off = 4; r.first_gr = 0; r.sr_idx = 0; r.lsf = 0;
-        r.payload_avail = 0;
-        DevInfo inf = {0, 0, 0, 0, 0, 0};
+        DevInfo inf;
+        rec_init(r, P, inf);
         uint64_t sw = 0; /* lane q < 4: side word of unit q = gr * 2 + ch */
         bool copy = false;
         uint32_t src_off = 0, frame_at = 0; /* payload and header positions in the stream */
         if (fb > 0) {
             if (w.pos != cur) w = load_win<M>(p0, len, cur, lane);
-            const uint32_t h1 = win_byte(w, 1), h2 = win_byte(w, 2), h3 = win_byte(w, 3);
-            const int nch = (h3 >> 6) == 3 ? 1 : 2;
-            const int crc = (h1 & 1) ? 0 : 2;
-            const bool lsf = hdr_kind(h1) == 2;
-            const int ngr = lsf ? 1 : 2;
-            const int side_bytes = lsf ? (nch == 1 ? 9 : 17) : (nch == 1 ? 17 : 32);
-            kind = hdr_kind(h1);
-            const uint32_t need = 4u + (uint32_t)crc + (uint32_t)side_bytes;
-            /* a final frame cut short still decodes (FFmpeg: the missing bytes
-             * read as zeros) once its header and side info are present */
-            if (cur + (uint32_t)fb <= len || cur + need <= len) {
-                const uint32_t have = min(len - cur, (uint32_t)fb);
-                const int plen = fb - 4 - crc - side_bytes;
-                r.frame_off = base + cur;
-                r.frame_bytes = (uint16_t)fb;
-                r.payload_len = (uint16_t)(plen > 0 ? plen : 0);
-                r.hdr1 = (uint8_t)h1; r.hdr2 = (uint8_t)h2; r.hdr3 = (uint8_t)h3;
-                r.nch = (uint8_t)nch;
-                r.side_off = (uint8_t)(4 + crc);
-                r.sr_idx = (uint8_t)hdr_sr_idx(h1, h2);
-                r.lsf = (uint8_t)lsf;
-                inf.frame_bytes = fb; inf.channels = nch; inf.hz = (int)MP3D_SAMPLE_RATE[r.sr_idx];
-                inf.layer = 3; inf.bitrate_kbps = (int)(c_frame_word[r.sr_idx][h2 >> 4] >> 16);
-                /* side info: bit offsets relative to the window's dword base */
-                const uint32_t sbit = 8u * (w.mis + 4u + (uint32_t)crc);
-                const int mdb = (int)(win_bits64(w, sbit) >> (lsf ? 56 : 55));
-                const int q = lane & 3, qgr = q >> 1, qch = q & 1;
-                const uint32_t ub = sbit + side_unit_bit(nch, qgr, qch, lsf);
-                const bool unit_ok = lane < 4 && qch < nch && qgr < ngr;
-                uint64_t v59;
-                uint32_t low5; /* side word bits 4..0: scfsi << 1 (MPEG-1) | scalefac_compress >> 4 (LSF) */
-                if (lsf) {
-                    /* 63-bit LSF unit (13818-3 2.4.1.7): part2_3 12, big_values 9,
-                     * global_gain 8, scalefac_compress 9, window switching 1 +
-                     * 22, scalefac_scale 1, count1table 1 -> the MPEG-1 layout
-                     * with scalefac_compress bits 0..3 in its 4-bit slot, the
-                     * intensity-right-channel flag in the preflag slot, bits
-                     * 4..8 in the side word's low 5 bits */
-                    const uint64_t v63 = win_bits64(w, ub) >> 1;
-                    const uint32_t sfc9 = (uint32_t)(v63 >> 25) & 511u;
-                    const uint64_t low25 = v63 & 0x1FFFFFFull;
-                    const bool is_right = (h3 >> 6) == 1 && ((h3 >> 4) & 1) && qch == 1;
-                    v59 = ((v63 >> 34) << 30) | ((uint64_t)(sfc9 & 15u) << 26) | ((low25 >> 2) << 3) |
-                          ((uint64_t)is_right << 2) | (low25 & 3u);
-                    low5 = sfc9 >> 4;
-                } else {
-                    v59 = win_bits64(w, ub) >> 5;
-                    low5 = (uint32_t)(win_bits64(w, sbit + 9 + (nch == 1 ? 5 : 3) + 4 * qch) >> 60) << 1;
-                }
-                const uint32_t myp23 = unit_ok ? (uint32_t)(v59 >> 47) : 0u;
-                /* FFmpeg drops the frame: big_values > 288, or
-                 * window switching with the reserved block_type 0 */
-                const bool mybad = unit_ok && (((v59 >> 38) & 0x1FFu) > 288u || (v59 & (7ull << 23)) == (4ull << 23));
-                sw = unit_ok ? (v59 << 5) | low5 : 0ull;
-                /* part2_3_length of unit (gr, ch), by select (an indexed
-                 * array would live in scratch) */
-                const int p00 = __builtin_amdgcn_readlane((int)myp23, 0), p01 = __builtin_amdgcn_readlane((int)myp23, 1),
-                          p10 = __builtin_amdgcn_readlane((int)myp23, 2), p11 = __builtin_amdgcn_readlane((int)myp23, 3);
-                auto p23 = [&](int gr, int ch) { return gr ? (ch ? p11 : p10) : (ch ? p01 : p00); };
-                /* MP3D_OPT_CRC_CHECK: a protected frame whose CRC-16 mismatches
-                 * is dropped like a bad one (FFmpeg handle_crc + explode) */
-                const bool crc_bad = (opts & MP3D_OPT_CRC_CHECK) && crc && !crc16_ok(w, (uint32_t)side_bytes, lane);
-                const bool bad = plen < 0 || __ballot(mybad) != 0ull || crc_bad;
-                const uint32_t tgo = 4u + (uint32_t)crc + (uint32_t)side_bytes;
-                const bool tag = stream_start && f == 0 && plen >= 4 && have == (uint32_t)fb &&
-                                 ((win_byte(w, tgo) == 'X' && win_byte(w, tgo + 1) == 'i' && win_byte(w, tgo + 2) == 'n' &&
-                                   win_byte(w, tgo + 3) == 'g') ||
-                                  (win_byte(w, tgo) == 'I' && win_byte(w, tgo + 1) == 'n' && win_byte(w, tgo + 2) == 'f' &&
-                                   win_byte(w, tgo + 3) == 'o'));
-                if (tag) {
-                    r.first_gr = REC_TAG;
-                    if (lane == 0) S.tag_info = parse_info_tag(p0 + cur + tgo, (uint32_t)fb - tgo, S.tag_frames);
-                } else if (bad) {
-                    /* FFmpeg drops the frame; its reservoir restarts as the frame's
-                     * last min(512, bytes - 4) post-header bytes (mp_decode_frame) */
-                    r.first_gr = REC_DROP;
-                    r.payload_len = (uint16_t)(fb - 4);
-                    avail = fb - 4 < MP3D_RES_BYTES ? fb - 4 : MP3D_RES_BYTES;
-                    P += (uint32_t)r.payload_len;
-                } else {
-                    int gr0 = 0;
-                    uint32_t mdbit;
-                    if (mdb <= avail) {
-                        mdbit = (P - (uint32_t)mdb) * 8u;
-                    } else {
-                        uint32_t bits = (uint32_t)avail * 8u;
-                        while (gr0 < ngr && (int)(bits >> 3) < mdb) {
-                            for (int ch = 0; ch < nch; ch++) bits += (uint32_t)p23(gr0, ch);
-                            gr0++;
-                        }
-                        mdbit = (P - (uint32_t)avail) * 8u + bits - 8u * (uint32_t)mdb;
-                    }
-                    uint32_t end = mdbit;
-                    for (int gr = gr0; gr < 2; gr++)
-                        for (int ch = 0; ch < nch; ch++) end += (uint32_t)p23(gr, ch);
-                    r.md_bit = mdbit;
-                    r.first_gr = (uint8_t)gr0;
-                    P += (uint32_t)plen;
-                    const int64_t after = (int64_t)P - (int64_t)((end + 7u) >> 3);
-                    avail = after < 0 ? 0 : (int)after;
-                    inf.samples = lsf ? 576 : 1152;
-                    decoded++;
-                }
-                const uint32_t body = (r.first_gr & REC_DROP) ? 4u : need;
-                const uint32_t av = have > body ? have - body : 0u;
-                r.payload_avail = (uint16_t)(av < r.payload_len ? av : r.payload_len);
+            FrameParse fp;
+            parse_frame<M>(w, p0, base, cur, len, fb, stream_start && f == 0, opts, S, fp, r, inf, lane);
+            kind = hdr_kind(fp.h1);
+            if (fp.fb) {
+                sw = fp.sw;
+                decoded += resolve_frame(fp, P, avail, r, inf);
+                const uint32_t body = frame_body(fp, r);
                 copy = !(r.first_gr & REC_TAG);
                 src_off = cur + body;
                 frame_at = cur;
-                cur = have == (uint32_t)fb ? cur + (uint32_t)fb : len;
+                cur = fp.have == (uint32_t)fb ? cur + (uint32_t)fb : len;
             } else {
                 cur = len;
             }
@@ -373,63 +496,7 @@ __device__ __forceinline__ void demux_stream(typename M::u8 *p0, uint64_t base, 
          * load made the compiler drain vmcnt(0) before it, i.e. wait for the
          * window right here) */
         if (cur + 4 <= len && f + 1 < F) w = load_win<M>(p0, len, cur, lane);
-        if (copy) {
-            typename M::u8 *src = p0 + src_off;
-            const uint32_t Pm = r.payload_md, L = r.payload_avail;
-            for (uint32_t i = L + lane; i < r.payload_len; i += 64) dst[Pm + i] = 0; /* cut-short final frame */
-            const uint32_t h = min((4u - (Pm & 3u)) & 3u, L);     /* head bytes up to an aligned word */
-            const uint32_t wb = (Pm + h) >> 2, we = (Pm + L) >> 2; /* whole words [wb, we)           */
-            /* tail bytes [t0, L) after the last whole word -- or after the head
-             * when there is none (an LSF payload can be < 8 bytes) */
-            const uint32_t t0 = 4u * we > Pm + h ? 4u * we - Pm : h; /* h <= t0 <= L */
-            /* edge-byte loads first, stored after the words' loads: every
-             * load of the payload is in flight before the first store waits */
-            /* (unconditional: lanes without an edge byte re-read the frame's
-             * first header byte, which is always in the stream) */
-            typename M::u8 *hb0 = p0 + frame_at;
-            const uint8_t hbv = *((uint32_t)lane < h ? src + lane : hb0);
-            const uint8_t tbv = *((uint32_t)lane < L - t0 ? src + t0 + lane : hb0);
-            if (wb < we) {
-                /* pointer arithmetic, not an integer round trip: the loads
-                 * stay global_load (a flat load waits on lgkmcnt too) */
-                typename M::u8 *sb = src + (4u * wb - Pm);
-                const uint32_t mis = (uint32_t)((uintptr_t)sb & 3u);
-                const uint32_t sh = mis * 8u;
-                typename M::u32 *swd = (typename M::u32 *)(sb - mis);
-                /* all words in flight before the first store (straight-line,
-                 * so no loop-header wait drains them early): one load latency
-                 * per frame instead of one per 64-word round; the next header
-                 * window (issued above) lands with them.  A payload is at most
-                 * 1437 B (1441-B frame) = 360 words < 6 x 64. */
-                /* Loads are unconditional (lanes past the payload re-read word
-                 * 0) and the shift is branch-free (alignbit by 0 = lo): with a
-                 * load under a branch the compiler's waitcnt pass loses track
-                 * at the join and drains vmcnt before every store.  The high
-                 * word is read only for a misaligned source (index select, not
-                 * a branch): it then still holds payload bytes.  Both words
-                 * are aligned dwords holding at least one payload byte, so no
-                 * load leaves the pages of the caller's buffer. */
-                const uint32_t nwd = we - wb;
-                uint32_t v[6];
-#pragma unroll
-                for (int j = 0; j < 6; j++) {
-                    const uint32_t k = 64u * j + (uint32_t)lane;
-                    const uint32_t kk = k < nwd ? k : 0u;
-                    v[j] = __builtin_amdgcn_alignbit(swd[sh ? kk + 1 : kk], swd[kk], sh);
-                }
-#pragma unroll
-                for (int j = 0; j < 6; j++) {
-                    const uint32_t k = 64u * j + (uint32_t)lane;
-                    if (k < nwd) ((uint32_t *)dst)[wb + k] = v[j];
-                }
-                for (uint32_t k = 384u + (uint32_t)lane; k < nwd; k += 64) { /* not reached (see above) */
-                    const uint32_t l = swd[k];
-                    ((uint32_t *)dst)[wb + k] = sh ? __builtin_amdgcn_alignbit(swd[k + 1], l, sh) : l;
-                }
-            }
-            if ((uint32_t)lane < h) dst[Pm + lane] = hbv;
-            if ((uint32_t)lane < L - t0) dst[Pm + t0 + lane] = tbv;
-        }
+        if (copy) copy_payload<M>(p0, dst, r, src_off, frame_at, lane);
     }
     /* carry: the last min(avail, 512) md bytes become the next call's carry-in
      * (the wave's md stores complete before it reads them back) */

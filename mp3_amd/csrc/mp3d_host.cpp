@@ -14,7 +14,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/mp3d.h"
@@ -28,6 +30,8 @@ hipError_t upload_synth_constants(const float *, const float *, const float *, c
 hipError_t upload_demux_constants(const uint16_t *);
 void launch_demux(const uint8_t *, const uint64_t *, const uint32_t *, uint8_t *, const uint64_t *, StreamState *,
                   FrameRec *, uint64_t *, void *, int, int, int, bool, uint32_t *, uint32_t, hipStream_t);
+void launch_demux_fp(const uint8_t *, uint32_t, const uint32_t *, uint8_t *, StreamState *, const float *,
+                     StreamState *, FrameRec *, uint64_t *, void *, int, int, hipStream_t);
 void launch_huffman(const uint8_t *, const uint64_t *, const FrameRec *, const uint64_t *, const DevTables *, int16_t *,
                     UnitMeta *, int, int, int, bool, uint32_t *, hipStream_t);
 void launch_synth(const FrameRec *, const int16_t *, const UnitMeta *, const DevTables *, StreamState *, void *, bool, int,
@@ -759,15 +763,50 @@ static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offse
     return MP3D_OK;
 }
 
+/* One run of pre-located, complete frames of one stream (the per-frame
+ * decoder's read-ahead, mp3d_host.cpp ra_fill): the bytes and the frame
+ * offsets in mapped host memory, read by k_demux_fp directly (no copy); the
+ * previous run's synthesis tail flushed and the state snapshot taken inside
+ * that kernel; no stream geometry to stage (one stream at md offset 0).  A
+ * run costs three kernel launches and no copy. */
+struct FpRun {
+    const uint8_t *in;   /* device address of the run's bytes (mapped)    */
+    uint32_t len;
+    const uint32_t *fo;  /* device address of the frame offsets (mapped) */
+    const float *tail_in; /* the handle's live synthesis tail, or null     */
+    StreamState *snap;   /* receives the state before the run             */
+};
+static int run_front_fp(mp3d_batch *b, const FpRun &fp, int F, hipStream_t s, mp3d_frame_info *dev_infos) {
+    if (b->max_streams != 1 || F <= 0 || F > 64 || F > b->max_frames) return MP3D_E_ARG;
+    int r = call_begin(b, s);
+    if (r) return r;
+    if (b->md_cap < (size_t)fp.len + MP3D_RES_BYTES + 8192) return MP3D_E_CAPACITY; /* sized at create */
+    DeviceCtx &dc = g_dev[b->device];
+    if (b->timing) HIPCHK(hipEventRecord(b->ev[0], s));
+    if (++b->call_seq == 0) b->call_seq = 1;
+    b->fam_ok = false;
+    launch_demux_fp(fp.in, fp.len, fp.fo, b->md, b->st, fp.tail_in, fp.snap, b->rec, b->sideu,
+                    dev_infos ? (void *)dev_infos : b->d_infos, F, b->opts, s);
+    if (b->timing) HIPCHK(hipEventRecord(b->ev[1], s));
+    /* md offset of the one stream: a zero word of d_work (d_work[4..5]) */
+    launch_huffman(b->md, (const uint64_t *)(b->d_work + 4), b->rec, b->sideu, dc.tables, b->is_buf, b->meta, 1, F,
+                   dc.n_cu, true, b->d_work, s);
+    if (b->timing) HIPCHK(hipEventRecord(b->ev[2], s));
+    HIPCHK(hipGetLastError());
+    return MP3D_OK;
+}
+
 /* decode into int16 (f32 = false) or float32 PCM, both [n][F][2304] */
 /* kinds: k_synth family variants to launch (bit 0 MPEG-1, bit 1 LSF); 3 for
  * a batch, one bit for the per-frame decoder, which knows its frame's family */
 /* mapped: frames, pcm and infos are device-accessible pinned host memory
  * (the per-frame decoder): the kernels read and write them in place and the
  * call ends with one stream sync */
+/* async (mapped only): return without waiting; the caller records an event */
 static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets, const uint32_t *sizes, int n,
                         int F, void *pcm, bool f32, mp3d_frame_info *infos, void *hip_stream, bool overwrite,
-                        int kinds = 3, bool mapped = false, int seg_len_req = 0) {
+                        int kinds = 3, bool mapped = false, int seg_len_req = 0, const FpRun *fp = nullptr,
+                        bool async = false) {
     if (!b || !pcm) return MP3D_E_ARG;
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : b->own;
     CallEnd done{b, s};
@@ -777,8 +816,9 @@ static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *of
      * copied to the host after the call */
     const bool inf_host = infos && !mapped && !is_device_ptr(infos, b->device); /* or another GPU's */
     mp3d_frame_info *dinf = infos && !inf_host ? infos : b->d_infos;
-    int r = run_front(b, frames, offsets, sizes, n, F, s, &sync_needed, mapped, dinf);
+    int r = fp ? run_front_fp(b, *fp, F, s, dinf) : run_front(b, frames, offsets, sizes, n, F, s, &sync_needed, mapped, dinf);
     if (r) return r;
+    if (async && !mapped) return MP3D_E_ARG;
     const size_t PB = f32 ? sizeof(float) : sizeof(int16_t), row = 2304 * PB;
     const size_t pcm_bytes = (size_t)n * F * row;
     void *dpcm = pcm;
@@ -845,7 +885,7 @@ static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *of
         HIPCHK(hipMemcpyAsync(infos, b->d_infos, ib, hipMemcpyDefault, s));
         sync_needed = sync_needed || ptr_kind(infos, b->device) == PTR_HOST;
     }
-    if (sync_needed) HIPCHK(hipStreamSynchronize(s));
+    if (sync_needed && !async) HIPCHK(hipStreamSynchronize(s));
     return MP3D_OK;
 }
 
@@ -1003,7 +1043,7 @@ extern "C" int mp3d_long_plan(const uint8_t *data, size_t bytes, int L, long lon
 
 static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *offsets, const uint32_t *sizes, int n,
                         int F, void *pcm, bool f32, mp3d_frame_info *infos, void *hip_stream, bool overwrite,
-                        int kinds, bool mapped, int seg_len_req);
+                        int kinds, bool mapped, int seg_len_req, const FpRun *fp, bool async);
 
 extern "C" int mp3d_batch_decode_long(mp3d_batch *b, const uint8_t *data, size_t bytes, int L, void *pcm, int f32,
                                       long long max_frames, mp3d_frame_info *infos, long long *n_frames,
@@ -1142,51 +1182,93 @@ struct mp3d_dec {
     uint32_t *h_done = nullptr, *m_done = nullptr;
     uint32_t seq = 0;
     bool fused = false;
-    /* Read-ahead: the player hands over the rest of its
-     * buffer, so one call decodes up to ra_max of the frames found there in
-     * ONE batch call (n = 1, F = ra_max, frame-parallel synthesis segments)
-     * into mapped buffers, and the next calls are served from them after
-     * checking that the caller's bytes at the located frame are the same.
+    /* Read-ahead: the player hands over the
+     * rest of its buffer, so one call decodes up to ra_max of the frames
+     * found there in ONE batch call (n = 1, F = ra_max; the host-located
+     * frames demuxed frame-parallel by k_demux_fp, frame-parallel synthesis
+     * segments) into mapped buffers, and the next calls are served from them
+     * after checking that the caller's bytes at the located frame are the
+     * same.  Two runs: while the calls are served from one, the next run
+     * (the frames after it in the same buffer) decodes behind them, launched
+     * without waiting, so a player's steady state never waits for a refill.
      * Any other input (a seek, a new buffer, other options or sink) settles
-     * first: the state saved before the read-ahead is restored and the
-     * frames already served are decoded again (exact), then the call runs
-     * normally.  MP3D_PF_READAHEAD = frames per read-ahead (0 / 1: off). */
+     * first: the state saved before the run being served is restored and
+     * the frames already served are decoded again (exact), the next run is
+     * dropped, then the call runs normally.  MP3D_PF_READAHEAD = frames per
+     * run (0 / 1: off); MP3D_PF_RA_NEXT=0: no next run (one run at a time). */
     int ra_max = 0;
     int ra_seg = MP3D_PF_RA_SEG; /* MP3D_PF_RA_SEG env: synthesis segment of a read-ahead */
-    uint8_t *ra_in = nullptr;                              /* frames back to back (pinned)         */
-    uint8_t *ra_dev = nullptr;                             /* their device copy (one DMA): the
-                                                            * demux then reads HBM, not PCIe       */
-    void *ra_pcm = nullptr, *ra_pcm_m = nullptr;           /* [ra_max][2304] f32-sized slots       */
-    mp3d_frame_info *ra_inf = nullptr, *ra_inf_m = nullptr;
-    StreamState *snap = nullptr;                           /* device: the state before the read-ahead */
+    bool ra_next_on = true;
     struct RaEnt {
-        uint32_t off, len; /* the frame's bytes in ra_in */
+        uint32_t off, len; /* the frame's bytes in the run's in buffer */
         size_t pos;        /* bytes skipped before it in its call's buffer */
     };
-    std::vector<RaEnt> ra;
-    size_t ra_next = 0;
-    bool ra_f32 = false;
-    long ra_frames0 = 0; /* frames / kind before the read-ahead */
-    int ra_kind0 = 0;
+    struct Run {
+        uint8_t *in = nullptr;        /* pinned, mapped: frames back to back, then the u32 frame offsets */
+        uint8_t *in_m = nullptr;      /* its device address: k_demux_fp reads it in place (all frames at
+                                       * once, so one PCIe round trip per phase, not one per frame) */
+        void *pcm = nullptr, *pcm_m = nullptr; /* [ra_max][2304] f32-sized slots (mapped) */
+        mp3d_frame_info *inf = nullptr, *inf_m = nullptr;
+        StreamState *snap = nullptr;  /* device: the state before the run */
+        hipEvent_t done = nullptr;    /* the run's batch call has completed */
+        std::vector<RaEnt> ents;
+        uint32_t fo_at = 0;           /* byte offset of the frame offsets in in / dev */
+        bool f32 = false;
+        bool pending = false;         /* launched without waiting (the next run) */
+    } run[2];
+    int cur = 0;       /* run[cur] is served; run[cur ^ 1] is the next run, if any */
+    size_t ra_next = 0; /* next entry of run[cur] to serve */
     /* back-off: a settle that drops frames decoded ahead wasted
      * them, so the next ra_cool calls decode their own frame only; each such
      * settle doubles the pause (up to 64 calls), a read-ahead served whole
      * clears it.  A player that saves its state every frame then pays one
      * read-ahead per ~65 frames instead of two batch decodes per frame. */
     int ra_cool = 0, ra_backoff = 0;
+    /* The next run's launch (its HIP calls: three kernel launches and an
+     * event, tens of microseconds of host time) runs on a helper thread, so
+     * the call that hands it over returns at once; the frames are staged
+     * into the run's buffer by the calling thread first (the caller's buffer
+     * is valid only during its call).  Every call that touches the batch
+     * handle joins the helper first (ra_join); a call served from the
+     * current run does not.  MP3D_PF_RA_THREAD=0: launch on the calling
+     * thread. */
+    bool wk_on = true;
+    std::thread wk;
+    std::mutex wk_mu;
+    std::condition_variable wk_cv;
+    bool wk_job = false, wk_quit = false;
+    int wk_rc = 0;
+    struct WkJob {
+        Run *u;
+        uint32_t o;
+        int kinds;
+        bool f32;
+    } wk_arg{};
+    mp3d_dec::Run &R() { return run[cur]; }
+    mp3d_dec::Run &N() { return run[cur ^ 1]; }
 };
 
 static void dec_free(mp3d_dec *d) {
-    if (d->b) mp3d_batch_destroy(d->b);
+    if (d->wk.joinable()) {
+        {
+            std::lock_guard<std::mutex> lk(d->wk_mu);
+            d->wk_quit = true;
+        }
+        d->wk_cv.notify_all();
+        d->wk.join(); /* (after its last job) */
+    }
+    if (d->b) mp3d_batch_destroy(d->b); /* (waits for the handle's work, a next run included) */
     if (d->h_in) (void)hipHostFree(d->h_in);
     if (d->h_out) (void)hipHostFree(d->h_out);
     if (d->h_info) (void)hipHostFree(d->h_info);
     if (d->h_done) (void)hipHostFree(d->h_done);
-    if (d->ra_in) (void)hipHostFree(d->ra_in);
-    if (d->ra_dev) (void)hipFree(d->ra_dev);
-    if (d->ra_pcm) (void)hipHostFree(d->ra_pcm);
-    if (d->ra_inf) (void)hipHostFree(d->ra_inf);
-    if (d->snap) (void)hipFree(d->snap);
+    for (auto &u : d->run) {
+        if (u.in) (void)hipHostFree(u.in);
+        if (u.pcm) (void)hipHostFree(u.pcm);
+        if (u.inf) (void)hipHostFree(u.inf);
+        if (u.snap) (void)hipFree(u.snap);
+        if (u.done) (void)hipEventDestroy(u.done);
+    }
     delete d;
 }
 
@@ -1201,6 +1283,10 @@ extern "C" int mp3d_dec_create_on(int device, mp3d_dec **out) {
         const char *g = getenv("MP3D_PF_RA_SEG");
         if (g) d->ra_seg = std::max(1, atoi(g));
         if (d->ra_max < 2) d->ra_max = 0;
+        const char *nx = getenv("MP3D_PF_RA_NEXT");
+        d->ra_next_on = !(nx && !strcmp(nx, "0"));
+        const char *th = getenv("MP3D_PF_RA_THREAD");
+        d->wk_on = !(th && !strcmp(th, "0"));
     }
     int r = mp3d_batch_create(device, 1, std::max(1, d->ra_max), &d->b);
     if (r) {
@@ -1235,16 +1321,28 @@ extern "C" int mp3d_dec_create_on(int device, mp3d_dec **out) {
     }
     if (d->ra_max && d->m_in) {
         const size_t K = (size_t)d->ra_max;
-        if (hipHostMalloc((void **)&d->ra_in, K * MP3D_MAX_FRAME_BYTES + 64) != hipSuccess ||
-            hipMalloc((void **)&d->ra_dev, K * MP3D_MAX_FRAME_BYTES + 64) != hipSuccess ||
-            hipHostMalloc(&d->ra_pcm, K * 2304 * sizeof(float), co) != hipSuccess ||
-            hipHostMalloc((void **)&d->ra_inf, K * sizeof(mp3d_frame_info), co) != hipSuccess ||
-            hipMalloc((void **)&d->snap, sizeof(StreamState)) != hipSuccess ||
-            hipHostGetDevicePointer(&d->ra_pcm_m, d->ra_pcm, 0) != hipSuccess ||
-            hipHostGetDevicePointer((void **)&d->ra_inf_m, d->ra_inf, 0) != hipSuccess) {
+        /* the md region of a run (k_demux_fp stages no geometry): carry +
+         * payloads of K maximal frames + the staging margin, zeroed */
+        const size_t md_need = MP3D_RES_BYTES + K * MP3D_MAX_FRAME_BYTES + MP3D_MAX_FRAME_BYTES + 16 + 8192;
+        if (grow((void **)&d->b->md, &d->b->md_cap, md_need) != MP3D_OK ||
+            hipMemset(d->b->md, 0, d->b->md_cap) != hipSuccess) {
             dec_free(d);
             return MP3D_E_NOMEM;
         }
+        /* frames, 64 zero bytes, then the frame offsets (4-B aligned) */
+        const size_t in_bytes = K * MP3D_MAX_FRAME_BYTES + 64 + 4 + 4 * K;
+        for (auto &u : d->run)
+            if (hipHostMalloc((void **)&u.in, in_bytes, hipHostMallocMapped) != hipSuccess ||
+                hipHostGetDevicePointer((void **)&u.in_m, u.in, 0) != hipSuccess ||
+                hipHostMalloc(&u.pcm, K * 2304 * sizeof(float), co) != hipSuccess ||
+                hipHostMalloc((void **)&u.inf, K * sizeof(mp3d_frame_info), co) != hipSuccess ||
+                hipMalloc((void **)&u.snap, sizeof(StreamState)) != hipSuccess ||
+                hipHostGetDevicePointer(&u.pcm_m, u.pcm, 0) != hipSuccess ||
+                hipHostGetDevicePointer((void **)&u.inf_m, u.inf, 0) != hipSuccess ||
+                hipEventCreateWithFlags(&u.done, hipEventDisableTiming) != hipSuccess) {
+                dec_free(d);
+                return MP3D_E_NOMEM;
+            }
     } else {
         d->ra_max = 0;
     }
@@ -1264,11 +1362,23 @@ extern "C" void mp3d_dec_destroy(mp3d_dec *d) {
 }
 
 static int ra_settle(mp3d_dec *d);
+static int ra_join(mp3d_dec *d);
+
+/* forget both read-ahead runs; a run still decoding is waited for first
+ * (its host buffers are reused by the next fill) */
+static void ra_drop(mp3d_dec *d) {
+    for (auto &u : d->run) {
+        if (u.pending) (void)hipEventSynchronize(u.done);
+        u.pending = false;
+        u.ents.clear();
+    }
+    d->ra_next = 0;
+}
 
 extern "C" void mp3d_dec_reset(mp3d_dec *d) {
     if (!d) return;
-    d->ra.clear(); /* the state is zeroed whole */
-    d->ra_next = 0;
+    (void)ra_join(d);
+    ra_drop(d); /* the state is zeroed whole */
     d->ra_cool = d->ra_backoff = 0;
     (void)mp3d_batch_reset(d->b);
     d->frames = 0;
@@ -1284,6 +1394,10 @@ extern "C" int mp3d_dec_set_options(mp3d_dec *d, int flags) {
 
 extern "C" int mp3d_dec_stream_info(mp3d_dec *d, mp3d_stream_info *out) {
     if (!d || !out) return MP3D_E_ARG;
+    {
+        const int rj = ra_join(d);
+        if (rj) return rj;
+    }
     return mp3d_batch_stream_info(d->b, 1, out);
 }
 
@@ -1324,17 +1438,24 @@ static int pf_fused(mp3d_dec *d, uint32_t have, bool f32, bool lsf) {
     }
 }
 
-/* Settle a read-ahead: the frames decoded ahead but not served are
+/* Settle the read-ahead: the frames decoded ahead but not served are
  * dropped, and the device state is put back to "after the frames served":
- * the state saved before the read-ahead, then those frames decoded again
- * (the same bytes, so the same state).  A no-op without a read-ahead. */
+ * the state saved before the run being served, then its frames served so
+ * far decoded again (the same bytes, so the same state) -- or, when that
+ * run was served whole and only the next one is ahead, the state saved
+ * before the next run.  A no-op without a read-ahead. */
+static int ra_join(mp3d_dec *d);
 static int ra_settle(mp3d_dec *d) {
-    if (d->ra.empty()) return MP3D_OK;
+    {
+        const int rj = ra_join(d); /* a launch still on the helper thread */
+        if (rj) return rj;
+    }
+    mp3d_dec::Run &c = d->R(), &n = d->N();
+    if (c.ents.empty() && n.ents.empty()) return MP3D_OK;
     const size_t served = d->ra_next;
-    const bool all = served == d->ra.size();
-    d->ra_next = 0;
-    if (all) { /* every frame was served: the state is where the caller is */
-        d->ra.clear();
+    const bool cur_all = served == c.ents.size();
+    if (cur_all && n.ents.empty()) { /* every frame was served: the state is where the caller is */
+        ra_drop(d);
         d->ra_backoff = 0;
         return MP3D_OK;
     }
@@ -1342,71 +1463,160 @@ static int ra_settle(mp3d_dec *d) {
     d->ra_cool = d->ra_backoff;
     mp3d_batch *b = d->b;
     HIPCHK(hipSetDevice(b->device));
-    int r = own_after_last(b);
+    int r = own_after_last(b); /* (the next run, if any, is on the own stream before this) */
     if (r) return r;
-    b->tail_live = -1; /* the tail holds the state after the whole read-ahead */
-    HIPCHK(hipMemcpyAsync(b->st, d->snap, sizeof(StreamState), hipMemcpyDeviceToDevice, b->own));
-    if (served) {
-        const uint64_t off = 0;
-        const uint32_t len = d->ra[served - 1].off + d->ra[served - 1].len;
-        r = batch_decode(b, d->ra_dev, &off, &len, 1, (int)served, d->ra_pcm_m, d->ra_f32, d->ra_inf_m, nullptr, true,
-                         3, true, d->ra_seg);
-        if (r) return r;
-    } else {
+    b->tail_live = -1; /* the tail holds the state after the last run */
+    if (cur_all) {
+        HIPCHK(hipMemcpyAsync(b->st, n.snap, sizeof(StreamState), hipMemcpyDeviceToDevice, b->own));
         HIPCHK(hipStreamSynchronize(b->own));
+    } else {
+        HIPCHK(hipMemcpyAsync(b->st, c.snap, sizeof(StreamState), hipMemcpyDeviceToDevice, b->own));
+        if (served) {
+            const uint64_t off = 0;
+            const uint32_t len = c.ents[served - 1].off + c.ents[served - 1].len;
+            (void)off;
+            const FpRun fp = {c.in_m, len, (const uint32_t *)(c.in_m + c.fo_at), nullptr, c.snap};
+            r = batch_decode(b, c.in_m, &off, &len, 1, (int)served, c.pcm_m, c.f32, c.inf_m, nullptr, true, 3, true,
+                             d->ra_seg, &fp, false);
+            if (r) return r;
+        } else {
+            HIPCHK(hipStreamSynchronize(b->own));
+        }
     }
-    d->ra.clear();
+    ra_drop(d);
     return MP3D_OK;
 }
 
-/* Read ahead from the call's buffer: the complete frames found there (up to
- * ra_max, located exactly as consecutive calls would locate them) are
- * decoded in one batch call; returns 1 when the first of them is to be
- * served, 0 when there are too few frames (the single-frame path then). */
-static int ra_fill(mp3d_dec *d, const uint8_t *buf, size_t bytes, bool f32) {
-    if (!d->ra_max) return 0;
-    if (d->ra_cool > 0) { /* backing off after a wasted read-ahead */
-        d->ra_cool--;
-        return 0;
-    }
+/* Stage run u from the call's buffer [buf, buf + bytes): the complete
+ * frames found there (up to ra_max, located exactly as consecutive calls
+ * would locate them: the first one with the stream-start rules when first is
+ * set, the MPEG family locked to *kind once known) copied back to back into
+ * u.in, then their offsets.  Host work only.  Returns the frames (0 for
+ * fewer than 2: nothing staged); *o_out = their bytes, *kinds_out = their
+ * families. */
+static int ra_stage(mp3d_dec *d, mp3d_dec::Run &u, const uint8_t *buf, size_t bytes, bool first, int *kind,
+                    uint32_t *o_out, int *kinds_out) {
     size_t cur = 0;
     uint32_t o = 0;
-    int kind = d->kind, kinds = 0;
-    std::vector<mp3d_dec::RaEnt> ents;
+    int kinds = 0;
+    u.ents.clear();
     for (int j = 0; j < d->ra_max; j++) {
         size_t pos = 0, have = 0;
         int fb = -1;
-        if (pf_locate(buf + cur, bytes - cur, kind, d->frames == 0 && j == 0, false, &pos, &fb, &have) <= 0 ||
+        if (pf_locate(buf + cur, bytes - cur, *kind, first && j == 0, false, &pos, &fb, &have) <= 0 ||
             have < (size_t)fb)
             break;
-        memcpy(d->ra_in + o, buf + cur + pos, (size_t)fb);
-        ents.push_back({o, (uint32_t)fb, pos});
+        memcpy(u.in + o, buf + cur + pos, (size_t)fb);
+        u.ents.push_back({o, (uint32_t)fb, pos});
         const int k = host_frame_kind(buf + cur + pos);
-        if (!kind) kind = k; /* checked again when each is served */
+        if (!*kind) *kind = k; /* checked again when each is served */
         kinds |= k;
         o += (uint32_t)fb;
         cur += pos + (size_t)fb;
     }
-    if (ents.size() < 2) return 0;
+    if (u.ents.size() < 2) {
+        u.ents.clear();
+        return 0;
+    }
+    /* 64 zero bytes after the frames, then the frame offsets (k_demux_fp) */
+    memset(u.in + o, 0, 64);
+    u.fo_at = (o + 64 + 3) & ~3u;
+    for (size_t j = 0; j < u.ents.size(); j++) ((uint32_t *)(u.in + u.fo_at))[j] = u.ents[j].off;
+    *o_out = o;
+    *kinds_out = kinds;
+    return (int)u.ents.size();
+}
+
+/* Decode a staged run in one batch call -- synchronously, or launched
+ * without waiting (async: the next run; its done event is recorded). */
+static int ra_launch(mp3d_dec *d, mp3d_dec::Run &u, uint32_t o, int kinds, bool f32, bool async) {
     mp3d_batch *b = d->b;
     HIPCHK(hipSetDevice(b->device));
     int r = own_after_last(b);
-    if (!r) r = flush_tail(b, b->own);
     if (r) return r;
-    /* the state before the read-ahead, for ra_settle; the frames to HBM */
-    HIPCHK(hipMemcpyAsync(d->snap, b->st, sizeof(StreamState), hipMemcpyDeviceToDevice, b->own));
-    memset(d->ra_in + o, 0, 64);
-    HIPCHK(hipMemcpyAsync(d->ra_dev, d->ra_in, o + 64, hipMemcpyHostToDevice, b->own));
+    /* the previous run's synthesis tail is flushed into the state, and the
+     * state before this run saved to u.snap (for ra_settle), by k_demux_fp */
+    const float *tail = b->tail_live >= 0 ? b->st_tail[b->tail_live] : nullptr;
+    b->tail_live = -1;
     const uint64_t off = 0;
-    r = batch_decode(b, d->ra_dev, &off, &o, 1, (int)ents.size(), d->ra_pcm_m, f32, d->ra_inf_m, nullptr, true, kinds,
-                     true, d->ra_seg);
+    const FpRun fp = {u.in_m, o, (const uint32_t *)(u.in_m + u.fo_at), tail, u.snap};
+    r = batch_decode(b, u.in_m, &off, &o, 1, (int)u.ents.size(), u.pcm_m, f32, u.inf_m, nullptr, true, kinds, true,
+                     d->ra_seg, &fp, async);
     if (r) return r;
-    d->ra.swap(ents);
-    d->ra_next = 0;
-    d->ra_f32 = f32;
-    d->ra_frames0 = d->frames;
-    d->ra_kind0 = d->kind;
+    u.f32 = f32;
+    u.pending = async;
+    if (async) HIPCHK(hipEventRecord(u.done, b->own));
+    return MP3D_OK;
+}
+
+/* wait for the helper thread's launch, if one was handed over; its status */
+static int ra_join(mp3d_dec *d) {
+    if (!d->wk.joinable()) return MP3D_OK;
+    std::unique_lock<std::mutex> lk(d->wk_mu);
+    d->wk_cv.wait(lk, [d] { return !d->wk_job; });
+    const int rc = d->wk_rc;
+    d->wk_rc = 0;
+    return rc;
+}
+
+static void ra_worker(mp3d_dec *d) {
+    for (;;) {
+        std::unique_lock<std::mutex> lk(d->wk_mu);
+        d->wk_cv.wait(lk, [d] { return d->wk_job || d->wk_quit; });
+        if (!d->wk_job) return; /* quit */
+        const mp3d_dec::WkJob j = d->wk_arg;
+        lk.unlock();
+        const int rc = ra_launch(d, *j.u, j.o, j.kinds, j.f32, true);
+        lk.lock();
+        if (rc) j.u->ents.clear(); /* (the caller sees no next run, and rc at its next join) */
+        d->wk_rc = rc;
+        d->wk_job = false;
+        lk.unlock();
+        d->wk_cv.notify_all();
+    }
+}
+
+/* Fill run u synchronously: stage + launch + wait.  Returns 1 for a run of
+ * >= 2 frames, else 0 and nothing launched. */
+static int ra_fill(mp3d_dec *d, mp3d_dec::Run &u, const uint8_t *buf, size_t bytes, bool f32, bool first, int *kind) {
+    uint32_t o = 0;
+    int kinds = 0;
+    if (!ra_stage(d, u, buf, bytes, first, kind, &o, &kinds)) return 0;
+    const int r = ra_launch(d, u, o, kinds, f32, false);
+    if (r) {
+        u.ents.clear();
+        return r;
+    }
     return 1;
+}
+
+/* the next run: the frames after run[cur] in the call's buffer (which starts
+ * at run[cur]'s first frame), staged here and launched by the helper thread,
+ * decoding behind the calls served from run[cur] */
+static int ra_launch_next(mp3d_dec *d, const uint8_t *buf, size_t bytes, bool f32) {
+    if (!d->ra_next_on) return MP3D_OK;
+    size_t at = 0;
+    for (const auto &e : d->R().ents) at += e.pos + e.len;
+    if (at >= bytes) return MP3D_OK;
+    /* the family lock: the stream's, or its first frame's (run[cur]'s first) */
+    int kind = d->kind ? d->kind : host_frame_kind(buf + d->R().ents[0].pos);
+    mp3d_dec::Run &u = d->N();
+    uint32_t o = 0;
+    int kinds = 0;
+    if (!ra_stage(d, u, buf + at, bytes - at, false, &kind, &o, &kinds)) return MP3D_OK;
+    if (!d->wk_on) {
+        const int r = ra_launch(d, u, o, kinds, f32, true);
+        if (r) u.ents.clear();
+        return r;
+    }
+    if (!d->wk.joinable()) d->wk = std::thread(ra_worker, d);
+    {
+        std::lock_guard<std::mutex> lk(d->wk_mu);
+        d->wk_arg = {&u, o, kinds, f32};
+        d->wk_job = true;
+    }
+    d->wk_cv.notify_all();
+    return MP3D_OK;
 }
 
 static int decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, void *pcm, bool f32, bool last,
@@ -1421,33 +1631,66 @@ static int decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, void *pcm
      * MP3D_FRAME_LAST: decoded with the missing bytes as zeros (k_demux) */
     const int loc = pf_locate(buf, bytes, d->kind, d->frames == 0, last, &pos, &fb, &have);
     /* a frame read ahead: the same bytes at the same place, the same sink */
-    if (d->ra_next < d->ra.size()) {
-        const mp3d_dec::RaEnt &e = d->ra[d->ra_next];
-        if (!(loc > 0 && f32 == d->ra_f32 && pos == e.pos && have == (size_t)fb && (size_t)fb == e.len &&
-              !memcmp(buf + pos, d->ra_in + e.off, e.len))) {
+    auto same = [&](const mp3d_dec::Run &u, const mp3d_dec::RaEnt &e) {
+        return loc > 0 && f32 == u.f32 && pos == e.pos && have == (size_t)fb && (size_t)fb == e.len &&
+               !memcmp(buf + pos, u.in + e.off, e.len);
+    };
+    if (d->ra_next < d->R().ents.size()) {
+        if (!same(d->R(), d->R().ents[d->ra_next])) {
             const int r = ra_settle(d);
             if (r) return r;
         }
-    } else if (!d->ra.empty()) {
-        d->ra.clear(); /* all served */
-        d->ra_next = 0;
-        d->ra_backoff = 0;
+    } else if (!d->R().ents.empty()) {
+        /* the run being served is used up: on to the next run when this call
+         * asks for its first frame (it was decoding behind the served calls),
+         * and launch the one after it */
+        const int rj = ra_join(d); /* the helper's launch of it (its status) */
+        if (rj) return rj;
+        mp3d_dec::Run &n = d->N();
+        if (!n.ents.empty() && same(n, n.ents[0])) {
+            if (n.pending) HIPCHK(hipEventSynchronize(n.done));
+            n.pending = false;
+            d->R().ents.clear();
+            d->cur ^= 1;
+            d->ra_next = 0;
+            d->ra_backoff = 0;
+            const int r = ra_launch_next(d, buf, bytes, f32);
+            if (r) return r;
+        } else {
+            const int r = ra_settle(d); /* (served whole: a no-op unless a next run is dropped) */
+            if (r) return r;
+        }
     }
     if (loc <= 0) {
         info->frame_bytes = (int)pos;
         return loc;
     }
-    bool cached = d->ra_next < d->ra.size();
-    if (!cached && have == (size_t)fb) {
-        const int r = ra_fill(d, buf, bytes, f32);
-        if (r < 0) return r;
-        cached = r == 1;
+    bool cached = d->ra_next < d->R().ents.size();
+    if (!cached) { /* the batch handle is used below */
+        const int rj = ra_join(d);
+        if (rj) return rj;
+    }
+    if (!cached && have == (size_t)fb && d->ra_max) {
+        if (d->ra_cool > 0) { /* backing off after a wasted read-ahead */
+            d->ra_cool--;
+        } else {
+            int kind = d->kind;
+            const int r = ra_fill(d, d->R(), buf, bytes, f32, d->frames == 0, &kind);
+            if (r < 0) return r;
+            cached = r == 1;
+            if (cached) {
+                d->ra_next = 0;
+                const int r2 = ra_launch_next(d, buf, bytes, f32);
+                if (r2) return r2;
+            }
+        }
     }
     mp3d_frame_info fi;
     const void *out;
     if (cached) {
-        fi = d->ra_inf[d->ra_next];
-        out = (const uint8_t *)d->ra_pcm + d->ra_next * 2304 * (f32 ? sizeof(float) : sizeof(int16_t));
+        const mp3d_dec::Run &c = d->R();
+        fi = c.inf[d->ra_next];
+        out = (const uint8_t *)c.pcm + d->ra_next * 2304 * (f32 ? sizeof(float) : sizeof(int16_t));
         d->ra_next++;
     } else {
         uint64_t off = 0;
@@ -1462,9 +1705,9 @@ static int decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, void *pcm
              * info in place (three launches + one sync); else staged copies */
             const bool mapped = d->m_in != nullptr;
             r = mapped ? batch_decode(d->b, d->m_in, &off, &sz, 1, 1, d->m_out, f32, d->m_info, nullptr, true,
-                                      host_frame_kind(buf + pos), true)
+                                      host_frame_kind(buf + pos), true, 0, nullptr, false)
                        : batch_decode(d->b, d->h_in, &off, &sz, 1, 1, d->h_out, f32, d->h_info, nullptr, true,
-                                      host_frame_kind(buf + pos)); /* 1 MPEG-1, 2 LSF */
+                                      host_frame_kind(buf + pos), false, 0, nullptr, false); /* 1 MPEG-1, 2 LSF */
         }
         if (r) return r;
         fi = *d->h_info;
@@ -1546,8 +1789,8 @@ extern "C" int mp3d_dec_get_state(mp3d_dec *d, void *buf) {
 
 extern "C" int mp3d_dec_set_state(mp3d_dec *d, const void *buf) {
     if (!d || !buf) return MP3D_E_ARG;
-    d->ra.clear(); /* replaced whole: nothing read ahead applies */
-    d->ra_next = 0;
+    (void)ra_join(d);
+    ra_drop(d); /* replaced whole: nothing read ahead applies */
     const int r = mp3d_batch_set_state(d->b, 0, 1, buf);
     if (r) return r;
     /* host mirror of the family lock and "past the stream start" (ID3v2 skip) */

@@ -110,3 +110,42 @@ def test_readahead_backoff_state_every_frame():
     call = [("call", False)]
     script = (call + [("state",)]) * 90 + call * 70 + [("state",)] + [("reset",)] + (call + [("state",)]) * 20
     _same(_run(_dec(32), data, script), _run(_dec(0), data, script))
+
+
+def _dec_env(ra, **env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return _dec(ra)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("ra", [16, 32])
+def test_readahead_next_run_boundaries(ra):
+    """Two runs (the next one decoding behind the served calls, k_demux_fp
+    demuxing both): leaving at every kind of point of a 512-frame stream --
+    a state save right after a fill (next run pending), a jump at the run
+    boundary (the next run dropped), a sink change at a boundary, a state
+    save mid-run -- stays bit-identical to frame-by-frame decoding."""
+    data, _ = _golden.case("long_c3_512")
+    call = [("call", False)]
+    script = (call + [("state",)] + call * (ra - 1) + [("skip", 1)] + call * (2 * ra) + [("call", True)] +
+              call * 3 + [("state",)] + call * (ra + 5) + [("seek", 1)] + call * 150)
+    _same(_run(_dec(ra), data, script), _run(_dec(0), data, script))
+
+
+def test_readahead_next_run_off_same_output():
+    """MP3D_PF_RA_NEXT=0 (one run at a time), MP3D_PF_RA_THREAD=0 (the next
+    run launched on the calling thread) and the default (launched by the
+    helper thread) give the same bits over a long stream and an LSF stream."""
+    for name in ("long_c3_512", "lsf_scale_24k_is"):
+        data, _ = _golden.case(name)
+        script = [("call", False)] * 300
+        ref = _run(_dec(32), data, script)
+        _same(_run(_dec_env(32, MP3D_PF_RA_NEXT=0), data, script), ref)
+        _same(_run(_dec_env(32, MP3D_PF_RA_THREAD=0), data, script), ref)
