@@ -184,6 +184,12 @@ VARS = {
              "                        const uint32_t e = s_lut[((c1base + (hw >> c1sh)) & ~63u) + (uint32_t)lane];"),
             ("                        se = s_c1s[(v << 4) | ((hw << lq) >> 28)];",
              "                        se = s_c1s[(((v << 4) | ((hw << lq) >> 28)) & ~63u) + (uint32_t)lane];")],
+    # round 5, k_demux_fp ablations (output wrong; timing only): no parse / no serial resolve / no payload copy
+    "FPNP": [("        if (fb > 0) parse_frame<SrcGlobal>(w[j], p0, 0, cur, len, fb, stream_start && f == 0, opts, S, fp, r[j], inf[j], lane);",
+              "        (void)fb; (void)cur;")],
+    "FPNR": [("        for (int f = 0; f < F; f++) {\n            const FpRes q = s_res[f];",
+              "        for (int f = 0; f < 0; f++) {\n            const FpRes q = s_res[f];")],
+    "FPNC": [("            copy_payload<SrcGlobal>(p0, dst, r[j], fo[f] + body, fo[f], lane);", "            (void)body;")],
     # timing only (C3 holds no LSF stream): the LSF k_synth launch skipped on int16 batches (NL)
     "NL": [("        if (kinds & 2) MP3D_SYNTH_LAUNCH(false, true);", "")],
     # r03: k_mdcopy quadruples by one unaligned 16-B load each instead of 16 + 4 B and four funnel shifts (UA1)

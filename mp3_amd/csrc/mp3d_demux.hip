@@ -506,27 +506,56 @@ struct FpOut {      /* what it decides */
     uint32_t payload_md, md_bit, lens; /* lens: payload_len | payload_avail << 16 */
     uint32_t gr_samples;              /* first_gr | samples << 8 */
 };
+/* the run's frame offsets, by value (kernel arguments: scalar loads, no
+ * round trip to the host buffer) */
+struct FpOffs {
+    uint32_t o[FP_MAX];
+};
+#define FP_STAGE (FP_MAX * MP3D_MAX_FRAME_BYTES + 64) /* the run's bytes staged in LDS */
 __global__ void __launch_bounds__(64 * FP_WAVES)
-k_demux_fp(const uint8_t *__restrict__ in, uint32_t len, const uint32_t *__restrict__ fo, uint8_t *__restrict__ md,
+k_demux_fp(const uint8_t *__restrict__ in, uint32_t len, FpOffs fo, uint8_t *__restrict__ md,
            StreamState *__restrict__ st, const float *__restrict__ tail_in, StreamState *__restrict__ snap,
            FrameRec *__restrict__ rec, uint64_t *__restrict__ sideu, DevInfo *__restrict__ infos, int F, int opts) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) u32x4 s_run[(FP_STAGE + 15) / 16];
     __shared__ FpRes s_res[FP_MAX];
     __shared__ FpOut s_out[FP_MAX];
     __shared__ uint32_t s_h1[FP_MAX];
     __shared__ int s_fin[3];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    constexpr int NT = 64 * FP_WAVES;
     StreamState &S = st[0];
-    /* the previous run's final overlap + history (a segmented synthesis
-     * leaves them in the handle's tail) into the state, then the snapshot */
+    /* the run's bytes (the mapped host buffer, 16-B aligned) into LDS: every
+     * block's load in flight at once -- one bus round trip for the run; the
+     * parse and the payload copy then read LDS */
+    const uint32_t nblk = (len + 15u) / 16u;
+    constexpr int PER = ((FP_STAGE + 15) / 16 + NT - 1) / NT;
+    u32x4 v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const uint32_t i = (uint32_t)tid + (uint32_t)(NT * k);
+        v[k] = ((const u32x4 *)in)[i < nblk ? i : 0u]; /* unconditional: the loads stay in flight together */
+    }
+    /* meanwhile: the previous run's final overlap + history (a segmented
+     * synthesis leaves them in the handle's tail) into the state, and the
+     * state before this run (tail applied) into the snapshot, in one pass */
+    constexpr int TAIL0 = (int)(offsetof(StreamState, overlap) / 4);
     constexpr int TAILW = (int)(sizeof(S.overlap) + sizeof(S.fifo)) / 4;
-    if (tail_in)
-        for (int i = tid; i < TAILW; i += 64 * FP_WAVES) (&S.overlap[0][0][0])[i] = tail_in[i];
-    __syncthreads();
-    for (int i = tid; i < (int)(sizeof(StreamState) / 4); i += 64 * FP_WAVES)
-        ((uint32_t *)snap)[i] = ((const uint32_t *)&S)[i];
-    __syncthreads(); /* every read of the state before the run is done (the tag write below) */
-    const uint8_t *p0 = in;
+    for (int i = tid; i < (int)(sizeof(StreamState) / 4); i += NT) {
+        const bool t = tail_in && i >= TAIL0 && i < TAIL0 + TAILW;
+        const uint32_t x = t ? ((const uint32_t *)tail_in)[i - TAIL0] : ((const uint32_t *)&S)[i];
+        if (t) ((uint32_t *)&S)[i] = x;
+        ((uint32_t *)snap)[i] = x;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const uint32_t i = (uint32_t)tid + (uint32_t)(NT * k);
+        if (i < nblk) s_run[i] = v[k];
+    }
+    if (tid == 0) s_run[nblk] = (u32x4){0u, 0u, 0u, 0u}; /* (the tail: the host zeroed 64 B past the frames too) */
+    __syncthreads(); /* the staged bytes; every read of the state before the run (the tag write below) */
+    SrcLds::u8 *p0 = (SrcLds::u8 *)(uintptr_t)s_run;
     uint8_t *dst = md;
     const int carry_in = __builtin_amdgcn_readfirstlane(S.res_len);
     const bool stream_start = __builtin_amdgcn_readfirstlane((int)S.frames) == 0;
@@ -537,7 +566,7 @@ k_demux_fp(const uint8_t *__restrict__ in, uint32_t len, const uint32_t *__restr
 #pragma unroll
     for (int j = 0; j < FP_PER; j++) {
         const int f = wv + FP_WAVES * j;
-        if (f < F) w[j] = load_win<SrcGlobal>(p0, len, fo[f], lane);
+        if (f < F) w[j] = load_win<SrcLds>(p0, len, fo.o[f], lane);
     }
     FrameRec r[FP_PER];
     DevInfo inf[FP_PER];
@@ -550,7 +579,7 @@ k_demux_fp(const uint8_t *__restrict__ in, uint32_t len, const uint32_t *__restr
         need[j] = 0u;
         rec_init(r[j], 0u, inf[j]);
         if (f >= F) continue;
-        const uint32_t cur = fo[f];
+        const uint32_t cur = fo.o[f];
         /* (the family was checked on the host: every frame's header is of
          * the stream's family) */
         const int fb = hdr_frame_bytes(win_byte(w[j], 1), win_byte(w[j], 2), 0);
@@ -558,7 +587,7 @@ k_demux_fp(const uint8_t *__restrict__ in, uint32_t len, const uint32_t *__restr
         fp.fb = 0;
         fp.sw = 0;
         fp.h1 = 0u; /* stays 0: no header found (a valid one has h1 >= 0xE0) */
-        if (fb > 0) parse_frame<SrcGlobal>(w[j], p0, 0, cur, len, fb, stream_start && f == 0, opts, S, fp, r[j], inf[j], lane);
+        if (fb > 0) parse_frame<SrcLds>(w[j], p0, 0, cur, len, fb, stream_start && f == 0, opts, S, fp, r[j], inf[j], lane);
         has[j] = fp.fb != 0;
         need[j] = fp.need;
         if (lane < 4) sideu[(size_t)f * 4 + lane] = fp.fb ? fp.sw : 0ull;
@@ -572,39 +601,93 @@ k_demux_fp(const uint8_t *__restrict__ in, uint32_t len, const uint32_t *__restr
         }
     }
     __syncthreads();
-    /* the bit-reservoir map, in stream order (one wave, uniform) */
+    /* The bit-reservoir map (resolve_frame's rules) for all frames at once,
+     * lane f = frame f (F <= 64): each payload's md position is a prefix sum
+     * of the payload lengths; the bytes available after a frame depend on
+     * the frames before it only through the underflow test mdb > avail, so
+     * every frame's "avail after" is first taken as if no frame underflowed,
+     * the avail before each frame found by a last-setter scan, and the
+     * frames that do underflow recomputed until nothing changes (one pass
+     * unless a stream starts mid-way or a frame is dropped).  Done serially
+     * by one wave this step took 17 of the kernel's 30 us (32 frames). */
     if (wv == 0) {
-        uint32_t P = (uint32_t)carry_in;
-        int avail = carry_in, decoded = 0;
-        for (int f = 0; f < F; f++) {
-            const FpRes q = s_res[f];
-            FrameParse fp;
-            fp.fb = q.fb; fp.plen = q.plen; fp.mdb = q.mdb; fp.need = q.need;
-            fp.p00 = q.p00; fp.p01 = q.p01; fp.p10 = q.p10; fp.p11 = q.p11;
-            fp.lsf = q.flags & 1u; fp.bad = (q.flags >> 1) & 1u; fp.tag = (q.flags >> 2) & 1u;
-            fp.nch = (q.flags & 8u) ? 2 : 1;
-            fp.ngr = fp.lsf ? 1 : 2;
-            fp.have = (uint32_t)q.fb; /* complete frames */
-            FrameRec rr;
-            DevInfo ii;
-            rec_init(rr, P, ii);
-            rr.payload_len = (uint16_t)(q.plen > 0 ? q.plen : 0);
-            if (q.fb) {
-                decoded += resolve_frame(fp, P, avail, rr, ii);
-                (void)frame_body(fp, rr);
-            }
-            if (lane == 0) {
-                FpOut o;
-                o.payload_md = rr.payload_md;
-                o.md_bit = rr.md_bit;
-                o.lens = (uint32_t)rr.payload_len | (uint32_t)rr.payload_avail << 16;
-                o.gr_samples = (uint32_t)rr.first_gr | (uint32_t)ii.samples << 8;
-                s_out[f] = o;
-            }
+        const bool live = lane < F;
+        FpRes q = {0, 0, 0, 0u, 0, 0, 0, 0, 0u};
+        if (live) q = s_res[lane];
+        const bool found = live && q.fb != 0;
+        const bool tag = found && (q.flags & 4u);
+        const bool bad = found && !tag && (q.flags & 2u);
+        const bool aud = found && !tag && !bad;
+        const int delta = bad ? q.fb - 4 : aud ? q.plen : 0;
+        int incl = delta;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(incl, o);
+            if (lane >= o) incl += t;
         }
+        const uint32_t Pb = (uint32_t)carry_in + (uint32_t)(incl - delta), Pa = Pb + (uint32_t)delta;
+        const uint32_t g0 = (uint32_t)(q.p00 + q.p01), g1 = (uint32_t)(q.p10 + q.p11); /* per granule (0 if absent) */
+        const int ngr = (q.flags & 1u) ? 1 : 2;
+        const bool sets = bad || aud; /* tags and empty slots pass avail through */
+        /* avail after this frame from avail before it (resolve_frame) */
+        auto after = [&](int av_prev, int &gr0, uint32_t &mdbit) {
+            if (bad) return q.fb - 4 < MP3D_RES_BYTES ? q.fb - 4 : MP3D_RES_BYTES;
+            gr0 = 0;
+            if (q.mdb <= av_prev) {
+                mdbit = (Pb - (uint32_t)q.mdb) * 8u;
+            } else {
+                uint32_t bits = (uint32_t)av_prev * 8u;
+                while (gr0 < ngr && (int)(bits >> 3) < q.mdb) {
+                    bits += gr0 ? g1 : g0;
+                    gr0++;
+                }
+                mdbit = (Pb - (uint32_t)av_prev) * 8u + bits - 8u * (uint32_t)q.mdb;
+            }
+            const uint32_t end = mdbit + (gr0 == 0 ? g0 : 0u) + (gr0 <= 1 ? g1 : 0u);
+            const int64_t a = (int64_t)Pa - (int64_t)((end + 7u) >> 3);
+            return a < 0 ? 0 : (int)a;
+        };
+        int gr0 = 0;
+        uint32_t mdbit = 0u;
+        int av = sets ? after(1 << 30, gr0, mdbit) : 0; /* as if nothing underflowed */
+        int av_prev = carry_in, last = carry_in;
+        for (int it = 0; it <= 64; it++) {
+            /* last setter at or before each lane (inclusive), then shifted */
+            int val = av, set = sets ? 1 : 0;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int tv = __shfl_up(val, o), ts = __shfl_up(set, o);
+                if (lane >= o && !set) {
+                    val = tv;
+                    set = ts;
+                }
+            }
+            const int pv = __shfl_up(val, 1), ps = __shfl_up(set, 1);
+            av_prev = (lane == 0 || !ps) ? carry_in : pv;
+            last = __shfl(set ? val : carry_in, F > 0 ? F - 1 : 0);
+            const int av2 = sets ? after(av_prev, gr0, mdbit) : 0;
+            const bool changed = __ballot(av2 != av) != 0ull;
+            av = av2;
+            if (!changed) break;
+        }
+        if (live) {
+            FpOut o;
+            o.payload_md = Pb;
+            o.md_bit = aud ? mdbit : 0u;
+            const uint32_t plen = bad ? (uint32_t)(q.fb - 4) : (uint32_t)(q.plen > 0 ? q.plen : 0);
+            const uint32_t body = bad ? 4u : q.need;
+            const uint32_t avb = (uint32_t)q.fb > body ? (uint32_t)q.fb - body : 0u; /* complete frames */
+            o.lens = plen | (found ? (avb < plen ? avb : plen) : 0u) << 16;
+            o.gr_samples = tag ? (uint32_t)REC_TAG
+                               : bad ? (uint32_t)REC_DROP
+                                     : aud ? (uint32_t)gr0 | (uint32_t)((q.flags & 1u) ? 576 : 1152) << 8 : 0u;
+            s_out[lane] = o;
+        }
+        const uint32_t P_end = F > 0 ? (uint32_t)__shfl((int)Pa, F - 1) : (uint32_t)carry_in;
+        const int decoded = __popcll(__ballot(aud));
         if (lane == 0) {
-            s_fin[0] = (int)P;
-            s_fin[1] = avail;
+            s_fin[0] = (int)P_end;
+            s_fin[1] = F > 0 ? last : carry_in;
             s_fin[2] = decoded;
         }
     }
@@ -630,7 +713,7 @@ k_demux_fp(const uint8_t *__restrict__ in, uint32_t len, const uint32_t *__restr
         }
         if (has[j] && !(r[j].first_gr & REC_TAG)) {
             const uint32_t body = (r[j].first_gr & REC_DROP) ? 4u : need[j];
-            copy_payload<SrcGlobal>(p0, dst, r[j], fo[f] + body, fo[f], lane);
+            copy_payload<SrcLds>(p0, dst, r[j], fo.o[f] + body, fo.o[f], lane);
         }
     }
     __syncthreads(); /* every wave's md stores before the carry is read back */
@@ -652,12 +735,15 @@ k_demux_fp(const uint8_t *__restrict__ in, uint32_t len, const uint32_t *__restr
     }
 }
 
-/* one pre-located run (k_demux_fp): in = its bytes (len), fo = its frame
- * offsets, md = the handle's md region (stream 0 at offset 0) */
+/* one pre-located run (k_demux_fp): in = its bytes (len), fo = its F frame
+ * offsets (host array, passed by value), md = the handle's md region (stream
+ * 0 at offset 0) */
 void launch_demux_fp(const uint8_t *in, uint32_t len, const uint32_t *fo, uint8_t *md, StreamState *st,
                      const float *tail_in, StreamState *snap, FrameRec *rec, uint64_t *sideu, void *infos, int F,
                      int opts, hipStream_t strm) {
-    hipLaunchKernelGGL(k_demux_fp, dim3(1), dim3(64 * FP_WAVES), 0, strm, in, len, fo, md, st, tail_in, snap, rec,
+    FpOffs o = {};
+    for (int f = 0; f < F && f < FP_MAX; f++) o.o[f] = fo[f];
+    hipLaunchKernelGGL(k_demux_fp, dim3(1), dim3(64 * FP_WAVES), 0, strm, in, len, o, md, st, tail_in, snap, rec,
                        sideu, (DevInfo *)infos, F, opts);
 }
 

@@ -772,7 +772,7 @@ static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offse
 struct FpRun {
     const uint8_t *in;   /* device address of the run's bytes (mapped)    */
     uint32_t len;
-    const uint32_t *fo;  /* device address of the frame offsets (mapped) */
+    const uint32_t *fo;  /* the frame offsets (host; passed as kernel arguments) */
     const float *tail_in; /* the handle's live synthesis tail, or null     */
     StreamState *snap;   /* receives the state before the run             */
 };
@@ -1475,7 +1475,7 @@ static int ra_settle(mp3d_dec *d) {
             const uint64_t off = 0;
             const uint32_t len = c.ents[served - 1].off + c.ents[served - 1].len;
             (void)off;
-            const FpRun fp = {c.in_m, len, (const uint32_t *)(c.in_m + c.fo_at), nullptr, c.snap};
+            const FpRun fp = {c.in_m, len, (const uint32_t *)(c.in + c.fo_at), nullptr, c.snap};
             r = batch_decode(b, c.in_m, &off, &len, 1, (int)served, c.pcm_m, c.f32, c.inf_m, nullptr, true, 3, true,
                              d->ra_seg, &fp, false);
             if (r) return r;
@@ -1539,7 +1539,7 @@ static int ra_launch(mp3d_dec *d, mp3d_dec::Run &u, uint32_t o, int kinds, bool 
     const float *tail = b->tail_live >= 0 ? b->st_tail[b->tail_live] : nullptr;
     b->tail_live = -1;
     const uint64_t off = 0;
-    const FpRun fp = {u.in_m, o, (const uint32_t *)(u.in_m + u.fo_at), tail, u.snap};
+    const FpRun fp = {u.in_m, o, (const uint32_t *)(u.in + u.fo_at), tail, u.snap};
     r = batch_decode(b, u.in_m, &off, &o, 1, (int)u.ents.size(), u.pcm_m, f32, u.inf_m, nullptr, true, kinds, true,
                      d->ra_seg, &fp, async);
     if (r) return r;
