@@ -567,6 +567,9 @@ extern "C" int mp3d_batch_create(int device, int max_streams, int max_frames, mp
         return MP3D_E_HIP;
     }
     for (int i = 0; i < 4; i++) (void)hipEventCreate(&b->ev[i]);
+    if (getenv("MP3D_DEBUG_ADDR")) /* placement diagnostics (tools/dbg/place.py) */
+        fprintf(stderr, "mp3d: st %p rec %p sideu %p is_buf %p meta %p infos %p\n", (void *)b->st, (void *)b->rec,
+                (void *)b->sideu, (void *)b->is_buf, (void *)b->meta, (void *)b->d_infos);
     /* zeroed on the handle's own stream and waited for: a null-stream
      * hipMemset is asynchronous for device memory and does not order before
      * kernels on non-blocking streams (a first call could read the previous
