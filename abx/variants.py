@@ -488,6 +488,24 @@ VARS["PST2"] = VARS["PST"] + [
 VARS["NOSLPALL"] = [("FLAGS", "-fno-slp-vectorize")]
 VARS["UNR"] = [("FLAGS", "-mllvm"), ("FLAGS", "-unroll-threshold=400")]
 
+# k_huffman store cost (round 5): big_values group stores kept only when the
+# group's four words xor to a value no group has (the decode itself stays live)
+VARS["NST"] = [("                        *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);",
+                "                        if ((wv[0] ^ wv[1] ^ wv[2] ^ wv[3]) == 0x7FFF8001u) *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);")]
+# ... and the count1 stores too
+VARS["NSTC"] = VARS["NST"] + [
+    ("                        __builtin_memcpy(row + k, &q, 16);",
+     "                        if ((q.x ^ q.w) == 0x7FFF8001u) __builtin_memcpy(row + k, &q, 16);")]
+# k_huffman: main-data staging loads non-temporal (leave L2 to the is[] rows being filled)
+VARS["NTL"] = [("                            if (i + 4 * k < len) v[k] = *(const uint4 *)(src + i + 4 * k);",
+                "                            if (i + 4 * k < len) { typedef uint32_t u4v __attribute__((ext_vector_type(4))); const u4v t = __builtin_nontemporal_load((const u4v *)(src + i + 4 * k)); v[k] = make_uint4(t.x, t.y, t.z, t.w); }")]
+# k_huffman: big_values group stores non-temporal
+VARS["NTS"] = [("                        *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);",
+                "                        { typedef uint32_t u4v __attribute__((ext_vector_type(4))); __builtin_nontemporal_store((u4v){wv[0], wv[1], wv[2], wv[3]}, (u4v *)(row + k)); }")]
+# k_huffman waves per CU (open is[] rows per CU = 64 x waves)
+VARS["HW12"] = [("#define HUFF_WAVES 16", "#define HUFF_WAVES 12")]
+VARS["HW8"] = [("#define HUFF_WAVES 16", "#define HUFF_WAVES 8")]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
