@@ -505,6 +505,9 @@ VARS["NTS"] = [("                        *(uint4 *)(row + k) = make_uint4(wv[0],
 # k_huffman waves per CU (open is[] rows per CU = 64 x waves)
 VARS["HW12"] = [("#define HUFF_WAVES 16", "#define HUFF_WAVES 12")]
 VARS["HW8"] = [("#define HUFF_WAVES 16", "#define HUFF_WAVES 8")]
+# k_rank segment size (units ranked together): 1 024 / 2 048 instead of 4 096
+VARS["RK1"] = [("#define RANK_PER 4      /* units per thread */", "#define RANK_PER 1")]
+VARS["RK2"] = [("#define RANK_PER 4      /* units per thread */", "#define RANK_PER 2")]
 
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):

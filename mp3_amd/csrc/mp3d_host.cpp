@@ -33,7 +33,7 @@ void launch_demux(const uint8_t *, const uint64_t *, const uint32_t *, uint8_t *
 void launch_demux_fp(const uint8_t *, uint32_t, const uint32_t *, uint8_t *, StreamState *, const float *,
                      StreamState *, FrameRec *, uint64_t *, void *, int, int, hipStream_t);
 void launch_huffman(const uint8_t *, const uint64_t *, const FrameRec *, const uint64_t *, const DevTables *, int16_t *,
-                    UnitMeta *, int, int, int, bool, uint32_t *, hipStream_t);
+                    UnitMeta *, int, int, int, bool, uint32_t *, uint32_t *, hipStream_t);
 void launch_synth(const FrameRec *, const int16_t *, const UnitMeta *, const DevTables *, StreamState *, void *, bool, int,
                   int, int, int, float *, const float *, const uint32_t *, uint32_t, int, hipStream_t);
 void launch_synth_xr(const float *, const uint8_t *, const uint8_t *, const DevTables *, StreamState *, int16_t *, int,
@@ -323,6 +323,7 @@ struct mp3d_batch {
     FrameRec *rec = nullptr;
     uint64_t *sideu = nullptr; /* per-unit side info (k_demux -> k_huffman) */
     int16_t *is_buf = nullptr;
+    uint32_t *rank = nullptr; /* k_rank: the units in big_values order per segment */
     UnitMeta *meta = nullptr;
     /* Stream geometry of a call (input offsets, sizes, md-region offsets) in
      * two device slots, each filled from its own pinned host buffer by an
@@ -551,6 +552,7 @@ extern "C" int mp3d_batch_create(int device, int max_streams, int max_frames, mp
     BALLOC(b->sideu, sizeof(uint64_t) * units);
     BALLOC(b->is_buf, sizeof(int16_t) * 576 * units);
     BALLOC(b->meta, sizeof(UnitMeta) * units);
+    BALLOC(b->rank, sizeof(uint32_t) * units); /* k_huffman's big_values order (k_rank) */
     for (auto &g : b->geo) BALLOC(g.d, 20 * (size_t)max_streams);
     BALLOC(b->d_infos, sizeof(mp3d_frame_info) * (size_t)max_streams * max_frames);
     BALLOC(b->d_work, 256);
@@ -589,7 +591,7 @@ extern "C" void mp3d_batch_destroy(mp3d_batch *b) {
     if (b->ev_done) (void)hipEventSynchronize(b->ev_done);
     if (b->own) (void)hipStreamSynchronize(b->own);
     if (b->copy) (void)hipStreamSynchronize(b->copy);
-    void *ptrs[] = {b->st, b->rec, b->sideu, b->is_buf, b->meta, b->geo[0].d, b->geo[1].d, b->d_work,
+    void *ptrs[] = {b->st, b->rec, b->sideu, b->is_buf, b->meta, b->rank, b->geo[0].d, b->geo[1].d, b->d_work,
                     b->d_infos, b->md, b->d_in, b->d_pcm, b->d_xr, b->d_bt, b->d_mx, b->st_tail[0], b->st_tail[1]};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
@@ -758,7 +760,7 @@ static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offse
                  dev_infos ? (void *)dev_infos : b->d_infos, n, F, b->opts, wide, b->d_work + 1, b->call_seq, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[1], s));
     launch_huffman(b->md, g.md_off(), b->rec, b->sideu, dc.tables, b->is_buf, b->meta, n, F, dc.n_cu,
-                   huffman_wave(n * F * 4), b->d_work, s);
+                   huffman_wave(n * F * 4), b->d_work, b->rank, s);
     HIPCHK(hipEventRecord(g.freed, s)); /* the slot's last reader */
     b->geo[b->geo_i].fresh = true;
     if (b->timing) HIPCHK(hipEventRecord(b->ev[2], s));
@@ -793,7 +795,7 @@ static int run_front_fp(mp3d_batch *b, const FpRun &fp, int F, hipStream_t s, mp
     if (b->timing) HIPCHK(hipEventRecord(b->ev[1], s));
     /* md offset of the one stream: a zero word of d_work (d_work[4..5]) */
     launch_huffman(b->md, (const uint64_t *)(b->d_work + 4), b->rec, b->sideu, dc.tables, b->is_buf, b->meta, 1, F,
-                   dc.n_cu, true, b->d_work, s);
+                   dc.n_cu, true, b->d_work, nullptr, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[2], s));
     HIPCHK(hipGetLastError());
     return MP3D_OK;

@@ -10,16 +10,68 @@
 
 namespace mp3d {
 
+/* ---- ranking (k_rank): the units of each RANK_SEG-unit segment in
+ * descending big_values order, by a counting sort in LDS, so each 64-unit
+ * round of k_huffman holds units of (nearly) one length: the branch-free
+ * big_values loop runs max-over-lanes iterations.  On C3 (generator side
+ * info) rounds ranked over 256 units run 1.50x the lane-steps of an exact
+ * order, over 4 096 units 1.03x.  A whole-launch order (1.00x) scattered
+ * each round's rows over the whole is[] buffer and ran slower.  The order
+ * inside a bin is the order of the LDS atomics (not deterministic): it
+ * changes which lane decodes a unit, not what is decoded. */
+#define RANK_BINS 320   /* big_values 0 .. 319 (the field's legal range is 0 .. 288) */
+#define RANK_BLOCK 1024
+#define RANK_PER 4      /* units per thread */
+#define RANK_SEG (RANK_BLOCK * RANK_PER)
+__global__ void __launch_bounds__(RANK_BLOCK) k_rank(const uint64_t *__restrict__ sideu, int n_units,
+                                                     uint32_t *__restrict__ perm) {
+    __shared__ uint32_t h[RANK_BINS];
+    const int tid = threadIdx.x, seg0 = blockIdx.x * RANK_SEG;
+    for (int i = tid; i < RANK_BINS; i += RANK_BLOCK) h[i] = 0u;
+    __syncthreads();
+    uint32_t bin[RANK_PER], r[RANK_PER];
+#pragma unroll
+    for (int j = 0; j < RANK_PER; j++) {
+        const int u = seg0 + j * RANK_BLOCK + tid;
+        const uint32_t bv = u < n_units ? (uint32_t)(sideu[u] >> 43) & 0x1FFu : 0u;
+        bin[j] = RANK_BINS - 1u - (bv < RANK_BINS ? bv : RANK_BINS - 1u); /* descending big_values */
+        r[j] = u < n_units ? atomicAdd(&h[bin[j]], 1u) : 0u;
+    }
+    __syncthreads();
+    if (tid < 64) {
+        /* exclusive scan of the counts: lane owns bins 5 lane .. +4 */
+        uint32_t c[5], sum = 0u;
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            c[k] = h[5 * tid + k];
+            sum += c[k];
+        }
+        const uint32_t incl = wave_incl_scan(sum);
+        uint32_t run = incl - sum;
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            h[5 * tid + k] = run;
+            run += c[k];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RANK_PER; j++) {
+        const int u = seg0 + j * RANK_BLOCK + tid;
+        if (u < n_units) perm[seg0 + h[bin[j]] + r[j]] = (uint32_t)u;
+    }
+}
+
 /* k_huffman: one lane per unit (its layout constants and helpers: mp3d_huffman_dev.h) */
-/* work: the handle's work-item counter; this launch's tickets start at
- * ticket0 (every wave takes tickets until one is past the last unit);
- * n_big: how many tickets are whole super-chunks (the rest single rounds) */
+/* work: the handle's work-item counter (zeroed before the launch); perm: each
+ * segment's units in descending big_values order (k_rank).  Work item t =
+ * units perm[64 t .. 64 t + 63]. */
 __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restrict__ md, const uint64_t *__restrict__ md_off,
                                                         const FrameRec *__restrict__ rec,
                                                         const uint64_t *__restrict__ sideu,
                                                         const DevTables *__restrict__ tab, int16_t *__restrict__ is_buf,
                                                         UnitMeta *__restrict__ meta, int n_units, int F,
-                                                        uint32_t *__restrict__ work, uint32_t ticket0, int n_big) {
+                                                        uint32_t *__restrict__ work, const uint32_t *__restrict__ perm) {
     __shared__ __attribute__((aligned(16))) uint16_t s_lut[MP3D_LUT_MAX];
     /* per-wave staging areas after a 4-word guard: win64g / win32g read the
      * word below a window that starts on a word boundary */
@@ -52,61 +104,13 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
     const int qb1 = tab->lut_hdr.bits1[MP3D_LUT_TABLES - 1];
     /* count1 table B: after the zero table (huff_tables_lane) */
     const uint32_t c1b_base = ((qbase + (1u << qb1) + 1u) & ~1u) + MP3D_C1B_OFF;
-    /* work items: tickets below n_big are super-chunks of HUFF_SUPER units
-     * (HUFF_ROUNDS rounds), the rest single rounds of 64 units covering the
-     * last units: the waves' finishing times then differ by a round, not by
-     * a super-chunk (the tail of a persistent launch) */
-    const int big_units = n_big * HUFF_SUPER;
     for (;;) {
         uint32_t t = 0u;
-        if (lane == 0) t = atomicAdd(work, 1u) - ticket0;
-        const int sc = (int)__builtin_amdgcn_readfirstlane(t);
-        const bool big = sc < n_big;
-        const int ubase = big ? sc * HUFF_SUPER : big_units + (sc - n_big) * 64;
-        const int nr = big ? HUFF_ROUNDS : 1;
+        if (lane == 0) t = atomicAdd(work, 1u);
+        const int ubase = 64 * (int)__builtin_amdgcn_readfirstlane(t);
         if (ubase >= n_units) break;
-        /* ---- order the work item's units by big_values (counting sort in
-         * LDS: histogram by ds_add_rtn, wave scan), so each 64-unit round
-         * holds units of similar length -- the big_values loop runs
-         * max-over-lanes iterations.  The order (u16) lives past the
-         * staging area, the histogram in it. */
-        uint16_t *order16 = (uint16_t *)(bits + HUFF_STAGEW + 4);
-        wave_sync();
-        for (int i = lane; i < 320; i += 64) bits[i] = 0u;
-        wave_sync();
-        uint32_t bvk[HUFF_ROUNDS], slot[HUFF_ROUNDS];
-#pragma unroll
-        for (int j = 0; j < HUFF_ROUNDS; j++) {
-            const int u = ubase + 64 * j + lane;
-            bvk[j] = u < n_units ? (uint32_t)(sideu[u] >> 43) & 0x1FFu : 0u;
-            bvk[j] = bvk[j] < 320u ? bvk[j] : 319u;
-            slot[j] = 0u;
-            if (j < nr) slot[j] = atomicAdd(&bits[bvk[j]], 1u);
-        }
-        wave_sync();
-        {   /* exclusive prefix over the 320 bins: lane owns bins 5 lane .. +4 */
-            uint32_t c[5], sum = 0;
-#pragma unroll
-            for (int k = 0; k < 5; k++) {
-                c[k] = bits[5 * lane + k];
-                sum += c[k];
-            }
-            const uint32_t incl = wave_incl_scan(sum);
-            uint32_t run = incl - sum;
-#pragma unroll
-            for (int k = 0; k < 5; k++) {
-                bits[5 * lane + k] = run;
-                run += c[k];
-            }
-        }
-        wave_sync();
-#pragma unroll
-        for (int j = 0; j < HUFF_ROUNDS; j++)
-            if (j < nr) order16[bits[bvk[j]] + slot[j]] = (uint16_t)(64 * j + lane);
-        wave_sync();
-
-        for (int rd = 0; rd < nr; rd++) {
-            const int u = ubase + (int)order16[64 * rd + lane];
+        {
+            const int u = ubase + lane < n_units ? (int)perm[ubase + lane] : n_units;
             const int fr = u >> 2, gr = (u >> 1) & 1, ch = u & 1;
             bool valid = u < n_units;
             /* the stream's md base, loaded together with the frame record (not
@@ -400,31 +404,29 @@ __global__ void __launch_bounds__(64 * HW_UNITS) k_huffman_wave(const uint8_t *_
 /* ------------------------------------------------------------------------ */
 /* wave: one wave per unit (k_huffman_wave; small batches), else one lane
  * per unit (k_huffman) */
-/* work: k_huffman's super-chunk counter (4 B of device memory per handle) */
+/* work: k_huffman's work-item counter (4 B of device memory per handle);
+ * rank: one word per unit (k_rank) */
 void launch_huffman(const uint8_t *md, const uint64_t *md_off, const FrameRec *rec, const uint64_t *sideu,
                     const DevTables *tab, int16_t *is_buf, UnitMeta *meta, int n_streams, int F, int n_cu, bool wave,
-                    uint32_t *work, hipStream_t strm) {
+                    uint32_t *work, uint32_t *rank, hipStream_t strm) {
     int n_units = n_streams * F * 4;
-    int supers = (n_units + HUFF_SUPER - 1) / HUFF_SUPER;
-    /* one workgroup per CU (its LDS is the whole CU's), fewer when there
-     * are fewer super-chunks than waves; the waves take super-chunks from the
-     * counter as they finish, so uneven super-chunks balance themselves */
-    int blocks = (supers + HUFF_WAVES - 1) / HUFF_WAVES;
-    const int cus = n_cu > 0 ? n_cu : 256; /* (device_init's attribute query failed) */
-    blocks = blocks < cus ? (blocks > 0 ? blocks : 1) : cus;
-    /* the last ~2 rounds per wave as single-round work items (k_huffman) */
-    const int small_units = std::min(n_units, 2 * blocks * HUFF_WAVES * 64);
-    const int n_big = (n_units - small_units) / HUFF_SUPER;
     if (wave) {
         hipLaunchKernelGGL(k_huffman_wave, dim3((n_units + HW_UNITS - 1) / HW_UNITS), dim3(64 * HW_UNITS), 0, strm, md,
                            md_off, rec, sideu, tab, is_buf, meta, n_units, F);
         return;
     }
+    /* one workgroup per CU (its LDS is the whole CU's), fewer when there
+     * are fewer rounds than waves; the waves take rounds from the counter */
+    const int rounds = (n_units + 63) / 64;
+    int blocks = (rounds + HUFF_WAVES - 1) / HUFF_WAVES;
+    const int cus = n_cu > 0 ? n_cu : 256; /* (device_init's attribute query failed) */
+    blocks = blocks < cus ? (blocks > 0 ? blocks : 1) : cus;
     /* the counter restarts at 0 with every launch (a memset node of a few
      * us): a launch that failed can never leave the next one's tickets off */
     (void)hipMemsetAsync(work, 0, sizeof(uint32_t), strm);
+    hipLaunchKernelGGL(k_rank, dim3((n_units + RANK_SEG - 1) / RANK_SEG), dim3(RANK_BLOCK), 0, strm, sideu, n_units, rank);
     hipLaunchKernelGGL(k_huffman, dim3(blocks), dim3(HUFF_BLOCK), 0, strm, md, md_off, rec, sideu, tab, is_buf, meta,
-                       n_units, F, work, 0u, n_big);
+                       n_units, F, work, (const uint32_t *)rank);
 }
 
 } // namespace mp3d

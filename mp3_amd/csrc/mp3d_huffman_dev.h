@@ -24,16 +24,15 @@ namespace mp3d {
 /* Side info arrives pre-extracted by k_demux (one u64 per unit).           */
 /* ------------------------------------------------------------------------ */
 /* One 16-wave workgroup per CU (4 waves per SIMD at <= 128 VGPRs), sharing
- * one copy of the LUT; the waves take super-chunks from a work counter
- * (persistent).  4-wave workgroups held 3 LUT copies per CU and fit only 3
- * waves per SIMD beside the staging areas. */
+ * one copy of the LUT; the waves take 64-unit rounds of the launch's
+ * big_values order from a work counter (persistent).  4-wave workgroups held
+ * 3 LUT copies per CU and fit only 3 waves per SIMD beside the staging
+ * areas. */
 #define HUFF_WAVES 16
 #define MP3D_C1B_OFF 2 /* count1 table B after the zero table (huff_tables_lane) */
-#define HUFF_ROUNDS 4                    /* 64-unit rounds per super-chunk          */
-#define HUFF_SUPER (64 * HUFF_ROUNDS)    /* units ranked together by big_values     */
 #define HUFF_BLOCK (64 * HUFF_WAVES)
-#define HUFF_CAPW 2304 /* LDS words per wave (9.2 KB): staging + round order; 16 waves + the tables in 160 KB */
-#define HUFF_STAGEW (HUFF_CAPW - HUFF_SUPER / 2) /* staging words; the u16 order follows */
+#define HUFF_CAPW 2304 /* LDS words per wave (9.2 KB) of main-data staging; 16 waves + the tables in 160 KB */
+#define HUFF_STAGEW HUFF_CAPW /* staging words */
 
 /* wave-wide scan / min by ds_bpermute with the lane id re-derived at each
  * use (HIP's __shfl_up / __shfl_xor add width bounds whose lane-derived
