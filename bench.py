@@ -440,7 +440,7 @@ def run_per_frame(args):
             "latency_us": {"median": float(np.median(lat_us)), "p90": float(np.percentile(lat_us, 90)),
                            "p99": float(np.percentile(lat_us, 99)), "mean": float(lat_us.mean())},
             "steady_latency_us": steady,
-            "readahead_frames": int(os.environ.get("MP3D_PF_READAHEAD", 32)),
+            "readahead_frames": int(os.environ.get("MP3D_PF_READAHEAD", 64)),
             "note": "one call per frame as a player's loop makes them, the rest of the file passed each time: the "
                     "decoder reads up to readahead_frames frames ahead in one batch call and serves the next calls "
                     "from it, while the run after it decodes behind them (MP3D_PF_READAHEAD=0: every call decodes "

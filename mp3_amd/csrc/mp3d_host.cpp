@@ -1168,7 +1168,7 @@ done:
  * zero-padded to a fixed MP3D_PF_BYTES, which keeps the batch geometry
  * constant (uploaded once) across calls. */
 #define MP3D_PF_BYTES 4096
-#define MP3D_PF_READAHEAD 32 /* frames per read-ahead by default */
+#define MP3D_PF_READAHEAD 64 /* frames per read-ahead by default (k_demux_fp: <= 64) */
 #define MP3D_PF_RA_SEG 1     /* synthesis segment (frames) of a read-ahead */
 struct mp3d_dec {
     mp3d_batch *b = nullptr;

@@ -1187,6 +1187,15 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                 }
                 __syncthreads();
             }
+            /* a warm-up frame's granule 0 (frame-parallel segments): only
+             * its IMDCT overlap is used (granule 1's S reads it), so it skips
+             * S, phases M and W -- its synthesis history is replaced by granule
+             * 1's, whose window output is not stored either */
+            if (!SRC_XR && !LSF && PF == 0 && f < f0 && gr == 0) {
+                WAIT_VMCNT0(); /* (phase W's drain: the next granule's prefetch has landed) */
+                wave_sync();
+                continue;
+            }
             wave_sync(); /* every lane has read its xr before S overwrites it */
             {
                 /* S row layout: subbands 0..15, then 31 down to 16, so the

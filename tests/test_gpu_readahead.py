@@ -125,7 +125,7 @@ def _dec_env(ra, **env):
                 os.environ[k] = v
 
 
-@pytest.mark.parametrize("ra", [16, 32])
+@pytest.mark.parametrize("ra", [16, 32, 64])
 def test_readahead_next_run_boundaries(ra):
     """Two runs (the next one decoding behind the served calls, k_demux_fp
     demuxing both): leaving at every kind of point of a 512-frame stream --
