@@ -508,6 +508,69 @@ VARS["HW8"] = [("#define HUFF_WAVES 16", "#define HUFF_WAVES 8")]
 # k_rank segment size (units ranked together): 1 024 / 2 048 instead of 4 096
 VARS["RK1"] = [("#define RANK_PER 4      /* units per thread */", "#define RANK_PER 1")]
 VARS["RK2"] = [("#define RANK_PER 4      /* units per thread */", "#define RANK_PER 2")]
+# k_mdcopy occupancy: 16-wave workgroups; a persistent grid of 2 048 workgroups looping over streams
+VARS["MDC16"] = [("#define MDC_WAVES 4", "#define MDC_WAVES 16")]
+VARS["MDCP"] = [
+    ("""    const int s = blockIdx.x * MDC_WAVES + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (s >= n_streams) return; /* wave-level sync only below */""",
+     """    for (int s = blockIdx.x * MDC_WAVES + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); s < n_streams;
+         s += gridDim.x * MDC_WAVES) {"""),
+    ("""    if (lane == 0) S.res_len = c;
+}""", """    if (lane == 0) S.res_len = c;
+    }
+}"""),
+    ("hipLaunchKernelGGL(k_mdcopy, dim3((n_streams + MDC_WAVES - 1) / MDC_WAVES)",
+     "hipLaunchKernelGGL(k_mdcopy, dim3(std::min((n_streams + MDC_WAVES - 1) / MDC_WAVES, 2048))")]
+# k_demux_fp phase costs (round 5; output wrong by construction): return after staging, after the
+# state loads + carry-in copy, with the parse reduced to the frame-size lookup, after the parse, after
+# the resolve
+_FPS = """    SrcLds::u8 *p0 = (SrcLds::u8 *)(uintptr_t)s_run;
+    uint8_t *dst = md;"""
+_FPP = """    /* the wave's frames, one at a time in a loop that is not unrolled: the"""
+_FPR = """    __syncthreads();
+    /* The bit-reservoir map (resolve_frame's rules) for all frames at once,"""
+_FPE = """    __syncthreads();
+    /* records and payloads, the wave's own frames */"""
+VARS["FPX1"] = [(_FPS, "    if (F > 0) return;\n" + _FPS)]
+VARS["FPX1B"] = [(_FPP, "    if (F > 0) return;\n" + _FPP)]
+VARS["FPX2A"] = [("        if (fb > 0) parse_frame<SrcLds>(w, p0, 0, cur, len, fb, stream_start && f == 0, opts, S, fp, r, inf, lane, ht);",
+                  "        if (fb == 12345) parse_frame<SrcLds>(w, p0, 0, cur, len, fb, stream_start && f == 0, opts, S, fp, r, inf, lane, ht);"),
+                 (_FPR, _FPR.replace("__syncthreads();", "__syncthreads();\n    if (F > 0) return;", 1))]
+VARS["FPX2"] = [(_FPR, _FPR.replace("__syncthreads();", "__syncthreads();\n    if (F > 0) return;", 1))]
+VARS["FPX3"] = [(_FPE, _FPE.replace("__syncthreads();", "__syncthreads();\n    if (F > 0) return;", 1))]
+# k_demux_fp phase timestamps (s_memrealtime, 10 ns ticks) in the bitrate of frame infos 0..4
+# (tools/dbg/fp_times.py reads them): after staging, after the S loads, after the parse, after the resolve,
+# after wave 0's emits
+_FPT = "__builtin_amdgcn_s_memrealtime()"
+VARS["FPT"] = [
+    ("""    uint32_t fo_lane = 0u;""", """    const uint64_t t_0 = """ + _FPT + """;
+    uint32_t fo_lane = 0u;"""),
+    ("""    SrcLds::u8 *p0 = (SrcLds::u8 *)(uintptr_t)s_run;
+    uint8_t *dst = md;""", """    const uint64_t t_1 = """ + _FPT + """;
+    SrcLds::u8 *p0 = (SrcLds::u8 *)(uintptr_t)s_run;
+    uint8_t *dst = md;"""),
+    ("""    /* the wave's frames, one at a time in a loop that is not unrolled: the""",
+     """    const uint64_t t_2 = """ + _FPT + """;
+    /* the wave's frames, one at a time in a loop that is not unrolled: the"""),
+    ("""    __syncthreads();
+    /* The bit-reservoir map (resolve_frame's rules) for all frames at once,""",
+     """    __syncthreads();
+    const uint64_t t_3 = """ + _FPT + """;
+    /* The bit-reservoir map (resolve_frame's rules) for all frames at once,"""),
+    ("""    __syncthreads();
+    /* records and payloads, the wave's own frames */""",
+     """    __syncthreads();
+    const uint64_t t_4 = """ + _FPT + """;
+    /* records and payloads, the wave's own frames */"""),
+    ("""        /* the family of the last frame found (k_demux: of every frame) */""",
+     """        if (lane == 0 && infos && F >= 5) {
+            const uint64_t t_5 = """ + _FPT + """;
+            infos[0].bitrate_kbps = (int)(t_1 - t_0); infos[1].bitrate_kbps = (int)(t_2 - t_1);
+            infos[2].bitrate_kbps = (int)(t_3 - t_2); infos[3].bitrate_kbps = (int)(t_4 - t_3);
+            infos[4].bitrate_kbps = (int)(t_5 - t_4);
+        }
+        /* the family of the last frame found (k_demux: of every frame) */"""),
+]
 
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):

@@ -498,7 +498,7 @@ hipError_t upload_demux_constants(const uint16_t *frame_bytes) { return upload_d
 static_assert(FP_WAVES * FP_PER == FP_MAX, "k_demux_fp: frame slots");
 struct FpRes {      /* what the serial resolve needs of a parsed frame */
     int fb, plen, mdb;
-    uint32_t need;
+    uint32_t need, at; /* at: the header's offset in the run */
     int p00, p01, p10, p11;
     uint32_t flags; /* bit 0 lsf, 1 bad, 2 tag, 3 two channels */
 };
@@ -521,11 +521,20 @@ k_demux_fp(const uint8_t *__restrict__ in, uint32_t len, FpOffs fo, uint8_t *__r
     __shared__ FpRes s_res[FP_MAX];
     __shared__ FpOut s_out[FP_MAX];
     __shared__ uint32_t s_h1[FP_MAX];
+    __shared__ FrameRec s_rec[FP_MAX];
+    __shared__ DevInfo s_inf[FP_MAX];
     __shared__ int s_fin[3];
+    __shared__ uint32_t s_tab[HDR_TAB_WORDS];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
     constexpr int NT = 64 * FP_WAVES;
     StreamState &S = st[0];
+    /* the frame offsets (kernel arguments): all 64 loaded here, together,
+     * into lane f of every wave -- as fo.o[f] inside the frame loop each was
+     * a scalar load with its own round trip (8 of the kernel's 22 us) */
+    uint32_t fo_lane = 0u;
+#pragma unroll
+    for (int k = 0; k < FP_MAX; k++) fo_lane = lane == k ? fo.o[k] : fo_lane;
     /* the run's bytes (the mapped host buffer, 16-B aligned) into LDS: every
      * block's load in flight at once -- one bus round trip for the run; the
      * parse and the payload copy then read LDS */
@@ -554,6 +563,8 @@ k_demux_fp(const uint8_t *__restrict__ in, uint32_t len, FpOffs fo, uint8_t *__r
         if (i < nblk) s_run[i] = v[k];
     }
     if (tid == 0) s_run[nblk] = (u32x4){0u, 0u, 0u, 0u}; /* (the tail: the host zeroed 64 B past the frames too) */
+    hdr_tab_stage(s_tab, tid);
+    const HdrTabLds ht = {(const __attribute__((address_space(3))) uint32_t *)s_tab};
     __syncthreads(); /* the staged bytes; every read of the state before the run (the tag write below) */
     SrcLds::u8 *p0 = (SrcLds::u8 *)(uintptr_t)s_run;
     uint8_t *dst = md;
@@ -561,43 +572,35 @@ k_demux_fp(const uint8_t *__restrict__ in, uint32_t len, FpOffs fo, uint8_t *__r
     const bool stream_start = __builtin_amdgcn_readfirstlane((int)S.frames) == 0;
     if (wv == 0)
         for (int i = lane; i < (carry_in + 3) / 4; i += 64) ((uint32_t *)dst)[i] = ((const uint32_t *)S.res)[i];
-    /* the wave's frames' header windows, all in flight together */
-    HdrWin w[FP_PER];
-#pragma unroll
-    for (int j = 0; j < FP_PER; j++) {
-        const int f = wv + FP_WAVES * j;
-        if (f < F) w[j] = load_win<SrcLds>(p0, len, fo.o[f], lane);
-    }
-    FrameRec r[FP_PER];
-    DevInfo inf[FP_PER];
-    uint32_t need[FP_PER];
-    bool has[FP_PER];
-#pragma unroll
-    for (int j = 0; j < FP_PER; j++) {
-        const int f = wv + FP_WAVES * j;
-        has[j] = false;
-        need[j] = 0u;
-        rec_init(r[j], 0u, inf[j]);
-        if (f >= F) continue;
-        const uint32_t cur = fo.o[f];
+    /* the wave's frames, one at a time in a loop that is not unrolled: the
+     * kernel runs once per run, from a cold instruction cache, so its code
+     * size is time (the 4-way unrolled parse and copy made it 27.5 KB); the
+     * records go to LDS for the emit loop below */
+#pragma unroll 1
+    for (int f = wv; f < F; f += FP_WAVES) {
+        const uint32_t cur = (uint32_t)__builtin_amdgcn_readlane((int)fo_lane, f);
+        const HdrWin w = load_win<SrcLds>(p0, len, cur, lane);
+        FrameRec r;
+        DevInfo inf;
+        rec_init(r, 0u, inf);
         /* (the family was checked on the host: every frame's header is of
          * the stream's family) */
-        const int fb = hdr_frame_bytes(win_byte(w[j], 1), win_byte(w[j], 2), 0);
+        const int fb = hdr_frame_bytes(win_byte(w, 1), win_byte(w, 2), 0, ht);
         FrameParse fp;
         fp.fb = 0;
         fp.sw = 0;
         fp.h1 = 0u; /* stays 0: no header found (a valid one has h1 >= 0xE0) */
-        if (fb > 0) parse_frame<SrcLds>(w[j], p0, 0, cur, len, fb, stream_start && f == 0, opts, S, fp, r[j], inf[j], lane);
-        has[j] = fp.fb != 0;
-        need[j] = fp.need;
+        if (fb > 0) parse_frame<SrcLds>(w, p0, 0, cur, len, fb, stream_start && f == 0, opts, S, fp, r, inf, lane, ht);
         if (lane < 4) sideu[(size_t)f * 4 + lane] = fp.fb ? fp.sw : 0ull;
         if (lane == 0) {
             FpRes q;
-            q.fb = fp.fb; q.plen = fp.plen; q.mdb = fp.mdb; q.need = fp.need;
+            q.fb = fp.fb; q.plen = fp.plen; q.mdb = fp.mdb; q.need = fp.need; q.at = cur;
             q.p00 = fp.p00; q.p01 = fp.p01; q.p10 = fp.p10; q.p11 = fp.p11;
             q.flags = (fp.lsf ? 1u : 0u) | (fp.bad ? 2u : 0u) | (fp.tag ? 4u : 0u) | (fp.nch == 2 ? 8u : 0u);
             s_res[f] = q;
             s_h1[f] = fp.h1;
+            s_rec[f] = r;
+            s_inf[f] = inf;
         }
     }
     __syncthreads();
@@ -612,7 +615,7 @@ k_demux_fp(const uint8_t *__restrict__ in, uint32_t len, FpOffs fo, uint8_t *__r
      * by one wave this step took 17 of the kernel's 30 us (32 frames). */
     if (wv == 0) {
         const bool live = lane < F;
-        FpRes q = {0, 0, 0, 0u, 0, 0, 0, 0, 0u};
+        FpRes q = {0, 0, 0, 0u, 0u, 0, 0, 0, 0, 0u};
         if (live) q = s_res[lane];
         const bool found = live && q.fb != 0;
         const bool tag = found && (q.flags & 4u);
@@ -692,37 +695,60 @@ k_demux_fp(const uint8_t *__restrict__ in, uint32_t len, FpOffs fo, uint8_t *__r
         }
     }
     __syncthreads();
-    /* records and payloads, the wave's own frames (their parse results still
-     * in registers) */
-#pragma unroll
-    for (int j = 0; j < FP_PER; j++) {
-        const int f = wv + FP_WAVES * j;
-        if (f >= F) continue;
+    /* records and payloads, the wave's own frames */
+#pragma unroll 1
+    for (int f = wv; f < F; f += FP_WAVES) {
         const FpOut o = s_out[f];
-        r[j].payload_md = o.payload_md;
-        if (has[j]) {
-            r[j].md_bit = o.md_bit;
-            r[j].payload_len = (uint16_t)(o.lens & 0xFFFFu);
-            r[j].payload_avail = (uint16_t)(o.lens >> 16);
-            r[j].first_gr = (uint8_t)(o.gr_samples & 0xFFu);
-            inf[j].samples = (int)(o.gr_samples >> 8);
+        const FpRes q = s_res[f];
+        FrameRec r = s_rec[f];
+        DevInfo inf = s_inf[f];
+        r.payload_md = o.payload_md;
+        if (q.fb) {
+            r.md_bit = o.md_bit;
+            r.payload_len = (uint16_t)(o.lens & 0xFFFFu);
+            r.payload_avail = (uint16_t)(o.lens >> 16);
+            r.first_gr = (uint8_t)(o.gr_samples & 0xFFu);
+            inf.samples = (int)(o.gr_samples >> 8);
         }
         if (lane == 0) {
-            rec[f] = r[j];
-            if (infos) infos[f] = inf[j];
+            rec[f] = r;
+            if (infos) infos[f] = inf;
         }
-        if (has[j] && !(r[j].first_gr & REC_TAG)) {
-            const uint32_t body = (r[j].first_gr & REC_DROP) ? 4u : need[j];
-            copy_payload<SrcLds>(p0, dst, r[j], fo.o[f] + body, fo.o[f], lane);
+        if (q.fb && !(r.first_gr & REC_TAG)) {
+            const uint32_t body = (r.first_gr & REC_DROP) ? 4u : q.need;
+            copy_payload<SrcLds>(p0, dst, r, q.at + body, q.at, lane);
         }
     }
-    __syncthreads(); /* every wave's md stores before the carry is read back */
     if (wv == 0) {
+        /* the next carry: md bytes [P - c, P), taken from the staged run (or,
+         * before the run's first payload, from the carry-in), not read back
+         * from md -- so no barrier waits for the other waves' md stores */
         const uint32_t P = (uint32_t)s_fin[0];
         const int avail = s_fin[1];
         int c = avail < MP3D_RES_BYTES ? avail : MP3D_RES_BYTES;
         if ((uint32_t)c > P) c = (int)P;
-        for (int i = lane; i < c; i += 64) S.res[i] = dst[P - c + i];
+        for (int i = lane; i < c; i += 64) {
+            const uint32_t x = P - (uint32_t)c + (uint32_t)i;
+            /* the frame whose copied payload holds md byte x (payloads are
+             * back to back in md; a tag frame copies none) */
+            int f = F - 1;
+            for (; f >= 0; f--) {
+                const FpOut o = s_out[f];
+                const uint32_t plen = (o.gr_samples & REC_TAG) ? 0u : (o.lens & 0xFFFFu);
+                if (x >= o.payload_md && x < o.payload_md + plen) break;
+            }
+            uint32_t v;
+            if (f < 0) {
+                v = S.res[x]; /* the carry-in (md [0, carry_in)); x >= i: read before overwritten */
+            } else {
+                const FpOut o = s_out[f];
+                const FpRes q = s_res[f];
+                const uint32_t off = x - o.payload_md;
+                const uint32_t body = (o.gr_samples & REC_DROP) ? 4u : q.need;
+                v = off < (o.lens >> 16) ? (uint32_t)p0[q.at + body + off] : 0u; /* past the bytes present: zeros */
+            }
+            S.res[i] = (uint8_t)v;
+        }
         /* the family of the last frame found (k_demux: of every frame) */
         int kind = __builtin_amdgcn_readfirstlane(S.kind);
         for (int f = 0; f < F; f++)

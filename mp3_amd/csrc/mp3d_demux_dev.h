@@ -45,12 +45,31 @@ __device__ __forceinline__ int hdr_sr_idx(uint32_t b1, uint32_t b2) {
     const uint32_t ver = (b1 >> 3) & 3, si = (b2 >> 2) & 3;
     return (int)si + (ver == 3 ? 0 : ver == 2 ? 3 : 6);
 }
-__device__ __forceinline__ int hdr_frame_bytes(uint32_t b1, uint32_t b2, int kind) {
+/* the header tables: the __constant__ copies, or a kernel's LDS copy
+ * (k_demux_fp: a scalar load from L2 or HBM per frame was a round trip on
+ * every wave's chain of frames) */
+struct HdrTabConst {
+    __device__ __forceinline__ uint32_t fw(int sr, int bi) const { return c_frame_word[sr][bi]; }
+    __device__ __forceinline__ uint32_t hz(int sr) const { return MP3D_SAMPLE_RATE[sr]; }
+};
+struct HdrTabLds {
+    const __attribute__((address_space(3))) uint32_t *t; /* [9][16] frame words, then [9] sample rates */
+    __device__ __forceinline__ uint32_t fw(int sr, int bi) const { return t[16 * sr + bi]; }
+    __device__ __forceinline__ uint32_t hz(int sr) const { return t[144 + sr]; }
+};
+#define HDR_TAB_WORDS (9 * 16 + 9)
+/* an HdrTabLds table's words (tid < HDR_TAB_WORDS; the caller's barrier follows) */
+__device__ __forceinline__ void hdr_tab_stage(uint32_t *t, int tid) {
+    if (tid < 9 * 16) t[tid] = (&c_frame_word[0][0])[tid];
+    else if (tid < HDR_TAB_WORDS) t[tid] = MP3D_SAMPLE_RATE[tid - 9 * 16];
+}
+template <class T = HdrTabConst>
+__device__ __forceinline__ int hdr_frame_bytes(uint32_t b1, uint32_t b2, int kind, const T &tab = T()) {
     if ((b1 & 0xE0) != 0xE0 || ((b1 >> 1) & 3) != 1 || ((b1 >> 3) & 3) == 1) return -1;
     const int bi = (int)(b2 >> 4);
     if (bi == 0 || bi == 15 || ((b2 >> 2) & 3) == 3) return -1;
     if (kind && hdr_kind(b1) != kind) return -1;
-    return (int)(c_frame_word[hdr_sr_idx(b1, b2)][bi] & 0xFFFFu) + (int)((b2 >> 1) & 1);
+    return (int)(tab.fw(hdr_sr_idx(b1, b2), bi) & 0xFFFFu) + (int)((b2 >> 1) & 1);
 }
 
 /* bit offset of unit (gr, ch) inside the side info: MPEG-1 9-bit
@@ -211,10 +230,10 @@ struct FrameParse {
  * w at cur); f0 = the stream's first frame of the stream's first call (the
  * Xing/Info tag check); r / inf get the frame's fields.  The tag's LAME
  * fields go to S (lane 0). */
-template <class M>
+template <class M, class T = HdrTabConst>
 __device__ __forceinline__ void parse_frame(const HdrWin &w, typename M::u8 *p0, uint64_t base, uint32_t cur,
                                             uint32_t len, int fb, bool f0, int opts, StreamState &S, FrameParse &fp,
-                                            FrameRec &r, DevInfo &inf, int lane) {
+                                            FrameRec &r, DevInfo &inf, int lane, const T &tab = T()) {
     fp.fb = 0;
     fp.sw = 0;
     fp.bad = fp.tag = false;
@@ -241,8 +260,8 @@ __device__ __forceinline__ void parse_frame(const HdrWin &w, typename M::u8 *p0,
     r.side_off = (uint8_t)(4 + crc);
     r.sr_idx = (uint8_t)hdr_sr_idx(h1, h2);
     r.lsf = (uint8_t)lsf;
-    inf.frame_bytes = fb; inf.channels = nch; inf.hz = (int)MP3D_SAMPLE_RATE[r.sr_idx];
-    inf.layer = 3; inf.bitrate_kbps = (int)(c_frame_word[r.sr_idx][h2 >> 4] >> 16);
+    inf.frame_bytes = fb; inf.channels = nch; inf.hz = (int)tab.hz(r.sr_idx);
+    inf.layer = 3; inf.bitrate_kbps = (int)(tab.fw(r.sr_idx, (int)(h2 >> 4)) >> 16);
     /* side info: bit offsets relative to the window's dword base */
     const uint32_t sbit = 8u * (w.mis + 4u + (uint32_t)crc);
     fp.mdb = (int)(win_bits64(w, sbit) >> (lsf ? 56 : 55));
