@@ -538,9 +538,8 @@ VARS["FPX2A"] = [("        if (fb > 0) parse_frame<SrcLds>(w, p0, 0, cur, len, f
                  (_FPR, _FPR.replace("__syncthreads();", "__syncthreads();\n    if (F > 0) return;", 1))]
 VARS["FPX2"] = [(_FPR, _FPR.replace("__syncthreads();", "__syncthreads();\n    if (F > 0) return;", 1))]
 VARS["FPX3"] = [(_FPE, _FPE.replace("__syncthreads();", "__syncthreads();\n    if (F > 0) return;", 1))]
-# k_demux_fp phase timestamps (s_memrealtime, 10 ns ticks) in the bitrate of frame infos 0..4
-# (tools/dbg/fp_times.py reads them): after staging, after the S loads, after the parse, after the resolve,
-# after wave 0's emits
+# k_demux_fp phase timestamps (s_memrealtime, 10 ns ticks) in the bitrate of frame infos 0..3
+# (tools/dbg/fp_times.py reads them): staging, state loads, wave 0's parse + resolve, wave 0's emits
 _FPT = "__builtin_amdgcn_s_memrealtime()"
 VARS["FPT"] = [
     ("""    uint32_t fo_lane = 0u;""", """    const uint64_t t_0 = """ + _FPT + """;
@@ -549,25 +548,19 @@ VARS["FPT"] = [
     uint8_t *dst = md;""", """    const uint64_t t_1 = """ + _FPT + """;
     SrcLds::u8 *p0 = (SrcLds::u8 *)(uintptr_t)s_run;
     uint8_t *dst = md;"""),
-    ("""    /* the wave's frames, one at a time in a loop that is not unrolled: the""",
+    ("""    /* Wave 0 alone: the frames' headers and side info, lane f = frame f""",
      """    const uint64_t t_2 = """ + _FPT + """;
-    /* the wave's frames, one at a time in a loop that is not unrolled: the"""),
-    ("""    __syncthreads();
-    /* The bit-reservoir map (resolve_frame's rules) for all frames at once,""",
-     """    __syncthreads();
-    const uint64_t t_3 = """ + _FPT + """;
-    /* The bit-reservoir map (resolve_frame's rules) for all frames at once,"""),
+    /* Wave 0 alone: the frames' headers and side info, lane f = frame f"""),
     ("""    __syncthreads();
     /* records and payloads, the wave's own frames */""",
      """    __syncthreads();
-    const uint64_t t_4 = """ + _FPT + """;
+    const uint64_t t_3 = """ + _FPT + """;
     /* records and payloads, the wave's own frames */"""),
     ("""        /* the family of the last frame found (k_demux: of every frame) */""",
-     """        if (lane == 0 && infos && F >= 5) {
-            const uint64_t t_5 = """ + _FPT + """;
+     """        if (lane == 0 && infos && F >= 4) {
+            const uint64_t t_4 = """ + _FPT + """;
             infos[0].bitrate_kbps = (int)(t_1 - t_0); infos[1].bitrate_kbps = (int)(t_2 - t_1);
             infos[2].bitrate_kbps = (int)(t_3 - t_2); infos[3].bitrate_kbps = (int)(t_4 - t_3);
-            infos[4].bitrate_kbps = (int)(t_5 - t_4);
         }
         /* the family of the last frame found (k_demux: of every frame) */"""),
 ]

@@ -481,21 +481,19 @@ hipError_t upload_demux_constants(const uint16_t *frame_bytes) { return upload_d
 /* ------------------------------------------------------------------------ */
 /* k_demux_fp: one stream's run of pre-located, complete frames (the per-  */
 /* frame decoder's read-ahead runs, mp3d_host.cpp ra_fill: the host has     */
-/* found every frame, fo[f] = its header offset in the run's bytes, which  */
-/* the kernel reads from the mapped host buffer) demuxed frame-parallel in  */
-/* ONE workgroup, with the same results as k_demux: the waves parse the     */
-/* frames' headers and side info side by side (parse_frame), one wave runs  */
-/* the bit-reservoir map over them in order (resolve_frame, the only serial */
-/* step), then the waves write the records and copy the payloads in        */
-/* parallel.  It also does the run's state book-keeping that would         */
-/* otherwise be separate copies: the previous run's synthesis tail into     */
-/* StreamState (tail_in, may be null) and then the snapshot of the state   */
-/* before the run (snap) that a settle restores.                           */
+/* found every frame, fo[f] = its header offset in the run's bytes, passed  */
+/* as kernel arguments) demuxed frame-parallel in ONE workgroup, with the   */
+/* same results as k_demux: the run's bytes are staged in LDS, wave 0       */
+/* parses every frame's header and side info on its own lane and runs the  */
+/* bit-reservoir map over them (a prefix scan: resolve_frame's rules), then */
+/* the waves write the records and copy the payloads in parallel.  It also  */
+/* does the run's state book-keeping that would otherwise be separate       */
+/* copies: the previous run's synthesis tail into StreamState (tail_in, may */
+/* be null) and then the snapshot of the state before the run (snap) that a */
+/* settle restores.                                                        */
 /* ------------------------------------------------------------------------ */
 #define FP_WAVES 16
-#define FP_MAX 64   /* frames per run (MP3D_PF_READAHEAD <= 64) */
-#define FP_PER 4    /* frames per wave */
-static_assert(FP_WAVES * FP_PER == FP_MAX, "k_demux_fp: frame slots");
+#define FP_MAX 64   /* frames per run (MP3D_PF_READAHEAD <= 64): one lane of wave 0 each */
 struct FpRes {      /* what the serial resolve needs of a parsed frame */
     int fb, plen, mdb;
     uint32_t need, at; /* at: the header's offset in the run */
@@ -570,53 +568,113 @@ k_demux_fp(const uint8_t *__restrict__ in, uint32_t len, FpOffs fo, uint8_t *__r
     uint8_t *dst = md;
     const int carry_in = __builtin_amdgcn_readfirstlane(S.res_len);
     const bool stream_start = __builtin_amdgcn_readfirstlane((int)S.frames) == 0;
-    if (wv == 0)
+    if (wv == FP_WAVES - 1)
         for (int i = lane; i < (carry_in + 3) / 4; i += 64) ((uint32_t *)dst)[i] = ((const uint32_t *)S.res)[i];
-    /* the wave's frames, one at a time in a loop that is not unrolled: the
-     * kernel runs once per run, from a cold instruction cache, so its code
-     * size is time (the 4-way unrolled parse and copy made it 27.5 KB); the
-     * records go to LDS for the emit loop below */
-#pragma unroll 1
-    for (int f = wv; f < F; f += FP_WAVES) {
-        const uint32_t cur = (uint32_t)__builtin_amdgcn_readlane((int)fo_lane, f);
-        const HdrWin w = load_win<SrcLds>(p0, len, cur, lane);
-        FrameRec r;
-        DevInfo inf;
-        rec_init(r, 0u, inf);
-        /* (the family was checked on the host: every frame's header is of
-         * the stream's family) */
-        const int fb = hdr_frame_bytes(win_byte(w, 1), win_byte(w, 2), 0, ht);
-        FrameParse fp;
-        fp.fb = 0;
-        fp.sw = 0;
-        fp.h1 = 0u; /* stays 0: no header found (a valid one has h1 >= 0xE0) */
-        if (fb > 0) parse_frame<SrcLds>(w, p0, 0, cur, len, fb, stream_start && f == 0, opts, S, fp, r, inf, lane, ht);
-        if (lane < 4) sideu[(size_t)f * 4 + lane] = fp.fb ? fp.sw : 0ull;
-        if (lane == 0) {
-            FpRes q;
-            q.fb = fp.fb; q.plen = fp.plen; q.mdb = fp.mdb; q.need = fp.need; q.at = cur;
-            q.p00 = fp.p00; q.p01 = fp.p01; q.p10 = fp.p10; q.p11 = fp.p11;
-            q.flags = (fp.lsf ? 1u : 0u) | (fp.bad ? 2u : 0u) | (fp.tag ? 4u : 0u) | (fp.nch == 2 ? 8u : 0u);
-            s_res[f] = q;
-            s_h1[f] = fp.h1;
-            s_rec[f] = r;
-            s_inf[f] = inf;
-        }
-    }
-    __syncthreads();
-    /* The bit-reservoir map (resolve_frame's rules) for all frames at once,
-     * lane f = frame f (F <= 64): each payload's md position is a prefix sum
-     * of the payload lengths; the bytes available after a frame depend on
-     * the frames before it only through the underflow test mdb > avail, so
-     * every frame's "avail after" is first taken as if no frame underflowed,
-     * the avail before each frame found by a last-setter scan, and the
-     * frames that do underflow recomputed until nothing changes (one pass
-     * unless a stream starts mid-way or a frame is dropped).  Done serially
-     * by one wave this step took 17 of the kernel's 30 us (32 frames). */
+    /* Wave 0 alone: the frames' headers and side info, lane f = frame f
+     * (k_walk's lane-per-stream parse, over the staged run), then the
+     * bit-reservoir map over them.  (A wave per frame, four frames in turn
+     * per wave, spent 8.7 of the kernel's 22 us on its chains of cross-lane
+     * reads: s_memrealtime stamps, build FPT.)
+     * The map (resolve_frame's rules) for all frames at once: each
+     * payload's md position is a prefix sum of the payload lengths; the
+     * bytes available after a frame depend on the frames before it only
+     * through the underflow test mdb > avail, so every frame's "avail after"
+     * is first taken as if no frame underflowed, the avail before each frame
+     * found by a last-setter scan, and the frames that do underflow
+     * recomputed until nothing changes (one pass unless a stream starts
+     * mid-way or a frame is dropped).  Done serially by one wave this step
+     * took 17 of the kernel's 30 us (32 frames). */
     if (wv == 0) {
         const bool live = lane < F;
         FpRes q = {0, 0, 0, 0u, 0u, 0, 0, 0, 0, 0u};
-        if (live) q = s_res[lane];
+        FrameRec r;
+        DevInfo inf;
+        rec_init(r, 0u, inf);
+        uint32_t h1 = 0u; /* stays 0: no header found (a valid one has h1 >= 0xE0) */
+        uint64_t sw[4] = {0ull, 0ull, 0ull, 0ull};
+        if (live) {
+            const uint32_t cur = fo_lane;
+            LaneWin W; /* the frame's bytes where they are staged (64 zero bytes follow the run) */
+            W.w = (uint32_t *)s_run + (cur >> 2);
+            W.pos = cur;
+            W.mis = cur & 3u;
+            const uint32_t b1 = W.byte(1), b2 = W.byte(2), b3 = W.byte(3);
+            /* (the family was checked on the host: every frame's header is of
+             * the stream's family) */
+            const int fb = hdr_frame_bytes(b1, b2, 0, ht);
+            const int nch = (b3 >> 6) == 3 ? 1 : 2;
+            const int crc = (b1 & 1) ? 0 : 2;
+            const bool lsf = hdr_kind(b1) == 2;
+            const int ngr = lsf ? 1 : 2;
+            const int side_bytes = lsf ? (nch == 1 ? 9 : 17) : (nch == 1 ? 17 : 32);
+            const uint32_t need = 4u + (uint32_t)crc + (uint32_t)side_bytes;
+            /* a final frame cut short still decodes (FFmpeg: the missing
+             * bytes read as zeros) once its header and side info are present */
+            if (fb > 0 && (cur + (uint32_t)fb <= len || cur + need <= len)) {
+                const uint32_t have = min(len - cur, (uint32_t)fb);
+                const int plen = fb - 4 - crc - side_bytes;
+                r.frame_off = cur;
+                r.frame_bytes = (uint16_t)fb;
+                r.payload_len = (uint16_t)(plen > 0 ? plen : 0);
+                r.hdr1 = (uint8_t)b1; r.hdr2 = (uint8_t)b2; r.hdr3 = (uint8_t)b3;
+                r.nch = (uint8_t)nch;
+                r.side_off = (uint8_t)(4 + crc);
+                r.sr_idx = (uint8_t)hdr_sr_idx(b1, b2);
+                r.lsf = (uint8_t)lsf;
+                inf.frame_bytes = fb; inf.channels = nch; inf.hz = (int)ht.hz(r.sr_idx);
+                inf.layer = 3; inf.bitrate_kbps = (int)(ht.fw(r.sr_idx, (int)(b2 >> 4)) >> 16);
+                const uint32_t sbit = 8u * (4u + (uint32_t)crc);
+                const int mdb = (int)(W.bits64(sbit) >> (lsf ? 56 : 55));
+                uint32_t p23[4] = {0u, 0u, 0u, 0u};
+                bool anybad = false;
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int qgr = u >> 1, qch = u & 1;
+                    if (qch < nch && qgr < ngr) {
+                        const uint32_t ub = sbit + side_unit_bit(nch, qgr, qch, lsf);
+                        uint64_t v59;
+                        uint32_t low5;
+                        if (lsf) { /* the 63-bit LSF unit in the MPEG-1 layout (parse_frame) */
+                            const uint64_t v63 = W.bits64(ub) >> 1;
+                            const uint32_t sfc9 = (uint32_t)(v63 >> 25) & 511u;
+                            const uint64_t low25 = v63 & 0x1FFFFFFull;
+                            const bool is_right = (b3 >> 6) == 1 && ((b3 >> 4) & 1) && qch == 1;
+                            v59 = ((v63 >> 34) << 30) | ((uint64_t)(sfc9 & 15u) << 26) | ((low25 >> 2) << 3) |
+                                  ((uint64_t)is_right << 2) | (low25 & 3u);
+                            low5 = sfc9 >> 4;
+                        } else {
+                            v59 = W.bits64(ub) >> 5;
+                            low5 = (uint32_t)(W.bits64(sbit + 9 + (nch == 1 ? 5 : 3) + 4 * qch) >> 60) << 1;
+                        }
+                        p23[u] = (uint32_t)(v59 >> 47);
+                        /* FFmpeg drops the frame: big_values > 288, or window
+                         * switching with the reserved block_type 0 */
+                        anybad |= ((v59 >> 38) & 0x1FFu) > 288u || (v59 & (7ull << 23)) == (4ull << 23);
+                        sw[u] = (v59 << 5) | low5;
+                    }
+                }
+                const bool crc_bad = (opts & MP3D_OPT_CRC_CHECK) && crc && !walk_crc_ok(W, (uint32_t)side_bytes);
+                const uint32_t tgo = 4u + (uint32_t)crc + (uint32_t)side_bytes;
+                const bool tag = stream_start && lane == 0 && plen >= 4 && have == (uint32_t)fb &&
+                                 ((W.byte(tgo) == 'X' && W.byte(tgo + 1) == 'i' && W.byte(tgo + 2) == 'n' &&
+                                   W.byte(tgo + 3) == 'g') ||
+                                  (W.byte(tgo) == 'I' && W.byte(tgo + 1) == 'n' && W.byte(tgo + 2) == 'f' &&
+                                   W.byte(tgo + 3) == 'o'));
+                if (tag) S.tag_info = parse_info_tag(p0 + cur + tgo, (uint32_t)fb - tgo, S.tag_frames);
+                q.fb = fb; q.plen = plen; q.mdb = mdb; q.need = need; q.at = cur;
+                q.p00 = (int)p23[0]; q.p01 = (int)p23[1]; q.p10 = (int)p23[2]; q.p11 = (int)p23[3];
+                q.flags = (lsf ? 1u : 0u) | ((plen < 0 || anybad || crc_bad) ? 2u : 0u) | (tag ? 4u : 0u) |
+                          (nch == 2 ? 8u : 0u);
+                h1 = b1;
+            }
+            ulonglong2 *sd = (ulonglong2 *)&sideu[(size_t)lane * 4];
+            sd[0] = make_ulonglong2(sw[0], sw[1]);
+            sd[1] = make_ulonglong2(sw[2], sw[3]);
+            s_res[lane] = q;
+            s_h1[lane] = h1;
+            s_rec[lane] = r;
+            s_inf[lane] = inf;
+        }
         const bool found = live && q.fb != 0;
         const bool tag = found && (q.flags & 4u);
         const bool bad = found && !tag && (q.flags & 2u);

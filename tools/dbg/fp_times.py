@@ -2,7 +2,8 @@
 """k_demux_fp phase times from the FPT build (abx/variants.py): decode
 tests/golden/long_c3_512 through the per-frame call and print, per read-ahead
 run, the s_memrealtime deltas (us) the kernel left in the bitrate of the
-run's first five frame infos: staging, state loads, parse, resolve, emit."""
+run's first four frame infos: staging, state loads, wave 0's parse +
+resolve, wave 0's emits."""
 import os
 import sys
 
@@ -27,8 +28,8 @@ for rep in range(3):
         pos += info.frame_bytes
         cur.append(info.bitrate_kbps)
         k += 1
-    for r0 in range(0, len(cur) - 4, 64):
-        rows.append([x / 100.0 for x in cur[r0:r0 + 5]])
+    for r0 in range(0, len(cur) - 3, 64):
+        rows.append([x / 100.0 for x in cur[r0:r0 + 4]])
 a = np.array(rows)
 print("runs", len(a))
-print("median us: staging %.2f  state %.2f  parse %.2f  resolve %.2f  emit %.2f" % tuple(np.median(a, axis=0)))
+print("median us: staging %.2f  state %.2f  parse + resolve %.2f  emit %.2f" % tuple(np.median(a, axis=0)))
