@@ -336,6 +336,9 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
      * where the state starts: the call's state (StreamState or the previous
      * call's tail) for segment 0; zeros before a warm-up that fixes it */
     int fw = seg ? f0 - 1 : 0;
+    /* the last audio frame before f0 (decode path): its last granule is the
+     * last warm-up granule, the one whose X fixes the synthesis history */
+    int wlast = -1;
     bool from_state = seg == 0, ch1_state = false;
     if (!SRC_XR && seg > 0) {
         /* decode path (frame-parallel segments of a stream):
@@ -359,6 +362,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
         bool mono = false;
         for (int f = f0 - 1; f >= 0 && found < need; f--)
             if (audio(f)) {
+                if (!found) wlast = f;
                 found++;
                 fa = f;
                 mono = mono || !stereo(f);
@@ -1187,11 +1191,12 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                 }
                 __syncthreads();
             }
-            /* a warm-up frame's granule 0 (frame-parallel segments): only
-             * its IMDCT overlap is used (granule 1's S reads it), so it skips
-             * S, phases M and W -- its synthesis history is replaced by granule
-             * 1's, whose window output is not stored either */
-            if (!SRC_XR && !LSF && PF == 0 && f < f0 && gr == 0) {
+            /* a warm-up granule before the last one (frame-parallel
+             * segments): only its IMDCT overlap is used (the next granule's S
+             * reads it), so it skips S, phases M and W -- the synthesis
+             * history is rebuilt from one granule's X alone, the last warm-up
+             * granule's, and no warm-up output is stored */
+            if (!SRC_XR && PF == 0 && f < wlast + (LSF || gr == 1 ? 0 : 1)) {
                 WAIT_VMCNT0(); /* (phase W's drain: the next granule's prefetch has landed) */
                 wave_sync();
                 continue;
