@@ -564,6 +564,9 @@ VARS["FPT"] = [
         }
         /* the family of the last frame found (k_demux: of every frame) */"""),
 ]
+# is[] row stride (int16 per unit row): 640 (1 280 B, 10 lines), 608 (1 216 B, 9.5 lines)
+VARS["ISR640"] = [("FLAGS", "-DMP3D_IS_ROW=640")]
+VARS["ISR608"] = [("FLAGS", "-DMP3D_IS_ROW=608")]
 
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):

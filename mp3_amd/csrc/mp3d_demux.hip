@@ -361,7 +361,7 @@ __global__ void __launch_bounds__(64) k_walk(const uint8_t *__restrict__ in, con
  * branch makes the compiler's waitcnt pass drain vmcnt(0) at the join.  An
  * aligned source loads words (k - 1, k) instead of (k, k + 1), so no load
  * passes the payload's last word (word -1 is side info or header). */
-#define MDC_WAVES 4
+#define MDC_WAVES 16
 #define MDC_QROUNDS 2 /* 16-lane rounds of word quadruples per frame, unrolled: 512 B */
 __global__ void __launch_bounds__(64 * MDC_WAVES) k_mdcopy(const uint8_t *__restrict__ in, uint8_t *__restrict__ md,
                                                          const uint64_t *__restrict__ md_off,

@@ -550,7 +550,7 @@ extern "C" int mp3d_batch_create(int device, int max_streams, int max_frames, mp
     BALLOC(b->st, sizeof(StreamState) * max_streams);
     BALLOC(b->rec, sizeof(FrameRec) * (size_t)max_streams * max_frames);
     BALLOC(b->sideu, sizeof(uint64_t) * units);
-    BALLOC(b->is_buf, sizeof(int16_t) * 576 * units);
+    BALLOC(b->is_buf, sizeof(int16_t) * MP3D_IS_ROW * units);
     BALLOC(b->meta, sizeof(UnitMeta) * units);
     BALLOC(b->rank, sizeof(uint32_t) * units); /* k_huffman's big_values order (k_rank) */
     for (auto &g : b->geo) BALLOC(g.d, 20 * (size_t)max_streams);
@@ -918,12 +918,13 @@ extern "C" int mp3d_batch_huffman_only(mp3d_batch *b, const uint8_t *frames, con
          * returns whole rows, so clear them first */
         int r = call_begin(b, s);
         if (r) return r;
-        HIPCHK(hipMemsetAsync(b->is_buf, 0, units * 576 * sizeof(int16_t), s));
+        HIPCHK(hipMemsetAsync(b->is_buf, 0, units * MP3D_IS_ROW * sizeof(int16_t), s));
     }
     int r = run_front(b, frames, offsets, sizes, n, F, s, &sync_needed);
     if (r) return r;
     if (is_out) {
-        HIPCHK(hipMemcpyAsync(is_out, b->is_buf, units * 576 * sizeof(int16_t), hipMemcpyDefault, s));
+        HIPCHK(hipMemcpy2DAsync(is_out, 576 * sizeof(int16_t), b->is_buf, MP3D_IS_ROW * sizeof(int16_t),
+                                576 * sizeof(int16_t), units, hipMemcpyDefault, s));
         sync_needed |= ptr_kind(is_out, b->device) == PTR_HOST;
     }
     if (sf_out) {

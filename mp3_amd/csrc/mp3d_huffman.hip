@@ -232,7 +232,7 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                      * the part2_3 end (FFmpeg: a truncated unit's remaining
                      * lines read as zeros), stores a zero word and consumes no
                      * bits -- the count1 lines then overwrite the group's tail */
-                    int16_t *row = is_buf + (size_t)u * 576;
+                    int16_t *row = is_buf + (size_t)u * MP3D_IS_ROW;
                     int k = 0;
                     const uint32_t end_bit = start + seg + p23;
                     for (; __ballot(k < bv2); k += 8) {
@@ -353,7 +353,7 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
             }
             if (valid && !dec) {
                 /* granule lost to a reservoir underflow: silence (FFmpeg) */
-                int16_t *out = is_buf + (size_t)u * 576;
+                int16_t *out = is_buf + (size_t)u * MP3D_IS_ROW;
                 for (int kk = 0; kk < 576; kk += 8) *(uint4 *)(out + kk) = make_uint4(0, 0, 0, 0);
                 UnitMeta m;
 #pragma unroll

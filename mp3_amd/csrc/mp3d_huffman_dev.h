@@ -358,7 +358,7 @@ __device__ __forceinline__ void huffman_wave_unit(const uint8_t *__restrict__ md
     const uint64_t side = sq[q];
     if (!dec) {
         /* granule lost to a reservoir underflow: silence (FFmpeg) */
-        uint4 *out = (uint4 *)(is_buf + (size_t)u * 576);
+        uint4 *out = (uint4 *)(is_buf + (size_t)u * MP3D_IS_ROW);
         for (int i = lane; i < 72; i += 64) out[i] = make_uint4(0u, 0u, 0u, 0u);
         if (lane == 0) {
             UnitMeta m;
@@ -453,7 +453,7 @@ __device__ __forceinline__ void huffman_wave_unit(const uint8_t *__restrict__ md
     ts2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)ts2);
     pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)pos);
     /* the unit's is[] row as words (line pairs), nw written so far */
-    uint32_t *row = (uint32_t *)(is_buf + (size_t)u * 576);
+    uint32_t *row = (uint32_t *)(is_buf + (size_t)u * MP3D_IS_ROW);
     int nw = 0;
     const uint32_t end_bit = (uint32_t)__builtin_amdgcn_readfirstlane((int)(start + seg + p23));
     const int bvu = __builtin_amdgcn_readfirstlane(bv2);

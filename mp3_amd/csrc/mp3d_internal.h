@@ -7,7 +7,7 @@
  *   rec     : FrameRec[n_streams * F]         (k_demux, 32 B per frame)
  *   md      : per-stream main-data byte region (carry-in + payloads),
  *             stream s at md_off[s] (16-B aligned), read as big-endian words
- *   is_buf  : int16 [n_streams * F * 4][576]  (k_huffman -> k_synth)
+ *   is_buf  : int16 [n_streams * F * 4][MP3D_IS_ROW]  (k_huffman -> k_synth; 576 lines used)
  *   meta    : UnitMeta[n_streams * F * 4]    (scalefactors + gains)
  *   state   : StreamState[max_streams]        (reservoir, overlap, V FIFO)
  *   pcm     : int16 [n_streams * F][1152 * 2] (interleaved L/R; mono: 1152)
@@ -97,6 +97,11 @@ struct StreamState {
 };
 /* 0x05 in every byte: one hipMemset2D per slot array; 5 = the format of
  * ABI v5 (fifo = partial sums in float units) */
+/* int16 elements per unit row of is_buf (576 lines; a longer row only
+ * pads: the A/B of row placement in the L2) */
+#ifndef MP3D_IS_ROW
+#define MP3D_IS_ROW 576
+#endif
 #define MP3D_STATE_FMT 0x05050505u
 #define MP3D_STATE_FMT_BYTE 0x05
 

@@ -426,9 +426,9 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
     /* Per-stream buffer resources: every granule access below is a buffer
      * instruction with a uniform byte offset in an SGPR and the lane offset
      * in one VGPR, instead of a 64-bit address pair per lane and load. */
-    const int gb = 2 * 576 * 2;                   /* is[] bytes per granule (2 ch) */
+    const int rb = 2 * MP3D_IS_ROW, gb = 2 * rb; /* is[] bytes per row, per granule (2 ch) */
     const __amdgpu_buffer_rsrc_t r_is = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(is_buf + (size_t)s * F * 4 * 576), 0, F * 2 * gb, 0x00020000);
+        (void *)(is_buf + (size_t)s * F * 4 * MP3D_IS_ROW), 0, F * 2 * gb, 0x00020000);
     const __amdgpu_buffer_rsrc_t r_meta = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(meta + (size_t)s * F * 4), 0, F * 4 * (int)sizeof(UnitMeta), 0x00020000);
     const __amdgpu_buffer_rsrc_t r_rec = __builtin_amdgcn_make_buffer_rsrc(
@@ -481,13 +481,13 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
      * vmcnt(0) before phase W (and after prefetch_full); the hardware counts
      * these loads like any other, so the compiler's counted waits for its
      * own loads can only over-wait. */
-    const uint64_t isb = (uint64_t)(uintptr_t)(is_buf + (size_t)s * F * 4 * 576);
+    const uint64_t isb = (uint64_t)(uintptr_t)(is_buf + (size_t)s * F * 4 * MP3D_IS_ROW);
     auto dma_is = [&](int g, int nz0, int nz1) {
         const int lo = opaque(lane * 4);
         const uint32_t lds0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uintptr_t)(lds_cf32 *)(const float *)isq);
 #pragma unroll
         for (int c = 0; c < 2; c++) {
-            const uint64_t ra = isb + (uint64_t)(uint32_t)(g * gb + c * 1152);
+            const uint64_t ra = isb + (uint64_t)(uint32_t)(g * gb + c * rb);
             const u32x4 rs = {(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)ra),
                               (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(ra >> 32)) & 0xFFFFu,
                               (uint32_t)__builtin_amdgcn_readfirstlane(2 * (c ? nz1 : nz0)), 0x00020000u};
@@ -523,7 +523,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
             for (int i = 0; i < 5; i++) {
                 nis[c][i] = 0u;
                 if ((i < 4 || lane < 32) && 2 * lane + 128 * i < nz)
-                    nis[c][i] = __builtin_amdgcn_raw_buffer_load_b32(r_is, lo + c * 1152 + 256 * i, g * gb, 0);
+                    nis[c][i] = __builtin_amdgcn_raw_buffer_load_b32(r_is, lo + c * rb + 256 * i, g * gb, 0);
             }
         }
     };
