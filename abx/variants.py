@@ -567,6 +567,8 @@ VARS["FPT"] = [
 # is[] row stride (int16 per unit row): 640 (1 280 B, 10 lines), 608 (1 216 B, 9.5 lines)
 VARS["ISR640"] = [("FLAGS", "-DMP3D_IS_ROW=640")]
 VARS["ISR608"] = [("FLAGS", "-DMP3D_IS_ROW=608")]
+# k_huffman without the count1 loop (output wrong): what the count1 tail costs
+VARS["NC1"] = [("                    while (k <= 572 && pos < end_bit) {", "                    while (k <= 572 && pos < end_bit && F < 0) {")]
 
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
