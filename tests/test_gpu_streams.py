@@ -75,3 +75,34 @@ def test_state_buffer_size_checks():
     st = dec.get_state(0, 4)
     dec.set_state(torch.from_numpy(st.view(np.int32)).cuda(), first=0)  # 4 blobs as int32 words
     assert np.array_equal(dec.get_state(0, 4), st)
+
+
+def test_geometry_cache_large_batch():
+    """The geometry cache (mp3d_host.cpp prepare_geometry) at more than 1 024
+    streams: a call with the same offsets and sizes skips the staging copy, a
+    call that changes them (same count) stages again.  Three calls on one
+    handle -- batch A, batch B with A's geometry but other bytes, batch C with
+    other sizes -- each equal a fresh handle's decode of the same batch."""
+    n, F = 1500, 3
+    bufA, offs, sizes = _gen.batch(_gen.C5, 9300, n, F, threads=4)
+    bufB = bufA.copy()
+    # batch B: every stream's bytes replaced by another stream's (same sizes where they match)
+    bufC, offsC, sizesC = _gen.batch(_gen.C5, 9400, n, F, threads=4)
+    assert not np.array_equal(sizes, sizesC)
+    perm = np.roll(np.arange(n), 1)
+    same = sizes[perm] == sizes
+    for i in np.nonzero(same)[0]:
+        j = perm[i]
+        bufB[int(offs[i]):int(offs[i]) + int(sizes[i])] = bufA[int(offs[j]):int(offs[j]) + int(sizes[j])]
+    cases = [(bufA, offs, sizes), (bufB, offs, sizes), (bufC, offsC, sizesC)]
+    dec = mp3_amd.BatchDecoder(n, F)
+    for buf, o, z in cases:
+        d_in = torch.from_numpy(buf).cuda()
+        dec.reset()
+        got, gi = dec.decode(d_in, o, z, F)
+        ref_dec = mp3_amd.BatchDecoder(n, F)
+        ref, ri = ref_dec.decode(d_in, o, z, F)
+        ref_dec.close()
+        assert np.array_equal(gi, ri)
+        assert np.array_equal(got, ref)
+    dec.close()
