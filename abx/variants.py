@@ -569,6 +569,20 @@ VARS["ISR640"] = [("FLAGS", "-DMP3D_IS_ROW=640")]
 VARS["ISR608"] = [("FLAGS", "-DMP3D_IS_ROW=608")]
 # k_huffman without the count1 loop (output wrong): what the count1 tail costs
 VARS["NC1"] = [("                    while (k <= 572 && pos < end_bit) {", "                    while (k <= 572 && pos < end_bit && F < 0) {")]
+# k_mdcopy bound (output wrong): no payload word stores; no byte (head / tail / cut-short) stores;
+# payload words not loaded (stores of a constant)
+VARS["MDNS"] = [("""                    __builtin_amdgcn_raw_buffer_store_b128(
+                        __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v[j]), r_md,
+                        q < nq ? 4u * (wb + 4u * q) : 0x80000000u, 0, 0);""", """                    if (v[j].x == 0x12345679u) __builtin_amdgcn_raw_buffer_store_b128(
+                        __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v[j]), r_md,
+                        q < nq ? 4u * (wb + 4u * q) : 0x80000000u, 0, 0);""")]
+VARS["MDNB"] = [("""                if ((uint32_t)ql < h) dst[Pm + ql] = hbv;
+                if ((uint32_t)ql < L - t0) dst[Pm + t0 + ql] = tbv;""", """                if ((uint32_t)ql < h && hbv == 7) dst[Pm + ql] = hbv;
+                if ((uint32_t)ql < L - t0 && tbv == 7) dst[Pm + t0 + ql] = tbv;""")]
+VARS["MDNL"] = [("""                    uint4 a;
+                    __builtin_memcpy(&a, L, 16);
+                    const uint32_t e = L[4];""", """                    uint4 a = make_uint4(q, q + 1, q + 2, (uint32_t)(uintptr_t)L);
+                    const uint32_t e = q * 7u;""")]
 
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
