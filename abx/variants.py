@@ -583,6 +583,8 @@ VARS["MDNL"] = [("""                    uint4 a;
                     __builtin_memcpy(&a, L, 16);
                     const uint32_t e = L[4];""", """                    uint4 a = make_uint4(q, q + 1, q + 2, (uint32_t)(uintptr_t)L);
                     const uint32_t e = q * 7u;""")]
+VARS["RK8"] = [("#define RANK_PER 4      /* units per thread */", "#define RANK_PER 8")]
+VARS["RK16"] = [("#define RANK_PER 4      /* units per thread */", "#define RANK_PER 16")]
 
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
