@@ -1280,6 +1280,7 @@ static void dec_free(mp3d_dec *d) {
     delete d;
 }
 
+static void ra_worker(mp3d_dec *d);
 extern "C" int mp3d_dec_create_on(int device, mp3d_dec **out) {
     if (!out) return MP3D_E_ARG;
     *out = nullptr;
@@ -1353,6 +1354,16 @@ extern "C" int mp3d_dec_create_on(int device, mp3d_dec **out) {
             }
     } else {
         d->ra_max = 0;
+    }
+    /* the helper thread that launches the next run, started here: started
+     * on the first call that reads ahead past one run, its creation (tens of
+     * us) landed on that call's latency */
+    if (d->ra_max && d->ra_next_on && d->wk_on) {
+        try {
+            d->wk = std::thread(ra_worker, d);
+        } catch (...) {
+            d->wk_on = false; /* (the calling thread launches the next run) */
+        }
     }
     *out = d;
     return MP3D_OK;
