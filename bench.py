@@ -803,7 +803,9 @@ def report_decode(c, args, cfg, value, kt, frames_per_step):
                    "seed": c.seed if c.seed is not None else "default",
                    "parallelism": "streams sharded, 1 process per GPU, no data-path collective"},
         "roofline": {
-            "kernel": "k_synth", "bound": "valu-issue/latency", "roofline_class": "FP32 compute", "unit": "TFLOP/s",
+            "kernel": "k_synth", "bound": "mfma", "roofline_class": "FP32 compute", "unit": "TFLOP/s",
+            "bound_detail": "compute roofline at the dense FP32 peak (MFMA rate = vector rate); the kernel's limiter is "
+                            "VALU issue and dependent-chain latency (see limiter)",
             "achieved": achieved_tf, "peak": FP32_PEAK_TFLOPS, "frac": achieved_tf / FP32_PEAK_TFLOPS,
             "traffic": pmc.get("k_synth_hbm_bytes_per_launch"),
             "limiter": "FP32 compute roofline (vector rate = matrix rate, 157.3 TF); the PMC counters "
@@ -852,7 +854,8 @@ def report_c2(c, args, value, kt):
                    "seed": c.seed if c.seed is not None else "default",
                    "parallelism": "streams sharded, 1 process per GPU, no data-path collective"},
         "roofline": {
-            "kernel": "k_synth<xr>", "bound": "valu-issue/latency", "roofline_class": "FP32 compute",
+            "kernel": "k_synth<xr>", "bound": "mfma", "roofline_class": "FP32 compute",
+            "bound_detail": "compute roofline at the dense FP32 peak (MFMA rate = vector rate); VALU-issue limited",
             "unit": "TFLOP/s", "achieved": achieved_tf,
             "peak": FP32_PEAK_TFLOPS, "frac": achieved_tf / FP32_PEAK_TFLOPS,
             "traffic": pmc.get("k_synth_hbm_bytes_per_launch"),
