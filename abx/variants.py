@@ -585,6 +585,25 @@ VARS["MDNL"] = [("""                    uint4 a;
                     const uint32_t e = q * 7u;""")]
 VARS["RK8"] = [("#define RANK_PER 4      /* units per thread */", "#define RANK_PER 8")]
 VARS["RK16"] = [("#define RANK_PER 4      /* units per thread */", "#define RANK_PER 16")]
+# k_huffman: big_values groups stored two steps at a time (32 B, a whole sector, per lane)
+VARS["ST32"] = [("""                    for (; __ballot(k < bv2); k += 8) {
+                        uint32_t wv[4];""", """                    uint4 pend = make_uint4(0u, 0u, 0u, 0u);
+                    bool held = false;
+                    for (; __ballot(k < bv2); k += 8) {
+                        uint32_t wv[4];"""),
+    ("""                        *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+                    }
+                    k = bv2;""", """                        const uint4 cur = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+                        if (held) {
+                            *(uint4 *)(row + k - 8) = pend;
+                            *(uint4 *)(row + k) = cur;
+                        } else {
+                            pend = cur;
+                        }
+                        held = !held;
+                    }
+                    if (held) *(uint4 *)(row + k - 8) = pend;
+                    k = bv2;""")]
 
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):

@@ -235,6 +235,12 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                     int16_t *row = is_buf + (size_t)u * MP3D_IS_ROW;
                     int k = 0;
                     const uint32_t end_bit = start + seg + p23;
+                    /* stored two groups at a time: a lane writes 32 B (a whole
+                     * sector of its row's line) per store pair, not 16 B per
+                     * group -- a line evicted before the lane completes it then
+                     * holds only whole sectors (A/B ST32: -2.7 % k_huffman) */
+                    uint4 pend = make_uint4(0u, 0u, 0u, 0u);
+                    bool held = false;
                     for (; __ballot(k < bv2); k += 8) {
                         uint32_t wv[4];
 #pragma unroll
@@ -277,8 +283,16 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                             /* low halves of X and Y -> one word (v_perm_b32) */
                             wv[j] = live ? __builtin_amdgcn_perm((uint32_t)Y, (uint32_t)X, 0x05040100u) : 0u;
                         }
-                        *(uint4 *)(row + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+                        const uint4 cur = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+                        if (held) { /* (k is uniform: no divergence) */
+                            *(uint4 *)(row + k - 8) = pend;
+                            *(uint4 *)(row + k) = cur;
+                        } else {
+                            pend = cur;
+                        }
+                        held = !held;
                     }
+                    if (held) *(uint4 *)(row + k - 8) = pend; /* (before the count1 stores overwrite its tail) */
                     k = bv2;
                     /* count1 quadruples until the part2_3 end; a quadruple that
                      * overreads it is discarded (FFmpeg); lines
