@@ -604,6 +604,25 @@ VARS["ST32"] = [("""                    for (; __ballot(k < bv2); k += 8) {
                     }
                     if (held) *(uint4 *)(row + k - 8) = pend;
                     k = bv2;""")]
+# k_huffman: count1 groups stored in pairs too (32 B per lane every two iterations, 4-B aligned)
+VARS["C1P"] = [("""                    while (k <= 572 && pos < end_bit) {
+                        const uint32_t hw = win32g(bits, pos);""", """                    uint4 cpend = make_uint4(0u, 0u, 0u, 0u);
+                    int kpend = -1;
+                    while (k <= 572 && pos < end_bit) {
+                        const uint32_t hw = win32g(bits, pos);"""),
+    ("""                        __builtin_memcpy(row + k, &q, 16);
+                        k += 8;
+                    }""", """                        if (kpend >= 0) {
+                            __builtin_memcpy(row + kpend, &cpend, 16);
+                            __builtin_memcpy(row + k, &q, 16);
+                            kpend = -1;
+                        } else {
+                            cpend = q;
+                            kpend = k;
+                        }
+                        k += 8;
+                    }
+                    if (kpend >= 0) __builtin_memcpy(row + kpend, &cpend, 16);""")]
 
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
