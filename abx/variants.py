@@ -8,7 +8,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mp3_amd import _build  # noqa: E402
 
-KERNELS = ["mp3d_demux.hip", "mp3d_huffman.hip", "mp3d_synth.hip", "mp3d_demux_dev.h", "mp3d_huffman_dev.h"]
+KERNELS = ["mp3d_demux.hip", "mp3d_huffman.hip", "mp3d_synth.hip", "mp3d_demux_dev.h", "mp3d_huffman_dev.h", "mp3d_internal.h"]
 
 
 def variant(name, reps):
@@ -623,6 +623,42 @@ VARS["C1P"] = [("""                    while (k <= 572 && pos < end_bit) {
                         k += 8;
                     }
                     if (kpend >= 0) __builtin_memcpy(row + kpend, &cpend, 16);""")]
+# UnitMeta padded to 64 B; k_huffman writes it as two whole 32-B sectors (scalefactors 0..31 early,
+# scalefactors 32..39 + the tail + padding at the end; LSF units as before)
+VARS["MT64"] = [
+    ("""    uint16_t flags;      /* bit 0: granule lost to a reservoir underflow;  */
+                         /* bit 1: LSF intensity_scale (scalefac_compress  */
+                         /* bit 0 of an intensity frame's right channel)   */
+};""", """    uint16_t flags;      /* bit 0: granule lost to a reservoir underflow;  */
+                         /* bit 1: LSF intensity_scale (scalefac_compress  */
+                         /* bit 0 of an intensity frame's right channel)   */
+    uint32_t pad_[2];
+};"""),
+    ("""                        uint32_t sfw[10];
+#pragma unroll
+                        for (int i = 0; i < 10; i++) sfw[i] = 0u;""", """                        uint32_t sfw[10];
+#pragma unroll
+                        for (int i = 0; i < 10; i++) sfw[i] = 0u;"""),
+    ("""                        *(uint2 *)(mrec + 32) = make_uint2(sfw[8], sfw[9]);
+                    }""", """                        sf89 = make_uint2(sfw[8], sfw[9]);
+                    }"""),
+    ("""                    int lsf_pre = 0;
+                    if (r.lsf) {""", """                    int lsf_pre = 0;
+                    uint2 sf89 = make_uint2(0u, 0u);
+                    if (r.lsf) {"""),
+    ("""                    /* everything after sf[40]: one 16-B store */
+                    *(uint4 *)((uint8_t *)&meta[u] + 40) = *(const uint4 *)((const uint8_t *)&m + 40);""",
+     """                    {
+                        const uint4 t = *(const uint4 *)((const uint8_t *)&m + 40);
+                        uint8_t *mrec = (uint8_t *)&meta[u];
+                        if (r.lsf) {
+                            *(uint4 *)(mrec + 40) = t;
+                        } else {
+                            *(uint4 *)(mrec + 32) = make_uint4(sf89.x, sf89.y, t.x, t.y);
+                            *(uint4 *)(mrec + 48) = make_uint4(t.z, t.w, 0u, 0u);
+                        }
+                    }"""),
+]
 
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
