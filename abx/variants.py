@@ -660,6 +660,56 @@ VARS["MT64"] = [
                     }"""),
 ]
 
+
+# count1 tail without nested exec branches: both quadruples decoded every
+# iteration, their acceptance as selects (C1BF)
+VARS["C1BF"] = [("""                    while (k <= 572 && pos < end_bit) {
+                        const uint32_t hw = win32g(bits, pos);
+                        uint32_t se0, n0, se1, n1;
+                        c1_dec(hw, se0, n0);
+                        if (pos + n0 > end_bit) break;
+                        pos += n0;
+                        bool two = k <= 568 && pos < end_bit;
+                        if (two) {
+                            c1_dec(hw << n0, se1, n1);
+                            two = pos + n1 <= end_bit;
+                        }
+                        if (!two) {
+                            c1_store(k, se0);
+                            k += 4;
+                            break;
+                        }
+                        pos += n1;
+                        const uint4 q = make_uint4(
+                            __builtin_amdgcn_perm(se0, se0, 0x09030801u), __builtin_amdgcn_perm(se0 << 8, se0, 0x0B070A05u),
+                            __builtin_amdgcn_perm(se1, se1, 0x09030801u), __builtin_amdgcn_perm(se1 << 8, se1, 0x0B070A05u));
+                        __builtin_memcpy(row + k, &q, 16);
+                        k += 8;
+                    }""", """                    bool c1on = k <= 572 && pos < end_bit;
+                    while (__ballot(c1on)) {
+                        if (c1on) {
+                            const uint32_t hw = win32g(bits, pos);
+                            uint32_t se0, n0, se1, n1;
+                            c1_dec(hw, se0, n0);
+                            c1_dec(hw << n0, se1, n1);
+                            const uint32_t p1 = pos + n0, p2 = p1 + n1;
+                            const bool ok0 = p1 <= end_bit;
+                            const bool ok1 = ok0 && k <= 568 && p1 < end_bit && p2 <= end_bit;
+                            const uint2 q0 = make_uint2(__builtin_amdgcn_perm(se0, se0, 0x09030801u),
+                                                        __builtin_amdgcn_perm(se0 << 8, se0, 0x0B070A05u));
+                            if (ok1) {
+                                const uint4 q = make_uint4(q0.x, q0.y, __builtin_amdgcn_perm(se1, se1, 0x09030801u),
+                                                           __builtin_amdgcn_perm(se1 << 8, se1, 0x0B070A05u));
+                                __builtin_memcpy(row + k, &q, 16);
+                            } else if (ok0) {
+                                *(uint2 *)(row + k) = q0;
+                            }
+                            pos = ok1 ? p2 : (ok0 ? p1 : pos);
+                            k += ok1 ? 8 : (ok0 ? 4 : 0);
+                            c1on = ok1 && k <= 572 && pos < end_bit;
+                        }
+                    }""")]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
