@@ -710,6 +710,49 @@ VARS["C1BF"] = [("""                    while (k <= 572 && pos < end_bit) {
                         }
                     }""")]
 
+# compiler scheduling options (whole library): AMDGPU register-pressure trackers (TRK),
+# no unclustered high-pressure reschedule stage (DUH)
+VARS["TRK"] = [("FLAGS", "-mllvm"), ("FLAGS", "-amdgpu-use-amdgpu-trackers=1")]
+VARS["DUH"] = [("FLAGS", "-mllvm"), ("FLAGS", "-amdgpu-disable-unclustered-high-rp-reschedule")]
+
+# k_huffman big_values loop: the bit position carried negated (the window's
+# funnel shift takes it as is: no v_sub per pair) and the two signs applied as
+# one packed 16-bit xor / sub on the joined word (HMO)
+VARS["HMO"] = [
+    ("""                    uint4 pend = make_uint4(0u, 0u, 0u, 0u);
+                    bool held = false;
+                    for (; __ballot(k < bv2); k += 8) {""", """                    uint4 pend = make_uint4(0u, 0u, 0u, 0u);
+                    bool held = false;
+                    uint32_t npos = 0u - pos;
+                    const int nend = -(int)end_bit;
+                    for (; __ballot(k < bv2); k += 8) {"""),
+    ("""                            uint32_t hi, lo;
+                            win64g(bits, pos, hi, lo);""", """                            uint32_t hi, lo;
+                            {
+                                uint32_t w = (31u - npos) >> 5;
+                                __asm__("" : "+v"(w));
+                                const uint32_t w0 = bits[(int)w - 1], w1 = bits[w], w2 = bits[w + 1];
+                                hi = __builtin_amdgcn_alignbit(w0, w1, npos);
+                                lo = __builtin_amdgcn_alignbit(w1, w2, npos);
+                            }"""),
+    ("""                            const bool live = kk < bv2 && pos < end_bit;
+                            pos += live ? len_c + (32u - t3) : 0u;
+                            /* x = 0 gives X = 0 whatever the (absent) sign bit */
+                            const int X = ((int)(x + ex) ^ mx) - mx, Y = ((int)(y + ey) ^ my) - my;
+                            /* low halves of X and Y -> one word (v_perm_b32) */
+                            wv[j] = live ? __builtin_amdgcn_perm((uint32_t)Y, (uint32_t)X, 0x05040100u) : 0u;""",
+     """                            const bool live = kk < bv2 && (int)npos > nend;
+                            npos += live ? t3 - (((e >> 8) & 31u) | 32u) : 0u;
+                            const uint32_t axy = __builtin_amdgcn_perm(y + ey, x + ex, 0x05040100u);
+                            const uint32_t mxy = __builtin_amdgcn_perm((uint32_t)my, (uint32_t)mx, 0x05040100u);
+                            uint32_t sxy;
+                            __asm__("v_pk_sub_u16 %0, %1, %2" : "=v"(sxy) : "v"(axy ^ mxy), "v"(mxy));
+                            wv[j] = live ? sxy : 0u;"""),
+    ("""                    if (held) *(uint4 *)(row + k - 8) = pend; /* (before the count1 stores overwrite its tail) */""",
+     """                    pos = 0u - npos;
+                    if (held) *(uint4 *)(row + k - 8) = pend; /* (before the count1 stores overwrite its tail) */"""),
+]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
