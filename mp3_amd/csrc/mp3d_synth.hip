@@ -1484,9 +1484,18 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
         int F, int xr_nch, int xr_sr, int seg_len, float *__restrict__ st_tail,
         const float *__restrict__ st_tail_in, const uint32_t *__restrict__ fam, uint32_t seq) {
     constexpr int SYN_WAVES = SynCfg<SRC_XR, LSF>::WAVES;
-    __shared__ __attribute__((aligned(16))) SynShared<LSF> T;
-    __shared__ SynWave Wv[SYN_WAVES];
-    __shared__ __attribute__((aligned(16))) uint32_t s_isq[SynCfg<SRC_XR, LSF>::DMA ? SYN_WAVES : 1][2 * 320];
+    /* one LDS object, the shared tables first: as separate variables the
+     * compiler placed the tables last, above 64 KB, where no table address
+     * fits a DS instruction's 16-bit offset (a v_add per table read) */
+    struct Lds {
+        SynShared<LSF> T;
+        SynWave Wv[SYN_WAVES];
+        uint32_t isq[SynCfg<SRC_XR, LSF>::DMA ? SYN_WAVES : 1][2 * 320];
+    };
+    __shared__ __attribute__((aligned(16))) Lds L;
+    SynShared<LSF> &T = L.T;
+    SynWave *Wv = L.Wv;
+    auto &s_isq = L.isq;
     /* LSF variant of a batch decode (fam given): k_walk tagged the family
      * word with this call's seq if any stream is LSF; otherwise the whole
      * (small, persistent) grid leaves at once.  With LSF streams each
