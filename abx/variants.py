@@ -753,6 +753,24 @@ VARS["HMO"] = [
                     if (held) *(uint4 *)(row + k - 8) = pend; /* (before the count1 stores overwrite its tail) */"""),
 ]
 
+# k_synth phase Q: the scale address as one v_and_or_b32 (0xFC in a VGPR: VOP3 takes no literal on
+# gfx9, so the compiler split it into v_and + v_or); the fused path's alias neighbours by DPP moves with
+# no old value (update_dpp(0, ..) cost a v_mov of 0 per neighbour) (MQ1)
+VARS["MQ1"] = [
+    ("""                const uint8_t *p43b = (const uint8_t *)T.p43s;""",
+     """                const uint8_t *p43b = (const uint8_t *)T.p43s;
+                uint32_t kfc = 0xFCu; /* in a VGPR: the scale address below is one v_and_or_b32 */
+                __asm__ volatile("" : "+v"(kfc));"""),
+    ("""                        const float sc = *(lds_cf32 *)(uintptr_t)(scb | (tv2 & 0xFCu));""",
+     """                        const float sc = *(lds_cf32 *)(uintptr_t)(scb | (tv2 & kfc));"""),
+    ("""                        const float sc = *(lds_cf32 *)(uintptr_t)(sc_base[c] | (tv2 & 0xFCu));""",
+     """                        const float sc = *(lds_cf32 *)(uintptr_t)(sc_base[c] | (tv2 & kfc));"""),
+    ("""                        up[k] = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(xf[17 - k]), 0x138, 0xF, 0xF, false));
+                        dn[k] = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(xf[k]), 0x130, 0xF, 0xF, false));""",
+     """                        up[k] = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(xf[17 - k]), 0x138, 0xF, 0xF, true));
+                        dn[k] = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(xf[k]), 0x130, 0xF, 0xF, true));"""),
+]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
