@@ -771,6 +771,46 @@ VARS["MQ1"] = [
                         dn[k] = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(xf[k]), 0x130, 0xF, 0xF, true));"""),
 ]
 
+# k_huffman big_values rows stored 64 B (four groups) at a time: a lane completes half a line per
+# store burst (ST64)
+VARS["ST64"] = [
+    ("""                    uint4 pend = make_uint4(0u, 0u, 0u, 0u);
+                    bool held = false;""", """                    uint4 pend = make_uint4(0u, 0u, 0u, 0u), pend1 = pend, pend2 = pend;
+                    int held = 0;"""),
+    ("""                        const uint4 cur = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+                        if (held) { /* (k is uniform: no divergence) */
+                            *(uint4 *)(row + k - 8) = pend;
+                            *(uint4 *)(row + k) = cur;
+                        } else {
+                            pend = cur;
+                        }
+                        held = !held;""", """                        const uint4 cur = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+                        if (held == 3) { /* (k is uniform: no divergence) */
+                            *(uint4 *)(row + k - 24) = pend;
+                            *(uint4 *)(row + k - 16) = pend1;
+                            *(uint4 *)(row + k - 8) = pend2;
+                            *(uint4 *)(row + k) = cur;
+                        } else if (held == 2) {
+                            pend2 = cur;
+                        } else if (held == 1) {
+                            pend1 = cur;
+                        } else {
+                            pend = cur;
+                        }
+                        held = (held + 1) & 3;"""),
+    ("""                    if (held) *(uint4 *)(row + k - 8) = pend; /* (before the count1 stores overwrite its tail) */""",
+     """                    if (held == 3) {
+                        *(uint4 *)(row + k - 24) = pend;
+                        *(uint4 *)(row + k - 16) = pend1;
+                        *(uint4 *)(row + k - 8) = pend2;
+                    } else if (held == 2) {
+                        *(uint4 *)(row + k - 16) = pend;
+                        *(uint4 *)(row + k - 8) = pend1;
+                    } else if (held == 1) {
+                        *(uint4 *)(row + k - 8) = pend;
+                    }"""),
+]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
