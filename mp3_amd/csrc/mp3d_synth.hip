@@ -1492,6 +1492,8 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
         SynWave Wv[SYN_WAVES];
         uint32_t isq[SynCfg<SRC_XR, LSF>::DMA ? SYN_WAVES : 1][2 * 320];
     };
+    /* two MPEG-1 workgroups per CU (4 waves per SIMD): <= half of the CU's 160 KB */
+    static_assert(LSF || SRC_XR || sizeof(Lds) <= 160 * 1024 / 2, "k_synth: LDS for two workgroups per CU");
     __shared__ __attribute__((aligned(16))) Lds L;
     SynShared<LSF> &T = L.T;
     SynWave *Wv = L.Wv;
