@@ -1484,14 +1484,18 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
         int F, int xr_nch, int xr_sr, int seg_len, float *__restrict__ st_tail,
         const float *__restrict__ st_tail_in, const uint32_t *__restrict__ fam, uint32_t seq) {
     constexpr int SYN_WAVES = SynCfg<SRC_XR, LSF>::WAVES;
-    /* one LDS object, the shared tables first: as separate variables the
-     * compiler placed the tables last, above 64 KB, where no table address
-     * fits a DS instruction's 16-bit offset (a v_add per table read) */
+    /* one LDS object in a fixed order: the per-wave buffers at 0 (their
+     * row offsets then fit ds_read2's 8-bit offsets from the wave's base),
+     * the shared tables next and below 64 KB (every table address fits a
+     * DS instruction's 16-bit offset; as separate variables the compiler
+     * placed them last, above 64 KB: a v_add per table read), the is[]
+     * prefetch areas last */
     struct Lds {
-        SynShared<LSF> T;
         SynWave Wv[SYN_WAVES];
+        SynShared<LSF> T;
         uint32_t isq[SynCfg<SRC_XR, LSF>::DMA ? SYN_WAVES : 1][2 * 320];
     };
+    static_assert(offsetof(Lds, T) + sizeof(SynShared<LSF>) <= 65536, "k_synth: tables within DS offset reach");
     /* two MPEG-1 workgroups per CU (4 waves per SIMD): <= half of the CU's 160 KB */
     static_assert(LSF || SRC_XR || sizeof(Lds) <= 160 * 1024 / 2, "k_synth: LDS for two workgroups per CU");
     __shared__ __attribute__((aligned(16))) Lds L;
