@@ -811,6 +811,35 @@ VARS["ST64"] = [
                     }"""),
 ]
 
+# k_synth phase W: the shifted B pairs xbp[m] = (row 2m+1, row 2m+2) loaded by ds_read2_b32 straight
+# into aligned register pairs (inline asm, three bases) -- the compiler paired the rows (2m, 2m+1)
+# and shuffled them with 14 v_mov per granule (WXB)
+VARS["WXB"] = [
+    ("""#pragma unroll
+                for (int m = 0; m < 8; m++) xbp[m] = (f32x2){sBuf[pb + (2 * m + 1) * XROW], sBuf[pb + (2 * m + 2) * XROW]};""",
+     """                {
+                    static_assert(XROW == 36, "WXB offsets");
+                    const uint32_t ba = (uint32_t)(uintptr_t)(lds_cf32 *)&sBuf[pb];
+                    const uint32_t bb = ba + 7u * 4u * XROW, bc2 = ba + 15u * 4u * XROW;
+                    __asm__ volatile("ds_read2_b32 %0, %1 offset0:36 offset1:72" : "=v"(xbp[0]) : "v"(ba));
+                    __asm__ volatile("ds_read2_b32 %0, %1 offset0:108 offset1:144" : "=v"(xbp[1]) : "v"(ba));
+                    __asm__ volatile("ds_read2_b32 %0, %1 offset0:180 offset1:216" : "=v"(xbp[2]) : "v"(ba));
+                    __asm__ volatile("ds_read2_b32 %0, %1 offset0:0 offset1:36" : "=v"(xbp[3]) : "v"(bb));
+                    __asm__ volatile("ds_read2_b32 %0, %1 offset0:72 offset1:108" : "=v"(xbp[4]) : "v"(bb));
+                    __asm__ volatile("ds_read2_b32 %0, %1 offset0:144 offset1:180" : "=v"(xbp[5]) : "v"(bb));
+                    __asm__ volatile("ds_read2_b32 %0, %1 offset0:216 offset1:252" : "=v"(xbp[6]) : "v"(bb));
+                    __asm__ volatile("ds_read2_b32 %0, %1 offset0:0 offset1:36" : "=v"(xbp[7]) : "v"(bc2));
+                }"""),
+    ("""                xb0 = sBuf[pb];
+                xb17 = sBuf[pb + 17 * XROW];""",
+     """                xb0 = sBuf[pb];
+                xb17 = sBuf[pb + 17 * XROW];
+                /* the asm loads land before any use: the wait carries them */
+                __asm__ volatile("s_waitcnt lgkmcnt(0)"
+                                 : "+v"(xbp[0]), "+v"(xbp[1]), "+v"(xbp[2]), "+v"(xbp[3]), "+v"(xbp[4]), "+v"(xbp[5]),
+                                   "+v"(xbp[6]), "+v"(xbp[7]));"""),
+]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])

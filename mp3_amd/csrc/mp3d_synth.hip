@@ -1288,10 +1288,31 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                 float xb0, xb17;
 #pragma unroll
                 for (int m = 0; m < 9; m++) xap[m] = (f32x2){sBuf[pa + 2 * m * XROW], sBuf[pa + (2 * m + 1) * XROW]};
-#pragma unroll
-                for (int m = 0; m < 8; m++) xbp[m] = (f32x2){sBuf[pb + (2 * m + 1) * XROW], sBuf[pb + (2 * m + 2) * XROW]};
+                {
+                    /* the shifted pairs (rows 2m + 1, 2m + 2) by ds_read2_b32
+                     * straight into aligned register pairs, from three bases
+                     * (offsets <= 255 words): as C the compiler paired rows
+                     * (2m, 2m + 1) and rebuilt the pairs with 14 v_mov per
+                     * granule (A/B WXB: -1 % k_synth, bit-identical) */
+                    static_assert(XROW == 36, "xbp offsets below assume 36-word X rows");
+                    const uint32_t ba = (uint32_t)(uintptr_t)(lds_cf32 *)&sBuf[pb];
+                    const uint32_t bb = ba + 7u * 4u * XROW, bz = ba + 15u * 4u * XROW;
+                    __asm__ volatile("ds_read2_b32 %0, %1 offset0:36 offset1:72" : "=v"(xbp[0]) : "v"(ba));
+                    __asm__ volatile("ds_read2_b32 %0, %1 offset0:108 offset1:144" : "=v"(xbp[1]) : "v"(ba));
+                    __asm__ volatile("ds_read2_b32 %0, %1 offset0:180 offset1:216" : "=v"(xbp[2]) : "v"(ba));
+                    __asm__ volatile("ds_read2_b32 %0, %1 offset0:0 offset1:36" : "=v"(xbp[3]) : "v"(bb));
+                    __asm__ volatile("ds_read2_b32 %0, %1 offset0:72 offset1:108" : "=v"(xbp[4]) : "v"(bb));
+                    __asm__ volatile("ds_read2_b32 %0, %1 offset0:144 offset1:180" : "=v"(xbp[5]) : "v"(bb));
+                    __asm__ volatile("ds_read2_b32 %0, %1 offset0:216 offset1:252" : "=v"(xbp[6]) : "v"(bb));
+                    __asm__ volatile("ds_read2_b32 %0, %1 offset0:0 offset1:36" : "=v"(xbp[7]) : "v"(bz));
+                }
                 xb0 = sBuf[pb];
                 xb17 = sBuf[pb + 17 * XROW];
+                /* the compiler does not count the asm loads: this wait, with
+                 * the pairs as its operands, orders every use after them */
+                __asm__ volatile("s_waitcnt lgkmcnt(0)"
+                                 : "+v"(xbp[0]), "+v"(xbp[1]), "+v"(xbp[2]), "+v"(xbp[3]), "+v"(xbp[4]), "+v"(xbp[5]),
+                                   "+v"(xbp[6]), "+v"(xbp[7]));
                 /* mono frame: channel 1 keeps its synthesis history.  Its
                  * lanes park their partial sums in the channel-1 half of the
                  * X buffer (rows 18..35, which only channel-1 lanes read, and
