@@ -840,6 +840,60 @@ VARS["WXB"] = [
                                    "+v"(xbp[6]), "+v"(xbp[7]));"""),
 ]
 
+# timing probe (same output): per-phase shader-clock totals of one wave (block 0 / 4000, wave 0),
+# printed at the stream's end (PHT)
+VARS["PHT"] = [
+    ("    float *const sBuf = Wd.buf;\n",
+     "    float *const sBuf = Wd.buf;\n    unsigned long long ph_[4] = {0ull, 0ull, 0ull, 0ull}, tQ_ = 0ull, tI_ = 0ull, tM_ = 0ull, tW_ = 0ull;\n"),
+    (_QS, "            tQ_ = clock64();\n" + _QS),
+    (_IS, "            tI_ = clock64(); ph_[0] += tI_ - tQ_;\n" + _IS),
+    (_MS, "            tM_ = clock64(); ph_[1] += tM_ - tI_;\n" + _MS),
+    (_WS, "            tW_ = clock64(); ph_[2] += tW_ - tM_;\n" + _WS),
+    ("            wave_sync(); /* X reads done before the next granule's xr */",
+     "            wave_sync(); /* X reads done before the next granule's xr */\n            ph_[3] += clock64() - tW_;"),
+    ("    if (f1 == F && PF != 1) {",
+     "    if ((blockIdx.x == 0 || blockIdx.x == 4000) && threadIdx.x == 0 && !SRC_XR && !LSF)\n"
+     "        printf(\"PHT blk %d Q %llu I %llu M %llu W %llu\\n\", (int)blockIdx.x, ph_[0], ph_[1], ph_[2], ph_[3]);\n"
+     "    if (f1 == F && PF != 1) {"),
+]
+
+# PHT with phase Q split: Q1 band scales (to their wave_sync), Q2 requantise + stereo + scatter,
+# Q3 xin + prefetch issue; G = end of W to the next Q (PHT2)
+VARS["PHT2"] = [
+    ("    float *const sBuf = Wd.buf;\n",
+     "    float *const sBuf = Wd.buf;\n    unsigned long long ph_[8] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull}, tQ_ = 0ull, tI_ = 0ull, tM_ = 0ull, tW_ = 0ull, tE_ = 0ull, t1_ = 0ull, t2_ = 0ull;\n"),
+    (_QS, "            tQ_ = clock64(); if (tE_) ph_[7] += tQ_ - tE_;\n" + _QS),
+    ("                (void)m12a;\n", "                (void)m12a;\n                t1_ = clock64(); ph_[4] += t1_ - tQ_;\n"),
+    ("                xin();\n                } /* !fusedq */", "                t2_ = clock64(); ph_[5] += t2_ - t1_;\n                xin();\n                } /* !fusedq */"),
+    (_IS, "            tI_ = clock64(); ph_[0] += tI_ - tQ_; ph_[6] += tI_ - t2_;\n" + _IS),
+    (_MS, "            tM_ = clock64(); ph_[1] += tM_ - tI_;\n" + _MS),
+    (_WS, "            tW_ = clock64(); ph_[2] += tW_ - tM_;\n" + _WS),
+    ("            wave_sync(); /* X reads done before the next granule's xr */",
+     "            wave_sync(); /* X reads done before the next granule's xr */\n            tE_ = clock64(); ph_[3] += tE_ - tW_;"),
+    ("    if (f1 == F && PF != 1) {",
+     "    if ((blockIdx.x == 0 || blockIdx.x == 4000) && threadIdx.x == 0 && !SRC_XR && !LSF)\n"
+     "        printf(\"PHT2 blk %d Q %llu (Q1 %llu Q2 %llu Q3 %llu) I %llu M %llu W %llu G %llu\\n\", (int)blockIdx.x, ph_[0], ph_[4], ph_[5], ph_[6], ph_[1], ph_[2], ph_[3], ph_[7]);\n"
+     "    if (f1 == F && PF != 1) {"),
+]
+
+# PHT2 with Q2 split: Qa read_cis, Qb requant, Qc escape check + stereo, Qd scatter (PHT3)
+VARS["PHT3"] = [
+    ("    float *const sBuf = Wd.buf;\n",
+     "    float *const sBuf = Wd.buf;\n    unsigned long long ph_[8] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull}, tQ_ = 0ull, t1_ = 0ull, ta_ = 0ull, tb_ = 0ull, tc_ = 0ull;\n"),
+    ("                (void)m12a;\n", "                (void)m12a;\n                t1_ = clock64();\n"),
+    ("                else read_cis(std::integral_constant<int, 5>{});\n",
+     "                else read_cis(std::integral_constant<int, 5>{});\n                __asm__ volatile(\"s_waitcnt lgkmcnt(0)\" : \"+v\"(cis[0][0]), \"+v\"(cis[1][0]), \"+v\"(cis[0][1]), \"+v\"(cis[1][1]));\n                ta_ = clock64(); ph_[0] += ta_ - t1_;\n"),
+    ("                else requant(std::integral_constant<int, 5>{});\n",
+     "                else requant(std::integral_constant<int, 5>{});\n                __asm__ volatile(\"s_waitcnt lgkmcnt(0)\" : \"+v\"(xp[0][0]), \"+v\"(xp[1][0]));\n                tb_ = clock64(); ph_[1] += tb_ - ta_;\n"),
+    ("                if (ms_fold) {\n",
+     "                tc_ = clock64(); ph_[2] += tc_ - tb_;\n                if (ms_fold) {\n"),
+    ("                xin();\n                } /* !fusedq */", "                ph_[3] += clock64() - tc_;\n                xin();\n                } /* !fusedq */"),
+    ("    if (f1 == F && PF != 1) {",
+     "    if ((blockIdx.x == 0 || blockIdx.x == 4000) && threadIdx.x == 0 && !SRC_XR && !LSF)\n"
+     "        printf(\"PHT3 blk %d cis %llu requant %llu esc+stereo %llu scatter %llu\\n\", (int)blockIdx.x, ph_[0], ph_[1], ph_[2], ph_[3]);\n"
+     "    if (f1 == F && PF != 1) {"),
+]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
