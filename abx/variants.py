@@ -894,6 +894,20 @@ VARS["PHT3"] = [
      "    if (f1 == F && PF != 1) {"),
 ]
 
+# k_synth M/S scatter: chunks at or past nlive (all-zero lines) stored as zeros without the
+# sum / difference (MSZ)
+VARS["MSZ"] = [
+    ("""                            scatter(i, 0, xp[0][i] + xp[1][i]);
+                            scatter(i, 1, xp[0][i] - xp[1][i]);""",
+     """                            if (i < 2 || i < nlive) {
+                                scatter(i, 0, xp[0][i] + xp[1][i]);
+                                scatter(i, 1, xp[0][i] - xp[1][i]);
+                            } else {
+                                scatter(i, 0, (f32x2){0.f, 0.f});
+                                scatter(i, 1, (f32x2){0.f, 0.f});
+                            }"""),
+]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
