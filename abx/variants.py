@@ -908,6 +908,71 @@ VARS["MSZ"] = [
                             }"""),
 ]
 
+# k_synth phase M: the lane's S / X row offsets (two byte offsets, lane constants) computed once
+# before the frame loop; the per-granule addresses are the wave's buffer base plus them, the row
+# steps immediate offsets (MH)
+VARS["MH"] = [
+    ("    for (int f = fw; f < f1; f++) {\n        int nch, sr, mode = 0, mext = 0;",
+     "    const int mlane_ = (int)(threadIdx.x & 63);\n"
+     "    const uint32_t m_off_a = (uint32_t)(((mlane_ & 15) * SROW + 4 * (mlane_ >> 4)) * 4);\n"
+     "    const uint32_t m_off_c = (uint32_t)((((mlane_ & 15) < 4 ? 32 + (mlane_ & 15) : 35) * SROW + 4 * (mlane_ >> 4)) * 4);\n"
+     "    for (int f = fw; f < f1; f++) {\n        int nch, sr, mode = 0, mext = 0;"),
+    ("""#pragma unroll
+                for (int nt = 0; nt < 3; nt++) {
+                    int n = 16 * nt + r16;
+                    n = n < 36 ? n : 35;
+                    const f32x4 a4 = *(const f32x4 *)&sBuf[n * SROW + 4 * q];
+                    const f32x4 b4 = *(const f32x4 *)&sBuf[n * SROW + 16 + 4 * q]; /* S[31 - 4 q - ks] */""",
+     """                typedef __attribute__((address_space(3))) f32x4 lds_f32x4;
+                const uint32_t sbase_ = (uint32_t)(uintptr_t)(lds_cf32 *)(const float *)sBuf;
+                lds_f32x4 *const pA = (lds_f32x4 *)(uintptr_t)(sbase_ + m_off_a);
+                lds_f32x4 *const pC = (lds_f32x4 *)(uintptr_t)(sbase_ + m_off_c);
+#pragma unroll
+                for (int nt = 0; nt < 3; nt++) {
+                    lds_f32x4 *const pr = nt == 2 ? pC : pA + nt * (16 * SROW / 4);
+                    const f32x4 a4 = pr[0];
+                    const f32x4 b4 = pr[4]; /* S[31 - 4 q - ks] */"""),
+    ("""#pragma unroll
+                for (int nt = 0; nt < 3; nt++) {
+                    const int n = 16 * nt + r16;
+                    if (n < 36) {
+                        *(f32x4 *)&sBuf[n * XROW + 4 * q] = ce[nt];
+                        *(f32x4 *)&sBuf[n * XROW + 16 + 4 * q] = co[nt];
+                    }
+                }""",
+     """                static_assert(XROW == SROW, "X rows reuse the S row offsets");
+#pragma unroll
+                for (int nt = 0; nt < 3; nt++) {
+                    const int n = 16 * nt + r16;
+                    if (n < 36) {
+                        lds_f32x4 *const pr = nt == 2 ? pC : pA + nt * (16 * XROW / 4);
+                        pr[0] = ce[nt];
+                        pr[4] = co[nt];
+                    }
+                }"""),
+]
+
+# MH plus the S-row write offset and the A fragments' table offset hoisted the same way (MH2)
+VARS["MH2"] = [
+    (VARS["MH"][0][0], VARS["MH"][0][1].replace(
+        "    for (int f = fw; f < f1; f++) {",
+        "    const uint32_t m_off_s = (uint32_t)((18 * (mlane_ >> 5) * SROW + ((mlane_ & 31) < 16 ? (mlane_ & 31) : 47 - (mlane_ & 31))) * 4);\n"
+        "    const uint32_t m_off_e = (uint32_t)(((mlane_ & 15) * 16 + 4 * (mlane_ >> 4)) * 4);\n"
+        "    for (int f = fw; f < f1; f++) {")),
+    ("""                const int sw = opaque(18 * ch * SROW + (sb < 16 ? sb : 47 - sb));
+#pragma unroll
+                for (int t = 0; t < 18; t++) sBuf[sw + t * SROW] = o18[t]; /* frequency inversion already in */""",
+     """                typedef __attribute__((address_space(3))) float lds_f32;
+                lds_f32 *const ps = (lds_f32 *)(uintptr_t)((uint32_t)(uintptr_t)(lds_cf32 *)(const float *)sBuf + m_off_s);
+#pragma unroll
+                for (int t = 0; t < 18; t++) ps[t * SROW] = o18[t]; /* frequency inversion already in */"""),
+    ("""                const float4 ae = *(const float4 *)&T.ce[r16][4 * q];
+                const float4 ao = *(const float4 *)&T.co[r16][4 * q];""",
+     """                typedef __attribute__((address_space(3))) const f32x4 lds_cf4;
+                const f32x4 ae = *(lds_cf4 *)(uintptr_t)((uint32_t)(uintptr_t)(lds_cf32 *)&T.ce[0][0] + m_off_e);
+                const f32x4 ao = *(lds_cf4 *)(uintptr_t)((uint32_t)(uintptr_t)(lds_cf32 *)&T.co[0][0] + m_off_e);"""),
+] + VARS["MH"][1:]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])

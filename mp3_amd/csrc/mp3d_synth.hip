@@ -646,6 +646,13 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
         WAIT_VMCNT0();
     }
 
+    /* phase M's S / X row offsets of this lane (lane constants, held across
+     * the loop: recomputed from the lane id they cost 14 VALU a granule; A/B
+     * MH -0.9 % k_synth): row block 0 / 1 at m_off_a (+ 16 rows), block 2
+     * (rows 32..35, clamped) at m_off_c */
+    const int mlane_ = (int)(threadIdx.x & 63);
+    const uint32_t m_off_a = (uint32_t)(((mlane_ & 15) * SROW + 4 * (mlane_ >> 4)) * 4);
+    const uint32_t m_off_c = (uint32_t)((((mlane_ & 15) < 4 ? 32 + (mlane_ & 15) : 35) * SROW + 4 * (mlane_ >> 4)) * 4);
     for (int f = fw; f < f1; f++) {
         int nch, sr, mode = 0, mext = 0;
         const size_t fr = (size_t)s * F + f;
@@ -1225,12 +1232,15 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                 const float4 ao = *(const float4 *)&T.co[r16][4 * q];
                 const float Ae[4] = {ae.x, ae.y, ae.z, ae.w}, Ao[4] = {ao.x, ao.y, ao.z, ao.w};
                 float Be[3][4], Bo[3][4];
+                typedef __attribute__((address_space(3))) f32x4 lds_f32x4;
+                const uint32_t sbase_ = (uint32_t)(uintptr_t)(lds_cf32 *)(const float *)sBuf;
+                lds_f32x4 *const pA = (lds_f32x4 *)(uintptr_t)(sbase_ + m_off_a);
+                lds_f32x4 *const pC = (lds_f32x4 *)(uintptr_t)(sbase_ + m_off_c);
 #pragma unroll
                 for (int nt = 0; nt < 3; nt++) {
-                    int n = 16 * nt + r16;
-                    n = n < 36 ? n : 35;
-                    const f32x4 a4 = *(const f32x4 *)&sBuf[n * SROW + 4 * q];
-                    const f32x4 b4 = *(const f32x4 *)&sBuf[n * SROW + 16 + 4 * q]; /* S[31 - 4 q - ks] */
+                    lds_f32x4 *const pr = nt == 2 ? pC : pA + nt * (16 * SROW / 4);
+                    const f32x4 a4 = pr[0];
+                    const f32x4 b4 = pr[4]; /* S[31 - 4 q - ks] */
                     const f32x2 e01 = pfma(bc(1.f), a4.xy, b4.xy), e23 = pfma(bc(1.f), a4.zw, b4.zw);
                     const f32x2 o01 = pfma(bc(-1.f), b4.xy, a4.xy), o23 = pfma(bc(-1.f), b4.zw, a4.zw);
                     Be[nt][0] = e01.x; Be[nt][1] = e01.y; Be[nt][2] = e23.x; Be[nt][3] = e23.y;
@@ -1249,12 +1259,14 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                 wave_sync(); /* all S reads retired before X overwrites them */
                 /* D[row m = 4 q + r][col n]: X[n][2m] (even) at row n, 4 q + r;
                  * X[n][2m+1] (odd) at 16 + 4 q + r -- one 16-B store each */
+                static_assert(XROW == SROW, "X rows reuse the S row offsets");
 #pragma unroll
                 for (int nt = 0; nt < 3; nt++) {
                     const int n = 16 * nt + r16;
                     if (n < 36) {
-                        *(f32x4 *)&sBuf[n * XROW + 4 * q] = ce[nt];
-                        *(f32x4 *)&sBuf[n * XROW + 16 + 4 * q] = co[nt];
+                        lds_f32x4 *const pr = nt == 2 ? pC : pA + nt * (16 * XROW / 4);
+                        pr[0] = ce[nt];
+                        pr[4] = co[nt];
                     }
                 }
             }
