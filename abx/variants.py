@@ -973,6 +973,44 @@ VARS["MH2"] = [
                 const f32x4 ao = *(lds_cf4 *)(uintptr_t)((uint32_t)(uintptr_t)(lds_cf32 *)&T.co[0][0] + m_off_e);"""),
 ] + VARS["MH"][1:]
 
+# xin from one lane-constant address (8 words below the lane's lines; held across the loop) with
+# every read an immediate offset: the boundary subbands read a neighbour's words they do not use
+# instead of selecting their own; a 256-B pad keeps wave 0's look-back inside the LDS object (XIN)
+VARS["XIN"] = [
+    ("""    struct Lds {
+        SynWave Wv[SYN_WAVES];""", """    struct Lds {
+        float pad_[64]; /* xin's look-back of wave 0, subband 0 (words it does not use) */
+        SynWave Wv[SYN_WAVES];"""),
+    ("    const int mlane_ = (int)(threadIdx.x & 63);\n",
+     "    const int mlane_ = (int)(threadIdx.x & 63);\n"
+     "    const uint32_t xin_off = (uint32_t)(((mlane_ >> 5) * 576 + 18 * (mlane_ & 31) - 8) * 4);\n"),
+    ("""                const int lx = opaque((int)(threadIdx.x & 63));
+                const int base = (lx >> 5) * 576 + 18 * (lx & 31), sbx = lx & 31;
+#pragma unroll
+                for (int i = 0; i < 9; i++) {
+                    const float2 v = *(const float2 *)&sBuf[base + 2 * i];
+                    xf[2 * i] = v.x;
+                    xf[2 * i + 1] = v.y;
+                }
+                const int pb = sbx ? base - 8 : base, nb = sbx < 31 ? base + 18 : base;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const float2 p = *(const float2 *)&sBuf[pb + 2 * i];
+                    const float2 n = *(const float2 *)&sBuf[nb + 2 * i];""",
+     """                typedef __attribute__((address_space(3))) const f32x2 lds_cf2;
+                lds_cf2 *const P = (lds_cf2 *)(uintptr_t)((uint32_t)(uintptr_t)(lds_cf32 *)(const float *)sBuf + xin_off);
+#pragma unroll
+                for (int i = 0; i < 9; i++) {
+                    const f32x2 v = P[4 + i];
+                    xf[2 * i] = v.x;
+                    xf[2 * i + 1] = v.y;
+                }
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const f32x2 p = P[i];
+                    const f32x2 n = P[13 + i];"""),
+]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])

@@ -651,6 +651,11 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
      * MH -0.9 % k_synth): row block 0 / 1 at m_off_a (+ 16 rows), block 2
      * (rows 32..35, clamped) at m_off_c */
     const int mlane_ = (int)(threadIdx.x & 63);
+    /* xin's one read address: 8 words below the lane's 18 lines (the previous
+     * subband's last 8), every read an immediate offset from it; subbands 0
+     * and 31 read neighbour words they do not use (the LDS objects have a pad
+     * below wave 0's buffer) instead of selecting their own (A/B XIN) */
+    const uint32_t xin_off = (uint32_t)(((mlane_ >> 5) * 576 + 18 * (mlane_ & 31) - 8) * 4);
     const uint32_t m_off_a = (uint32_t)(((mlane_ & 15) * SROW + 4 * (mlane_ >> 4)) * 4);
     const uint32_t m_off_c = (uint32_t)((((mlane_ & 15) < 4 ? 32 + (mlane_ & 15) : 35) * SROW + 4 * (mlane_ >> 4)) * 4);
     for (int f = fw; f < f1; f++) {
@@ -706,19 +711,18 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
              * across the scatter paths' registers and spilled) */
             auto xin = [&]() {
                 wave_sync();
-                const int lx = opaque((int)(threadIdx.x & 63));
-                const int base = (lx >> 5) * 576 + 18 * (lx & 31), sbx = lx & 31;
+                typedef __attribute__((address_space(3))) const f32x2 lds_cf2;
+                lds_cf2 *const P = (lds_cf2 *)(uintptr_t)((uint32_t)(uintptr_t)(lds_cf32 *)(const float *)sBuf + xin_off);
 #pragma unroll
                 for (int i = 0; i < 9; i++) {
-                    const float2 v = *(const float2 *)&sBuf[base + 2 * i];
+                    const f32x2 v = P[4 + i];
                     xf[2 * i] = v.x;
                     xf[2 * i + 1] = v.y;
                 }
-                const int pb = sbx ? base - 8 : base, nb = sbx < 31 ? base + 18 : base;
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-                    const float2 p = *(const float2 *)&sBuf[pb + 2 * i];
-                    const float2 n = *(const float2 *)&sBuf[nb + 2 * i];
+                    const f32x2 p = P[i];
+                    const f32x2 n = P[13 + i];
                     up[7 - 2 * i] = p.x;
                     up[6 - 2 * i] = p.y;
                     dn[2 * i] = n.x;
@@ -1524,6 +1528,7 @@ k_synth(const FrameRec *__restrict__ rec, const int16_t *__restrict__ is_buf, co
      * placed them last, above 64 KB: a v_add per table read), the is[]
      * prefetch areas last */
     struct Lds {
+        float pad_[64]; /* xin's look-back of wave 0, subband 0 (words it does not use) */
         SynWave Wv[SYN_WAVES];
         SynShared<LSF> T;
         uint32_t isq[SynCfg<SRC_XR, LSF>::DMA ? SYN_WAVES : 1][2 * 320];
@@ -1629,7 +1634,12 @@ __global__ void __launch_bounds__(256) k_frame(const uint8_t *__restrict__ in_ho
                                                UnitMeta *__restrict__ meta, void *__restrict__ pcm,
                                                uint32_t *__restrict__ done, uint32_t seq) {
     __shared__ __attribute__((aligned(16))) SynShared<LSF> T;
-    __shared__ SynWave Wv[2];
+    /* a pad below wave 0's buffer: xin's look-back of subband 0 */
+    __shared__ struct {
+        float pad_[64];
+        SynWave w[2];
+    } WvP;
+    SynWave *const Wv = WvP.w;
     __shared__ float s_xch[47 * 64]; /* granule 0 -> 1 hand-off: overlap (18), history (14 + 15) per lane */
     __shared__ __attribute__((aligned(16))) uint16_t s_lut[MP3D_LUT_MAX];
     __shared__ __attribute__((aligned(16))) uint32_t s_bits[HW_UNITS][HW_WORDS + 4];
