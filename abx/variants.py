@@ -1011,6 +1011,22 @@ VARS["XIN"] = [
                     const f32x2 n = P[13 + i];"""),
 ]
 
+# phase Q: the is[] words read right after the requantiser path is known, before the band scales,
+# so their LDS latency overlaps the scales' chain (CISE)
+VARS["CISE"] = [
+    ("                fusedq = PAR && var[0] == 0 && var[1] == 0 && !is_on && !ms_fold;\n",
+     "                fusedq = PAR && var[0] == 0 && var[1] == 0 && !is_on && !ms_fold;\n"
+     "                if (!fusedq) {\n"
+     "                    if (nlive == 2) read_cis(std::integral_constant<int, 2>{});\n"
+     "                    else if (nlive == 3) read_cis(std::integral_constant<int, 3>{});\n"
+     "                    else read_cis(std::integral_constant<int, 5>{});\n"
+     "                }\n"),
+    ("""                if (nlive == 2) read_cis(std::integral_constant<int, 2>{});
+                else if (nlive == 3) read_cis(std::integral_constant<int, 3>{});
+                else read_cis(std::integral_constant<int, 5>{});
+                auto requant""", """                auto requant"""),
+]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
