@@ -1027,6 +1027,24 @@ VARS["CISE"] = [
                 auto requant""", """                auto requant"""),
 ]
 
+# phase W int16 stereo emit without the half-wave swap: each lane stores its own channel's two
+# samples (2 B each; one instruction covers 128 contiguous bytes of L/R) (EMS)
+VARS["EMS"] = [
+    ("""                            const int vo = vo_st;
+                            const int p0 = to_i32(o.x), p1 = to_i32(o.y);
+                            const auto r = __builtin_amdgcn_permlane32_swap(p0, p1, false, false);
+                            __builtin_amdgcn_raw_buffer_store_b32(
+                                __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16((int)r[0], (int)r[1])), r_pcm,
+                                vo + 256 * tp, so, 0);""",
+     """                            const int vo = vo_st;
+                            const uint32_t pk =
+                                __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16(to_i32(o.x), to_i32(o.y)));
+                            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)pk, r_pcm, vo + 256 * tp, so, 0);
+                            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(pk >> 16), r_pcm, vo + 256 * tp + 128, so, 0);"""),
+    ("const int vo_st = opaque((sb + 32 * ch) * (F32 ? 8 : 4))",
+     "const int vo_st = opaque(F32 ? (sb + 32 * ch) * 8 : (2 * sb + ch) * 2)"),
+]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
