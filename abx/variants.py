@@ -1045,6 +1045,18 @@ VARS["EMS"] = [
      "const int vo_st = opaque(F32 ? (sb + 32 * ch) * 8 : (2 * sb + ch) * 2)"),
 ]
 
+# phase Q's band scales: 2^((q & 3) / 4) by two independent selects instead of an LDS table read
+# (one LDS round trip off the scales' chain) (P2S)
+VARS["P2S"] = [
+    ("                auto p2q = [&](int q) { return ldexpf(T.p2q[q & 3], q >> 2) * msf; };",
+     """                auto p2q = [&](int q) {
+                    const bool o = (q & 1) != 0;
+                    const float lo = o ? 1.18920711500272106672f : 1.0f;
+                    const float hi = o ? 1.68179283050742908606f : 1.41421356237309504880f;
+                    return ldexpf((q & 2) ? hi : lo, q >> 2) * msf;
+                };"""),
+]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
