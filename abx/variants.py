@@ -1057,6 +1057,11 @@ VARS["P2S"] = [
                 };"""),
 ]
 
+# more is[] row strides (int16 lines): 584 (+16 B), 592 (+32 B), 704 (+256 B) (ISR584 / ISR592 / ISR704)
+VARS["ISR584"] = [("FLAGS", "-DMP3D_IS_ROW=584")]
+VARS["ISR592"] = [("FLAGS", "-DMP3D_IS_ROW=592")]
+VARS["ISR704"] = [("FLAGS", "-DMP3D_IS_ROW=704")]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
