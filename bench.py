@@ -452,7 +452,7 @@ def run_per_frame(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", type=int, default=3, choices=(1, 2, 3, 4, 5),
                     help="BASELINE.json configs[k-1]; 4 = 3 at --gpus 8 (65,536 streams per GPU)")
