@@ -1062,6 +1062,62 @@ VARS["ISR584"] = [("FLAGS", "-DMP3D_IS_ROW=584")]
 VARS["ISR592"] = [("FLAGS", "-DMP3D_IS_ROW=592")]
 VARS["ISR704"] = [("FLAGS", "-DMP3D_IS_ROW=704")]
 
+# k_huffman work queue: the next round's ticket taken at the start of a round and its units'
+# perm entries loaded right after this round's record loads, so neither latency sits between two
+# rounds (TKP)
+VARS["TKP"] = [
+    ("""    for (;;) {
+        uint32_t t = 0u;
+        if (lane == 0) t = atomicAdd(work, 1u);
+        const int ubase = 64 * (int)__builtin_amdgcn_readfirstlane(t);
+        if (ubase >= n_units) break;
+        {
+            const int u = ubase + lane < n_units ? (int)perm[ubase + lane] : n_units;
+            const int fr = u >> 2, gr = (u >> 1) & 1, ch = u & 1;
+            bool valid = u < n_units;
+            /* the stream's md base, loaded together with the frame record (not
+             * after it: one memory latency less per round) */
+            const uint64_t mdo = md_off[(valid ? fr : 0) / F];
+            FrameRec r;
+            uint64_t sq[4] = {0, 0, 0, 0};
+            if (valid) {
+                r = rec[fr];
+                valid = r.frame_bytes && !(r.first_gr & (REC_TAG | REC_DROP)) && ch < r.nch && (gr == 0 || !r.lsf);
+                const ulonglong2 a = *(const ulonglong2 *)&sideu[u & ~3];
+                const ulonglong2 b = *(const ulonglong2 *)&sideu[(u & ~3) + 2];
+                sq[0] = a.x; sq[1] = a.y; sq[2] = b.x; sq[3] = b.y;
+            }""", """    uint32_t tk = 0u;
+    if (lane == 0) tk = atomicAdd(work, 1u);
+    int ubase = 64 * (int)__builtin_amdgcn_readfirstlane(tk);
+    int u_pre = ubase + lane < n_units ? (int)perm[ubase + lane] : n_units;
+    for (;;) {
+        if (ubase >= n_units) break;
+        {
+            const int u = u_pre;
+            /* the next round's ticket, issued before this round's loads */
+            uint32_t tn = 0u;
+            if (lane == 0) tn = atomicAdd(work, 1u);
+            const int fr = u >> 2, gr = (u >> 1) & 1, ch = u & 1;
+            bool valid = u < n_units;
+            /* the stream's md base, loaded together with the frame record (not
+             * after it: one memory latency less per round) */
+            const uint64_t mdo = md_off[(valid ? fr : 0) / F];
+            FrameRec r;
+            uint64_t sq[4] = {0, 0, 0, 0};
+            if (valid) {
+                r = rec[fr];
+                valid = r.frame_bytes && !(r.first_gr & (REC_TAG | REC_DROP)) && ch < r.nch && (gr == 0 || !r.lsf);
+                const ulonglong2 a = *(const ulonglong2 *)&sideu[u & ~3];
+                const ulonglong2 b = *(const ulonglong2 *)&sideu[(u & ~3) + 2];
+                sq[0] = a.x; sq[1] = a.y; sq[2] = b.x; sq[3] = b.y;
+            }
+            /* ... and its units, in flight through this round (the barrier
+             * keeps the ticket's wait after this round's record loads) */
+            __asm__ volatile("" : "+v"(tn) : "v"(sq[0]), "v"(mdo));
+            ubase = 64 * (int)__builtin_amdgcn_readfirstlane(tn);
+            u_pre = ubase + lane < n_units ? (int)perm[ubase + lane] : n_units;"""),
+]
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
