@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <condition_variable>
 #include <mutex>
 #include <thread>
@@ -41,6 +42,7 @@ void launch_synth_xr(const float *, const uint8_t *, const uint8_t *, const DevT
 void launch_gather_frames(const void *, void *, const void *, void *, const int *, int, int, int, int, int,
                           hipStream_t);
 hipError_t upload_frame_constants(const uint16_t *);
+void launch_lds_poison(int, hipStream_t);
 void launch_frame(const uint8_t *, uint32_t, const uint64_t *, const uint32_t *, uint8_t *, const uint64_t *,
                   StreamState *, FrameRec *, uint64_t *, void *, int, const DevTables *, int16_t *, UnitMeta *, void *,
                   bool, bool, uint32_t *, uint32_t, hipStream_t);
@@ -382,6 +384,7 @@ struct mp3d_batch {
     hipEvent_t ev_done = nullptr;
     hipStream_t last_s = nullptr; /* compared with the next call's, never used */
     hipEvent_t ev[4] = {};
+    bool poison = false; /* MP3D_DEBUG_POISON at create */
 };
 
 /* an event after all of the handle's work issued so far */
@@ -399,14 +402,34 @@ static hipError_t state_clear(StreamState *st, int n, hipStream_t s) {
     return e;
 }
 
-static int grow(void **p, size_t *cap, size_t need) {
+/* MP3D_DEBUG_POISON=1 at create: every device and
+ * pinned allocation of the handle is filled with 0xFF when it is made, at
+ * create and at every grow(), before the zeroing the code does on purpose.
+ * A read of bytes nobody wrote then sees NaNs / huge lengths / all-ones
+ * words on EVERY run, instead of whatever an earlier allocation left --
+ * tests/test_gpu_poison.py runs the read-ahead, state and golden suites so. */
+static bool poison_env() {
+    const char *e = getenv("MP3D_DEBUG_POISON");
+    return e && e[0] && strcmp(e, "0") != 0;
+}
+static int poison_dev(bool on, void *p, size_t bytes, hipStream_t s) {
+    if (!on || !p || !bytes) return MP3D_OK;
+    HIPCHK(hipMemsetAsync(p, 0xFF, bytes, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return MP3D_OK;
+}
+static void poison_host(bool on, void *p, size_t bytes) {
+    if (on && p) memset(p, 0xFF, bytes);
+}
+
+static int grow(mp3d_batch *b, void **p, size_t *cap, size_t need) {
     if (need <= *cap) return MP3D_OK;
     if (*p) HIPCHK(hipFree(*p));
     *p = nullptr;
     *cap = 0;
     HIPCHK(hipMalloc(p, need));
     *cap = need;
-    return MP3D_OK;
+    return poison_dev(b->poison, *p, need, b->own);
 }
 
 /* Frames per k_synth segment for n streams x F frames: few streams leave
@@ -470,7 +493,7 @@ static int tail_plan(mp3d_batch *b, int n, int F, int seg_len, hipStream_t s, Ta
     if (seg_len < F) {
         const size_t need = STATE_TAIL * (size_t)n;
         const bool fresh = need > b->tail_cap[tp->t_out];
-        int r = grow((void **)&b->st_tail[tp->t_out], &b->tail_cap[tp->t_out], need);
+        int r = grow(b, (void **)&b->st_tail[tp->t_out], &b->tail_cap[tp->t_out], need);
         if (r) return r;
         /* k_synth writes the fifo slots the synthesis reads back (slot 0 only
          * at the columns some lane's window needs): zero the rest once, as
@@ -569,6 +592,22 @@ extern "C" int mp3d_batch_create(int device, int max_streams, int max_frames, mp
         return MP3D_E_HIP;
     }
     for (int i = 0; i < 4; i++) (void)hipEventCreate(&b->ev[i]);
+    b->poison = poison_env();
+    if (b->poison) {
+        const size_t fr = (size_t)max_streams * max_frames;
+        const struct { void *p; size_t n; } bufs[] = {
+            {b->st, sizeof(StreamState) * max_streams}, {b->rec, sizeof(FrameRec) * fr},
+            {b->sideu, sizeof(uint64_t) * units},       {b->is_buf, sizeof(int16_t) * MP3D_IS_ROW * units},
+            {b->meta, sizeof(UnitMeta) * units},        {b->rank, sizeof(uint32_t) * units},
+            {b->geo[0].d, 20 * (size_t)max_streams},    {b->geo[1].d, 20 * (size_t)max_streams},
+            {b->d_infos, sizeof(mp3d_frame_info) * fr}, {b->d_work, 256}};
+        for (const auto &x : bufs)
+            if (poison_dev(true, x.p, x.n, b->own)) {
+                mp3d_batch_destroy(b);
+                return MP3D_E_HIP;
+            }
+        for (auto &g : b->geo) poison_host(true, g.h, 20 * (size_t)max_streams);
+    }
     if (getenv("MP3D_DEBUG_ADDR")) /* placement diagnostics (tools/dbg/place.py) */
         fprintf(stderr, "mp3d: st %p rec %p sideu %p is_buf %p meta %p infos %p\n", (void *)b->st, (void *)b->rec,
                 (void *)b->sideu, (void *)b->is_buf, (void *)b->meta, (void *)b->d_infos);
@@ -711,7 +750,7 @@ static int prepare_geometry(mp3d_batch *b, const uint64_t *offsets, const uint32
     memcpy(g.h + 2 * (size_t)n, sizes, sizeof(uint32_t) * n);
     /* growing md frees the old region: hipFree waits for the device */
     const size_t md_was = b->md_cap;
-    int r = grow((void **)&b->md, &b->md_cap, o + 8192);
+    int r = grow(b, (void **)&b->md, &b->md_cap, o + 8192);
     if (r) return r;
     /* a new region starts zeroed: the Huffman staging reads whole words up
      * to 2 past a unit's end, and a corrupt unit may decode past its
@@ -742,7 +781,7 @@ static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offse
     for (int i = 0; i < n; i++) total = std::max<uint64_t>(total, offsets[i] + sizes[i]);
     const uint8_t *din = frames;
     if (!mapped && !is_device_ptr(frames, b->device)) {
-        r = grow((void **)&b->d_in, &b->in_cap, total + 64);
+        r = grow(b, (void **)&b->d_in, &b->in_cap, total + 64);
         if (r) return r;
         HIPCHK(hipMemcpyAsync(b->d_in, frames, total, hipMemcpyDefault, s));
         din = b->d_in;
@@ -758,9 +797,11 @@ static int run_front(mp3d_batch *b, const uint8_t *frames, const uint64_t *offse
     const bool wide = demux_wide(n);
     if (++b->call_seq == 0) b->call_seq = 1; /* (d_work[1] starts at 0) */
     b->fam_ok = wide;
+    if (b->poison) launch_lds_poison(dc.n_cu, s);
     launch_demux(din, g.in_off(), g.in_len(), b->md, g.md_off(), b->st, b->rec, b->sideu,
                  dev_infos ? (void *)dev_infos : b->d_infos, n, F, b->opts, wide, b->d_work + 1, b->call_seq, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[1], s));
+    if (b->poison) launch_lds_poison(dc.n_cu, s);
     launch_huffman(b->md, g.md_off(), b->rec, b->sideu, dc.tables, b->is_buf, b->meta, n, F, dc.n_cu,
                    huffman_wave(n * F * 4), b->d_work, b->rank, s);
     HIPCHK(hipEventRecord(g.freed, s)); /* the slot's last reader */
@@ -792,10 +833,12 @@ static int run_front_fp(mp3d_batch *b, const FpRun &fp, int F, hipStream_t s, mp
     if (b->timing) HIPCHK(hipEventRecord(b->ev[0], s));
     if (++b->call_seq == 0) b->call_seq = 1;
     b->fam_ok = false;
+    if (b->poison) launch_lds_poison(dc.n_cu, s);
     launch_demux_fp(fp.in, fp.len, fp.fo, b->md, b->st, fp.tail_in, fp.snap, b->rec, b->sideu,
                     dev_infos ? (void *)dev_infos : b->d_infos, F, b->opts, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[1], s));
     /* md offset of the one stream: a zero word of d_work (d_work[4..5]) */
+    if (b->poison) launch_lds_poison(dc.n_cu, s);
     launch_huffman(b->md, (const uint64_t *)(b->d_work + 4), b->rec, b->sideu, dc.tables, b->is_buf, b->meta, 1, F,
                    dc.n_cu, true, b->d_work, nullptr, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[2], s));
@@ -832,7 +875,7 @@ static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *of
     const PtrKind pk = mapped ? PTR_DEV : ptr_kind(pcm, b->device);
     bool pcm_host = pk == PTR_HOST;
     if (pk != PTR_DEV) {
-        r = grow((void **)&b->d_pcm, &b->pcm_cap, pcm_bytes);
+        r = grow(b, (void **)&b->d_pcm, &b->pcm_cap, pcm_bytes);
         if (r) return r;
         dpcm = b->d_pcm;
         /* another GPU's buffer: its rows the kernel does not write keep their
@@ -846,6 +889,7 @@ static int batch_decode(mp3d_batch *b, const uint8_t *frames, const uint64_t *of
     TailPlan tp;
     r = tail_plan(b, n, F, seg_len, s, &tp);
     if (r) return r;
+    if (b->poison) launch_lds_poison(dc.n_cu, s);
     launch_synth(b->rec, b->is_buf, b->meta, dc.tables, b->st, dpcm, f32, n, F, kinds, seg_len, tp.out, tp.in,
                  b->fam_ok ? b->d_work + 1 : nullptr, b->call_seq, dc.n_cu, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[3], s));
@@ -955,7 +999,7 @@ extern "C" int mp3d_batch_synth_only(mp3d_batch *b, const float *xr, const uint8
     const uint8_t *dbt = block_type, *dmx = mixed;
     if (!is_device_ptr(xr, b->device) || !is_device_ptr(block_type, b->device) || !is_device_ptr(mixed, b->device)) {
         size_t need = nx * 576 * sizeof(float) + 2 * nx + 64;
-        int r = grow((void **)&b->d_xr, &b->xr_cap, need);
+        int r = grow(b, (void **)&b->d_xr, &b->xr_cap, need);
         if (r) return r;
         uint8_t *base = (uint8_t *)b->d_xr;
         HIPCHK(hipMemcpyAsync(base, xr, nx * 576 * sizeof(float), hipMemcpyDefault, s));
@@ -971,7 +1015,7 @@ extern "C" int mp3d_batch_synth_only(mp3d_batch *b, const float *xr, const uint8
     const PtrKind pk = ptr_kind(pcm, b->device);
     const bool pcm_host = pk != PTR_DEV; /* host, or another GPU's (staged like host) */
     if (pcm_host) {
-        int r = grow((void **)&b->d_pcm, &b->pcm_cap, pcm_bytes);
+        int r = grow(b, (void **)&b->d_pcm, &b->pcm_cap, pcm_bytes);
         if (r) return r;
         dpcm = b->d_pcm;
         /* mono rows are half written: the rest keeps the caller's bytes */
@@ -989,6 +1033,7 @@ extern "C" int mp3d_batch_synth_only(mp3d_batch *b, const float *xr, const uint8
         int r = tail_plan(b, n, F, seg_len, s, &tp);
         if (r) return r;
     }
+    if (b->poison) launch_lds_poison(dc.n_cu, s);
     launch_synth_xr(dxr, dbt, dmx, dc.tables, b->st, dpcm, n, F, nch, sr, seg_len, tp.out, tp.in, s);
     if (b->timing) HIPCHK(hipEventRecord(b->ev[3], s));
     HIPCHK(hipGetLastError());
@@ -1089,7 +1134,7 @@ extern "C" int mp3d_batch_decode_long(mp3d_batch *b, const uint8_t *data, size_t
     }
     const uint8_t *din = data;
     if (!is_device_ptr(data, b->device)) { /* host or another GPU's: staged */
-        int r = grow((void **)&b->d_in, &b->in_cap, bytes + 64);
+        int r = grow(b, (void **)&b->d_in, &b->in_cap, bytes + 64);
         if (r) return r;
         HIPCHK(hipMemcpyAsync(b->d_in, data, bytes, hipMemcpyDefault, s));
         din = b->d_in;
@@ -1116,6 +1161,11 @@ extern "C" int mp3d_batch_decode_long(mp3d_batch *b, const uint8_t *data, size_t
     } while (0)
     LCHK(hipMalloc(&seg_pcm, (size_t)std::min<long long>(chunk, K) * F * row));
     LCHK(hipMalloc(&seg_st, sizeof(StreamState) * (size_t)std::min<long long>(chunk, K)));
+    if (b->poison && (poison_dev(true, seg_pcm, (size_t)std::min<long long>(chunk, K) * F * row, s) ||
+                      poison_dev(true, seg_st, sizeof(StreamState) * (size_t)std::min<long long>(chunk, K), s))) {
+        rc = MP3D_E_HIP;
+        goto done;
+    }
     b->st = seg_st;
     LCHK(hipMalloc(&d_a, sizeof(int) * K));
     a32.assign(a.begin(), a.end());
@@ -1125,6 +1175,11 @@ extern "C" int mp3d_batch_decode_long(mp3d_batch *b, const uint8_t *data, size_t
     if (infos) {
         out_inf = inf_dev ? infos : nullptr;
         if (!inf_dev) LCHK(hipMalloc(&out_inf, sizeof(mp3d_frame_info) * (size_t)N));
+    }
+    if (b->poison && ((!pcm_dev && poison_dev(true, out_pcm, (size_t)N * row, s)) ||
+                      (infos && !inf_dev && poison_dev(true, out_inf, sizeof(mp3d_frame_info) * (size_t)N, s)))) {
+        rc = MP3D_E_HIP;
+        goto done;
     }
     for (long long k0 = 0; k0 < K; k0 += chunk) {
         const int ns = (int)std::min<long long>(chunk, K - k0);
@@ -1232,6 +1287,17 @@ struct mp3d_dec {
      * clears it.  A player that saves its state every frame then pays one
      * read-ahead per ~65 frames instead of two batch decodes per frame. */
     int ra_cool = 0, ra_backoff = 0;
+    /* A read-ahead launch or settle that failed part-way may have advanced
+     * the device state (k_demux_fp writes it and the snapshot first) with no
+     * record of where to: every later call returns this error until
+     * mp3d_dec_reset or a successful mp3d_dec_set_state. */
+    int broken = 0;
+    /* MP3D_DEBUG_RA_DELAY_US: the helper thread sleeps this long before each
+     * launch (tests: the served calls must not depend on its timing) */
+    int wk_delay_us = 0;
+    /* MP3D_DEBUG_RA_FAIL=n: the n-th next-run launch reports MP3D_E_HIP after
+     * its kernels were queued (the state then sits past the served frames) */
+    int dbg_fail = 0, dbg_launches = 0;
     /* The next run's launch (its HIP calls: three kernel launches and an
      * event, tens of microseconds of host time) runs on a helper thread, so
      * the call that hands it over returns at once; the frames are staged
@@ -1296,6 +1362,12 @@ extern "C" int mp3d_dec_create_on(int device, mp3d_dec **out) {
         d->ra_next_on = !(nx && !strcmp(nx, "0"));
         const char *th = getenv("MP3D_PF_RA_THREAD");
         d->wk_on = !(th && !strcmp(th, "0"));
+        /* test hooks: the helper's launch delayed, the n-th next-run launch
+         * failed after it ran (tests/test_gpu_poison.py) */
+        const char *dl = getenv("MP3D_DEBUG_RA_DELAY_US");
+        d->wk_delay_us = dl ? std::max(0, atoi(dl)) : 0;
+        const char *fl = getenv("MP3D_DEBUG_RA_FAIL");
+        d->dbg_fail = fl ? std::max(0, atoi(fl)) : 0;
     }
     int r = mp3d_batch_create(device, 1, std::max(1, d->ra_max), &d->b);
     if (r) {
@@ -1311,6 +1383,11 @@ extern "C" int mp3d_dec_create_on(int device, mp3d_dec **out) {
         hipHostMalloc((void **)&d->h_done, 64, co) != hipSuccess) {
         dec_free(d);
         return MP3D_E_NOMEM;
+    }
+    if (d->b->poison) { /* MP3D_DEBUG_POISON: the per-call pinned buffers too */
+        poison_host(true, d->h_in, MP3D_PF_BYTES);
+        poison_host(true, d->h_out, sizeof(float) * 2304);
+        poison_host(true, d->h_info, sizeof(mp3d_frame_info));
     }
     *d->h_done = 0u;
     if (!getenv("MP3D_PF_STAGED") && hipHostGetDevicePointer((void **)&d->m_in, d->h_in, 0) == hipSuccess &&
@@ -1333,8 +1410,12 @@ extern "C" int mp3d_dec_create_on(int device, mp3d_dec **out) {
         /* the md region of a run (k_demux_fp stages no geometry): carry +
          * payloads of K maximal frames + the staging margin, zeroed */
         const size_t md_need = MP3D_RES_BYTES + K * MP3D_MAX_FRAME_BYTES + MP3D_MAX_FRAME_BYTES + 16 + 8192;
-        if (grow((void **)&d->b->md, &d->b->md_cap, md_need) != MP3D_OK ||
-            hipMemset(d->b->md, 0, d->b->md_cap) != hipSuccess) {
+        /* zeroed on the handle's own stream and waited for (a null-stream
+         * hipMemset does not order before kernels on non-blocking streams;
+         * ADVICE r05) */
+        if (grow(d->b, (void **)&d->b->md, &d->b->md_cap, md_need) != MP3D_OK ||
+            hipMemsetAsync(d->b->md, 0, d->b->md_cap, d->b->own) != hipSuccess ||
+            hipStreamSynchronize(d->b->own) != hipSuccess) {
             dec_free(d);
             return MP3D_E_NOMEM;
         }
@@ -1351,6 +1432,16 @@ extern "C" int mp3d_dec_create_on(int device, mp3d_dec **out) {
                 hipEventCreateWithFlags(&u.done, hipEventDisableTiming) != hipSuccess) {
                 dec_free(d);
                 return MP3D_E_NOMEM;
+            }
+        if (d->b->poison) /* (the runs' buffers; MP3D_DEBUG_POISON) */
+            for (auto &u : d->run) {
+                poison_host(true, u.in, in_bytes);
+                poison_host(true, u.pcm, K * 2304 * sizeof(float));
+                poison_host(true, u.inf, K * sizeof(mp3d_frame_info));
+                if (poison_dev(true, u.snap, sizeof(StreamState), d->b->own)) {
+                    dec_free(d);
+                    return MP3D_E_HIP;
+                }
             }
     } else {
         d->ra_max = 0;
@@ -1399,6 +1490,7 @@ extern "C" void mp3d_dec_reset(mp3d_dec *d) {
     (void)ra_join(d);
     ra_drop(d); /* the state is zeroed whole */
     d->ra_cool = d->ra_backoff = 0;
+    d->broken = 0;
     (void)mp3d_batch_reset(d->b);
     d->frames = 0;
     d->kind = 0;
@@ -1440,6 +1532,7 @@ static int pf_fused(mp3d_dec *d, uint32_t have, bool f32, bool lsf) {
     if (r) return r;
     const mp3d_batch::Geo &g = b->geo[b->geo_i];
     const uint32_t seq = ++d->seq ? d->seq : ++d->seq; /* never 0, the word's initial value */
+    if (b->poison) launch_lds_poison(g_dev[b->device].n_cu, s);
     launch_frame(d->m_in, have, g.in_off(), g.in_len(), b->md, g.md_off(), b->st, b->rec, b->sideu, d->m_info,
                  b->opts, g_dev[b->device].tables, b->is_buf, b->meta, d->m_out, f32, lsf, d->m_done, seq, s);
     HIPCHK(hipGetLastError());
@@ -1464,7 +1557,14 @@ static int pf_fused(mp3d_dec *d, uint32_t have, bool f32, bool lsf) {
  * run was served whole and only the next one is ahead, the state saved
  * before the next run.  A no-op without a read-ahead. */
 static int ra_join(mp3d_dec *d);
+static int ra_settle_(mp3d_dec *d);
 static int ra_settle(mp3d_dec *d) {
+    if (d->broken) return d->broken;
+    const int r = ra_settle_(d);
+    if (r) d->broken = r; /* the restore may have run part-way */
+    return r;
+}
+static int ra_settle_(mp3d_dec *d) {
     {
         const int rj = ra_join(d); /* a launch still on the helper thread */
         if (rj) return rj;
@@ -1562,6 +1662,10 @@ static int ra_launch(mp3d_dec *d, mp3d_dec::Run &u, uint32_t o, int kinds, bool 
     r = batch_decode(b, u.in_m, &off, &o, 1, (int)u.ents.size(), u.pcm_m, f32, u.inf_m, nullptr, true, kinds, true,
                      d->ra_seg, &fp, async);
     if (r) return r;
+    if (async && d->dbg_fail && ++d->dbg_launches == d->dbg_fail) {
+        (void)hipStreamSynchronize(b->own);
+        return MP3D_E_HIP;
+    }
     u.f32 = f32;
     u.pending = async;
     if (async) HIPCHK(hipEventRecord(u.done, b->own));
@@ -1585,9 +1689,13 @@ static void ra_worker(mp3d_dec *d) {
         if (!d->wk_job) return; /* quit */
         const mp3d_dec::WkJob j = d->wk_arg;
         lk.unlock();
+        if (d->wk_delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(d->wk_delay_us));
         const int rc = ra_launch(d, *j.u, j.o, j.kinds, j.f32, true);
         lk.lock();
-        if (rc) j.u->ents.clear(); /* (the caller sees no next run, and rc at its next join) */
+        if (rc) {
+            j.u->ents.clear(); /* (the caller sees no next run, and rc at its next join) */
+            d->broken = rc;    /* the state may be past the served frames */
+        }
         d->wk_rc = rc;
         d->wk_job = false;
         lk.unlock();
@@ -1604,6 +1712,7 @@ static int ra_fill(mp3d_dec *d, mp3d_dec::Run &u, const uint8_t *buf, size_t byt
     const int r = ra_launch(d, u, o, kinds, f32, false);
     if (r) {
         u.ents.clear();
+        d->broken = r;
         return r;
     }
     return 1;
@@ -1625,7 +1734,10 @@ static int ra_launch_next(mp3d_dec *d, const uint8_t *buf, size_t bytes, bool f3
     if (!ra_stage(d, u, buf + at, bytes - at, false, &kind, &o, &kinds)) return MP3D_OK;
     if (!d->wk_on) {
         const int r = ra_launch(d, u, o, kinds, f32, true);
-        if (r) u.ents.clear();
+        if (r) {
+            u.ents.clear();
+            d->broken = r;
+        }
         return r;
     }
     if (!d->wk.joinable()) d->wk = std::thread(ra_worker, d);
@@ -1641,6 +1753,7 @@ static int ra_launch_next(mp3d_dec *d, const uint8_t *buf, size_t bytes, bool f3
 static int decode_frame(mp3d_dec *d, const uint8_t *buf, size_t bytes, void *pcm, bool f32, bool last,
                         mp3d_frame_info *info) {
     if (!d || !buf) return MP3D_E_ARG;
+    if (d->broken) return d->broken;
     mp3d_frame_info tmp;
     if (!info) info = &tmp;
     memset(info, 0, sizeof(*info));
@@ -1760,30 +1873,41 @@ extern "C" int mp3d_decode_frame_ex(mp3d_dec *d, const uint8_t *buf, size_t byte
 /* ------------------------------------------------------------------------ */
 extern "C" size_t mp3d_state_bytes(void) { return sizeof(StreamState); }
 
+/* every blob must carry this build's format stamp (StreamState.fmt): a blob
+ * of another state format would decode with wrong history.  Reads only the
+ * blob (a device blob through the handle's own stream, after its last call);
+ * the handle's state is untouched. */
+static int blob_check(mp3d_batch *b, int n, const void *src) {
+    std::vector<uint32_t> fmt((size_t)n);
+    const uint8_t *f0 = (const uint8_t *)src + offsetof(StreamState, fmt);
+    if (ptr_kind(src, b->device) == PTR_HOST) {
+        for (int i = 0; i < n; i++) memcpy(&fmt[i], f0 + sizeof(StreamState) * (size_t)i, sizeof(uint32_t));
+    } else {
+        HIPCHK(hipSetDevice(b->device));
+        int r = own_after_last(b);
+        if (r) return r;
+        HIPCHK(hipMemcpy2DAsync(fmt.data(), sizeof(uint32_t), f0, sizeof(StreamState), sizeof(uint32_t), (size_t)n,
+                                hipMemcpyDefault, b->own));
+        HIPCHK(hipStreamSynchronize(b->own));
+    }
+    for (int i = 0; i < n; i++)
+        if (fmt[i] != MP3D_STATE_FMT) return MP3D_E_ARG;
+    return MP3D_OK;
+}
+
 static int state_copy(mp3d_batch *b, int first, int n, void *dst, const void *src, bool out) {
     if (!b || !(out ? dst : src) || first < 0 || n <= 0) return MP3D_E_ARG;
     if ((long long)first + n > b->max_streams) return MP3D_E_CAPACITY;
+    if (!out) {
+        const int rb = blob_check(b, n, src); /* before anything is written */
+        if (rb) return rb;
+    }
     HIPCHK(hipSetDevice(b->device));
     hipStream_t s = b->own;
     int r = own_after_last(b); /* after the handle's last call, on any stream */
     if (r) return r;
     r = flush_tail(b, s);
     if (r) return r;
-    if (!out) {
-        /* every blob must carry this build's format stamp (StreamState.fmt):
-         * a blob of another state format would decode with wrong history */
-        std::vector<uint32_t> fmt((size_t)n);
-        const uint8_t *f0 = (const uint8_t *)src + offsetof(StreamState, fmt);
-        if (ptr_kind(src, b->device) == PTR_HOST) {
-            for (int i = 0; i < n; i++) memcpy(&fmt[i], f0 + sizeof(StreamState) * (size_t)i, sizeof(uint32_t));
-        } else {
-            HIPCHK(hipMemcpy2DAsync(fmt.data(), sizeof(uint32_t), f0, sizeof(StreamState), sizeof(uint32_t), (size_t)n,
-                                    hipMemcpyDefault, s));
-            HIPCHK(hipStreamSynchronize(s));
-        }
-        for (int i = 0; i < n; i++)
-            if (fmt[i] != MP3D_STATE_FMT) return MP3D_E_ARG;
-    }
     StreamState *at = b->st + first;
     HIPCHK(hipMemcpyAsync(out ? dst : (void *)at, out ? (const void *)at : src, sizeof(StreamState) * (size_t)n,
                           hipMemcpyDefault, s));
@@ -1808,10 +1932,17 @@ extern "C" int mp3d_dec_get_state(mp3d_dec *d, void *buf) {
 
 extern "C" int mp3d_dec_set_state(mp3d_dec *d, const void *buf) {
     if (!d || !buf) return MP3D_E_ARG;
-    (void)ra_join(d);
+    {
+        /* a refused blob writes nothing (mp3d.h): checked BEFORE the read-ahead
+         * is forgotten, so the decoder stays at the frame it served */
+        (void)ra_join(d); /* (a failed launch left d->broken, which a new state clears) */
+        const int rb = blob_check(d->b, 1, buf);
+        if (rb) return rb;
+    }
     ra_drop(d); /* replaced whole: nothing read ahead applies */
     const int r = mp3d_batch_set_state(d->b, 0, 1, buf);
     if (r) return r;
+    d->broken = 0; /* a whole new state: a failed read-ahead no longer matters */
     /* host mirror of the family lock and "past the stream start" (ID3v2 skip) */
     StreamState h;
     HIPCHK(hipMemcpy(&h, d->b->st, sizeof(h), hipMemcpyDeviceToHost));

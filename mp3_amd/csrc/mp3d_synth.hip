@@ -1805,6 +1805,24 @@ void launch_synth_xr(const float *xr, const uint8_t *bt, const uint8_t *mixed, c
                        (const uint32_t *)nullptr, 0u);
 }
 
+/* MP3D_DEBUG_POISON only (mp3d_host.cpp poison_env): fill the whole LDS of
+ * every CU with 0xFF before each of the handle's launches, so the first
+ * workgroup the next kernel places on a CU finds all-ones words (NaN as
+ * float) in any LDS it reads before writing, on every run -- not whatever
+ * the previous kernel on that CU left.  160 KB per workgroup, so one per CU
+ * at a time; 4 per CU. */
+#define LDS_POISON_WORDS (160 * 1024 / 4)
+__global__ void __launch_bounds__(1024) k_lds_poison() {
+    __shared__ uint32_t s[LDS_POISON_WORDS];
+    /* volatile: LDS is dead at kernel end, so plain stores are removed */
+    volatile uint32_t *v = s;
+    for (int i = threadIdx.x; i < LDS_POISON_WORDS; i += 1024) v[i] = 0xFFFFFFFFu;
+}
+
+void launch_lds_poison(int n_cu, hipStream_t strm) {
+    hipLaunchKernelGGL(k_lds_poison, dim3(4 * (n_cu > 0 ? n_cu : 256)), dim3(1024), 0, strm);
+}
+
 void launch_gather_frames(const void *src, void *dst, const void *isrc, void *idst, const int *a, int L, int F, int k0,
                           int n_out, int bytes_per_row, hipStream_t strm) {
     hipLaunchKernelGGL(k_gather_frames, dim3(n_out), dim3(256), 0, strm, (const uint4 *)src, (uint4 *)dst,

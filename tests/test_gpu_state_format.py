@@ -164,3 +164,35 @@ def test_first_call_on_dirty_reused_memory(ra):
         for k, ((n, p), (n_ref, r)) in enumerate(zip(got, ref)):
             assert n == n_ref and np.array_equal(p, r), (rep, k)
         b.close()
+
+
+@pytest.mark.parametrize("ra", [16, 64])
+def test_refused_blob_keeps_read_ahead_position(ra):
+    """a decoder 10 frames into a read-ahead run is handed
+    a blob without the format stamp.  set_state must refuse it AND leave the
+    decoder at the frame it served: the frames after it equal a decoder that
+    never read ahead (before the fix the run was forgotten with the device
+    state already past it, and the next frames decoded with the wrong
+    reservoir, overlap and history, silently)."""
+    data, _ = _golden.case("bench_c5_g1")
+    d, ref = _dec(ra), _dec(0)
+    pos = 0
+    for _ in range(10):
+        n, p, info = d.decode_frame(data[pos:], last=True)
+        n_r, p_r, info_r = ref.decode_frame(data[pos:], last=True)
+        assert n == n_r and np.array_equal(p, p_r)
+        pos += info.frame_bytes
+    bad = ref.get_state()  # (from the decoder without read-ahead: d stays mid-run)
+    bad[FMT_OFF:FMT_OFF + 4] = 0
+    with pytest.raises(mp3_amd.MP3DError):
+        d.set_state(bad)
+    k = 0
+    while pos < len(data):
+        n, p, info = d.decode_frame(data[pos:], last=True)
+        n_r, p_r, info_r = ref.decode_frame(data[pos:], last=True)
+        assert info.frame_bytes == info_r.frame_bytes and n == n_r and np.array_equal(p, p_r), k
+        if info.frame_bytes <= 0:
+            break
+        pos += info.frame_bytes
+        k += 1
+    assert k >= 10
