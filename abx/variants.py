@@ -1118,6 +1118,59 @@ VARS["TKP"] = [
             u_pre = ubase + lane < n_units ? (int)perm[ubase + lane] : n_units;"""),
 ]
 
+
+# ---- round 6 bounds (timing only; output wrong by construction) ----
+# NOIM: phase I without the fast 36-point IMDCT (its 18 inputs passed through
+# as the DCT-IV outputs): the most any IMDCT speed-up (e.g. on the matrix
+# cores, VERDICT r05 item 2) could take off k_synth
+VARS["NOIM"] = [("""                    imdct36_wp(x, W, (const f32x2 *)(uintptr_t)(uint32_t)opaque((int)(uintptr_t)(lds_cf32 *)(const float *)&T.kc[0]));""",
+                 """#pragma unroll
+                    for (int n = 0; n < 9; n++) W[n] = (f32x2){x[n], x[17 - n]};""")]
+# NOBS: phase Q without the band-scale step (lane = band: sf word by a
+# cross-lane read, 2^(q/4), the LDS store and the wave sync after it) -- the
+# scale rows keep whatever they held: the most a precomputed per-band scale
+# (VERDICT r05 item 3) could take off
+VARS["NOBS"] = [("""                    const float v = p2q(gain - ((sf + pre) << shift));
+                    if (bl < 22) Wd.scale[c][bl] = v;""", """                    (void)gain; (void)shift; (void)wd; (void)sf; (void)pre; (void)bl;"""),
+                ("""                wave_sync();
+                (void)m12a;""", """                (void)m12a;""")]
+
+
+
+# NOXIN: phase I's inputs not read back from the
+# xr scatter (constants instead; the scatter stores stay): the most a
+# register-only requantiser for M/S frames could save
+VARS["NOXIN"] = [("""                    const f32x2 v = P[4 + i];
+                    xf[2 * i] = v.x;""", """                    const f32x2 v = (f32x2){(float)i, 0.5f};
+                    xf[2 * i] = v.x;"""),
+                 ("""                    const f32x2 p = P[i];
+                    const f32x2 n = P[13 + i];""", """                    const f32x2 p = (f32x2){0.25f, (float)i};
+                    const f32x2 n = (f32x2){(float)i, 0.75f};""")]
+
+
+
+# what in the band-scale step costs (NOBS took 9 % off k_synth):
+# BSA: the compiler fence after the band scales dropped (the store -> read
+#      order within the wave stays: LDS executes in order, and the scale reads'
+#      addresses are integer-built, so the compiler keeps them after the
+#      store) -- output unchanged
+VARS["BSA"] = [("""                wave_sync();
+                (void)m12a;""", """                (void)m12a;""")]
+# BSB: the lane's scalefactor word from its own lane (no cross-lane read;
+#      wrong scales, timing only)
+VARS["BSB"] = [("""                    const uint32_t wd = (uint32_t)__shfl((int)wm[cs], c * MW + (j >> 2));
+                    const int sf = (int)(wd >> (8 * (j & 3))) & 0xFF;
+                    const int pre = (g11 & 0xFFu) ? (int)(MP3D_PRETAB_BITS >> (2 * j)) & 3 : 0;
+                    const float v = p2q(gain - ((sf + pre) << shift));""",
+                """                    const uint32_t wd = wm[cs];
+                    const int sf = (int)(wd >> (8 * (j & 3))) & 0xFF;
+                    const int pre = (g11 & 0xFFu) ? (int)(MP3D_PRETAB_BITS >> (2 * j)) & 3 : 0;
+                    const float v = p2q(gain - ((sf + pre) << shift));""")]
+# BSC: 2^((q & 3)/4) not read from the LDS table (1.0; wrong scales, timing only)
+VARS["BSC"] = [("""                auto p2q = [&](int q) { return ldexpf(T.p2q[q & 3], q >> 2) * msf; };""",
+                """                auto p2q = [&](int q) { return ldexpf(1.0f, q >> 2) * msf; };""")]
+
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
