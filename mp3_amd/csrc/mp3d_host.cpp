@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
@@ -1291,7 +1292,7 @@ struct mp3d_dec {
      * the device state (k_demux_fp writes it and the snapshot first) with no
      * record of where to: every later call returns this error until
      * mp3d_dec_reset or a successful mp3d_dec_set_state. */
-    int broken = 0;
+    std::atomic<int> broken{0}; /* (written by the helper thread, read by the caller's) */
     /* MP3D_DEBUG_RA_DELAY_US: the helper thread sleeps this long before each
      * launch (tests: the served calls must not depend on its timing) */
     int wk_delay_us = 0;
