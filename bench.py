@@ -812,6 +812,12 @@ def report_decode(c, args, cfg, value, kt, frames_per_step):
                        "(profiles/) show k_synth limited by VALU issue and dependent-chain latency, not by the "
                        "matrix cores (see mfma_util_pmc)",
             "flop_per_frame": FLOP_PER_FRAME, "frames_per_launch": frames_per_launch, "launch_us": kt["synth"],
+            "clock_mhz_pmc": pmc.get("k_synth_clock_mhz"),
+            "frac_at_clock": (achieved_tf / (FP32_PEAK_TFLOPS * pmc["k_synth_clock_mhz"] / 2400.0)
+                              if pmc.get("k_synth_clock_mhz") else None),
+            "clock_note": "k_synth's mean engine clock in the committed PMC profile (GRBM_GUI_ACTIVE / 8 XCDs / "
+                          "duration, profiles/pmc_traffic.json): power-limited below the 2400 MHz the peak assumes; "
+                          "frac_at_clock = achieved / the FP32 peak at that clock",
             "executed_flop_per_frame": EXEC_FLOP_PER_FRAME,
             "executed_frac": EXEC_FLOP_PER_FRAME * frames_per_launch / synth_s / 1e12 / FP32_PEAK_TFLOPS
             if synth_s else 0,
@@ -860,6 +866,9 @@ def report_c2(c, args, value, kt):
             "peak": FP32_PEAK_TFLOPS, "frac": achieved_tf / FP32_PEAK_TFLOPS,
             "traffic": pmc.get("k_synth_hbm_bytes_per_launch"),
             "flop_per_frame": C2_FLOP_PER_FRAME, "frames_per_launch": fpl, "launch_us": kt["synth"],
+            "clock_mhz_pmc": pmc.get("k_synth_clock_mhz"),
+            "frac_at_clock": (achieved_tf / (FP32_PEAK_TFLOPS * pmc["k_synth_clock_mhz"] / 2400.0)
+                              if pmc.get("k_synth_clock_mhz") else None),
             "hbm_GBs_algorithmic": gbs, "hbm_frac": gbs / HBM_PEAK_GBS,
             "bytes_per_frame": C2_BYTES_PER_FRAME,
             "limiter": "22 FLOP/B against a machine balance of 19.7: both rooflines are reported"},

@@ -30,6 +30,12 @@ def counters(d):
             continue
         k = name.split("(")[0].replace("void ", "").replace("mp3d::", "")
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        if r["Counter_Name"] == "GRBM_GUI_ACTIVE" and r.get("End_Timestamp"):
+            # the launch's mean engine clock: GRBM_GUI_ACTIVE is summed over the
+            # 8 XCDs (MI355X_MICROARCH.md DVFS note), timestamps in ns
+            dt = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            if dt > 0:
+                agg[k]["clock_mhz"].append(float(r["Counter_Value"]) / 8.0 / dt * 1e3)
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in agg.items()}
 
 
@@ -75,6 +81,7 @@ def main():
             "k_synth_hbm_bytes_per_launch": synth["hbm_bytes_per_launch"],
             "k_synth_fetch_kib": synth["FETCH_SIZE"], "k_synth_write_kib": synth["WRITE_SIZE"],
             "k_synth_mfma_util": synth.get("mfma_util"),
+            "k_synth_clock_mhz": synth.get("clock_mhz"),
             "k_synth_mfma_f32_flop_per_launch": synth.get("mfma_f32_flop_per_launch"),
             "step_hbm_bytes": sum(cs.get("hbm_bytes_per_launch", 0.0) for cs in out.values()),
             "per_kernel_hbm_bytes": {k: cs.get("hbm_bytes_per_launch") for k, cs in out.items()},
