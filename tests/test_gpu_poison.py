@@ -165,3 +165,67 @@ def test_failed_next_run_then_set_state(monkeypatch):
     d.set_state(saved)
     monkeypatch.delenv("MP3D_DEBUG_RA_FAIL")
     RA._same(RA._run(d, data, script), ref)
+
+
+# ---- the batch paths under the poison (round 6): every golden through the
+# batch API, odd and ragged shapes, LSF, CRC, corrupted main data, both demux
+# paths, the segmented synth-only entry, the long-stream decode and gapless
+import test_gpu_c2 as C2  # noqa: E402
+import test_gpu_crc as CRC  # noqa: E402
+import test_gpu_demux_paths as DP  # noqa: E402
+import test_gpu_edges as ED  # noqa: E402
+import test_gpu_fuzz as FZ  # noqa: E402
+import test_gpu_gapless as GL  # noqa: E402
+import test_gpu_long as LG  # noqa: E402
+import test_gpu_lsf as LSF  # noqa: E402
+import test_gpu_parity as PA  # noqa: E402
+
+
+@pytest.mark.parametrize("name", _golden.names())
+def test_poison_batch_every_golden(name):
+    PA.test_golden_cases_batch_api(name)
+
+
+def test_poison_edges():
+    for args in ((ED._gen.C5, 501, 37, 5), (ED._gen.C3, 502, 3, 7)):
+        ED.test_odd_shapes_pcm(*args)
+    ED.test_ragged_mixed_batch()
+    ED.test_high_bitrate_staging_batches()
+
+
+def test_poison_lsf():
+    LSF.test_mixed_family_batch()
+    LSF.test_mixed_family_wide_batch_persistent_lsf_grid()
+    LSF.test_lsf_state_carries_across_calls()
+    LSF.test_lsf_per_frame_api()
+
+
+@pytest.mark.parametrize("opts", [0, mp3_amd.OPT_CRC_CHECK])
+def test_poison_crc(opts):
+    CRC.test_batch_crc_option_vs_oracle(opts)
+
+
+def test_poison_corrupted_main_data():
+    FZ.test_corrupted_main_data_vs_oracle(FZ._gen.C5, 1201)
+    FZ.test_random_garbage_never_faults()
+
+
+@pytest.mark.parametrize("pad", [False, True])
+def test_poison_demux_paths(pad):
+    DP.test_paths_identical(0, pad)
+
+
+def test_poison_c2_segments():
+    C2.test_c2_segments_bit_identical_across_calls()
+    C2.test_c2_state_tails_across_calls()
+
+
+@pytest.mark.parametrize("name", ["keypress_128k_js", "edge_bv_drop", "edge_garbage"])
+def test_poison_long_goldens(name):
+    LG.test_long_golden_matches_sequential(name, 4)
+
+
+def test_poison_gapless():
+    GL.test_batch_gapless_matches_ffmpeg_tagged()
+    GL.test_per_frame_gapless_matches_ffmpeg_tagged()
+    GL.test_tag_split_across_calls()
