@@ -1171,6 +1171,73 @@ VARS["BSC"] = [("""                auto p2q = [&](int q) { return ldexpf(T.p2q[q
                 """                auto p2q = [&](int q) { return ldexpf(1.0f, q >> 2) * msf; };""")]
 
 
+
+# HSTAT (round 6, VERDICT r05 item 4: account for k_huffman's reads): the
+# staged main-data bytes of a launch and the distinct 128-B lines they span,
+# counted by atomics (per lane: its segment's words and lines; plus one
+# FrameRec + side-word line pair per frame), read back through an extra
+# symbol of this build only (mp3d_dbg_hstat, abx/hstat.py).  Output unchanged.
+VARS["HSTAT"] = [
+    ("""            const uint32_t *src = (const uint32_t *)(md + (dec ? mdo : 0)) + w0;""",
+     """            const uint32_t *src = (const uint32_t *)(md + (dec ? mdo : 0)) + w0;
+            if (dec) {
+                const uint64_t a0 = (uint64_t)(uintptr_t)src, a1 = a0 + 4ull * len;
+                atomicAdd(&g_hstat[0], (unsigned long long)(4ull * len));
+                atomicAdd(&g_hstat[1], (unsigned long long)(((a1 - 1) >> 7) - (a0 >> 7) + 1));
+                atomicAdd(&g_hstat[2], 1ull);
+            }"""),
+    ("""/* k_huffman: one lane per unit (its layout constants and helpers: mp3d_huffman_dev.h) */""",
+     """__device__ unsigned long long g_hstat[4];
+/* k_huffman: one lane per unit (its layout constants and helpers: mp3d_huffman_dev.h) */"""),
+    ("""    int n_units = n_streams * F * 4;
+    if (wave) {""", """    int n_units = n_streams * F * 4;
+    {
+        static const unsigned long long z[4] = {0, 0, 0, 0};
+        (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_hstat), z, sizeof(z), 0, hipMemcpyHostToDevice, strm);
+    }
+    if (wave) {"""),
+    ("""                       n_units, F, work, (const uint32_t *)rank);
+}
+
+} // namespace mp3d
+""", """                       n_units, F, work, (const uint32_t *)rank);
+}
+
+} // namespace mp3d
+extern "C" __attribute__((visibility("default"))) int mp3d_dbg_hstat(unsigned long long *out4) {
+    return (int)hipMemcpyFromSymbol(out4, HIP_SYMBOL(mp3d::g_hstat), 4 * sizeof(unsigned long long), 0,
+                                    hipMemcpyDeviceToHost);
+}
+"""),
+]
+
+
+
+# HSTAT2: HSTAT plus the bytes k_huffman's store instructions carry (every
+# lane's big_values group stores, dead zero groups included, count1 stores,
+# UnitMeta), one atomic per unit, into g_hstat[3]
+VARS["HSTAT2"] = VARS["HSTAT"] + [
+    ("""                    uint4 pend = make_uint4(0u, 0u, 0u, 0u);
+                    bool held = false;""", """                    uint4 pend = make_uint4(0u, 0u, 0u, 0u);
+                    bool held = false;
+                    unsigned long long st_bytes = 56ull; /* UnitMeta: sf 40 B + 16 B */"""),
+    ("""                        if (held) { /* (k is uniform: no divergence) */""",
+     """                        st_bytes += 16ull;
+                        if (held) { /* (k is uniform: no divergence) */"""),
+    ("""                        if (!two) {
+                            c1_store(k, se0);""", """                        if (!two) {
+                            st_bytes += 8ull;
+                            c1_store(k, se0);"""),
+    ("""                        __builtin_memcpy(row + k, &q, 16);
+                        k += 8;
+                    }""", """                        __builtin_memcpy(row + k, &q, 16);
+                        st_bytes += 16ull;
+                        k += 8;
+                    }
+                    atomicAdd(&g_hstat[3], st_bytes);"""),
+]
+
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
