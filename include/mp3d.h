@@ -75,7 +75,10 @@ typedef struct mp3d_batch mp3d_batch;
  * frame).  info->frame_bytes (+ any skipped prefix) tells how far to
  * advance; pcm may be NULL (decode for state only).  Reservoir underflow
  * (a stream entered mid-way) follows FFmpeg: the affected granules decode
- * as silence.                                                               */
+ * as silence.  A HIP error while the decoder was reading ahead (or putting
+ * a read-ahead back) leaves its state undefined: that error is returned by
+ * every later decode / get_state / set_options call until mp3d_dec_reset or
+ * a successful mp3d_dec_set_state.                                          */
 MP3D_API int mp3d_dec_create(mp3d_dec **out);
 MP3D_API int mp3d_dec_create_on(int device, mp3d_dec **out);
 MP3D_API void mp3d_dec_destroy(mp3d_dec *dec);
