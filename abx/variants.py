@@ -1238,6 +1238,31 @@ VARS["HSTAT2"] = VARS["HSTAT"] + [
 ]
 
 
+
+# WPRE (timing only; wrong decode): the big_values loop's window words read
+# at the PREVIOUS pair's position, one pair ahead, so the window load is off
+# the pair-to-pair dependency chain (the funnel shift still uses the current
+# position): the most a register-resident bit buffer could take off k_huffman
+VARS["WPRE"] = [
+    ("""                    uint4 pend = make_uint4(0u, 0u, 0u, 0u);
+                    bool held = false;""", """                    uint4 pend = make_uint4(0u, 0u, 0u, 0u);
+                    bool held = false;
+                    uint32_t pw0, pw1, pw2;
+                    {
+                        const uint32_t w = (pos + 31u) >> 5;
+                        pw0 = bits[(int)w - 1]; pw1 = bits[w]; pw2 = bits[w + 1];
+                    }"""),
+    ("""                            uint32_t hi, lo;
+                            win64g(bits, pos, hi, lo);""", """                            uint32_t hi, lo;
+                            hi = __builtin_amdgcn_alignbit(pw0, pw1, 0u - pos);
+                            lo = __builtin_amdgcn_alignbit(pw1, pw2, 0u - pos);
+                            {
+                                const uint32_t w = (pos + 31u) >> 5;
+                                pw0 = bits[(int)w - 1]; pw1 = bits[w]; pw2 = bits[w + 1];
+                            }"""),
+]
+
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
