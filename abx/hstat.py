@@ -27,7 +27,7 @@ def main():
     pcm = torch.empty((n, F, 2304), dtype=torch.int16, device="cuda")
     dec = mp3_amd.BatchDecoder(n, F)
     L = mp3_amd.lib()
-    out = (ctypes.c_ulonglong * 4)()
+    out = (ctypes.c_ulonglong * 8)()
     res = []
     for rep in range(2):
         dec.reset()
@@ -35,7 +35,7 @@ def main():
         torch.cuda.synchronize()
         assert L.mp3d_dbg_hstat(out) == 0
         res.append([int(x) for x in out])
-    staged, lines, units, stored = res[-1]
+    staged, lines, units, stored, batches, rounds, spill, _ = res[-1]
     frames = n * F
     print(json.dumps({
         "probe": "k_huffman read account (HSTAT build)", "streams": n, "frames": frames,
@@ -43,6 +43,8 @@ def main():
         "staged_lines_128B": lines, "staged_line_bytes": 128 * lines,
         "store_bytes": stored, "store_bytes_note": "HSTAT2 builds only: bytes k_huffman's store instructions carry "
         "(big_values groups incl. the dead zero groups of lanes past their big_values, count1, UnitMeta); 0 with HSTAT",
+        "staging_batches": batches, "rounds": rounds, "batches_per_round": batches / max(1, rounds),
+        "lanes_past_first_batch": spill, "note_batches": "HSTAT3 builds only (0 otherwise)",
         "records_bytes": frames * (32 + 32) + n * 8 + 4 * frames * 4,
         "note": "records = FrameRec 32 B + side words 32 B per frame, md offset 8 B per stream, rank 4 B per unit",
         "input_payload_bytes": int(sizes.astype("int64").sum())}))

@@ -1187,12 +1187,12 @@ VARS["HSTAT"] = [
                 atomicAdd(&g_hstat[2], 1ull);
             }"""),
     ("""/* k_huffman: one lane per unit (its layout constants and helpers: mp3d_huffman_dev.h) */""",
-     """__device__ unsigned long long g_hstat[4];
+     """__device__ unsigned long long g_hstat[8];
 /* k_huffman: one lane per unit (its layout constants and helpers: mp3d_huffman_dev.h) */"""),
     ("""    int n_units = n_streams * F * 4;
     if (wave) {""", """    int n_units = n_streams * F * 4;
     {
-        static const unsigned long long z[4] = {0, 0, 0, 0};
+        static const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_hstat), z, sizeof(z), 0, hipMemcpyHostToDevice, strm);
     }
     if (wave) {"""),
@@ -1204,8 +1204,8 @@ VARS["HSTAT"] = [
 }
 
 } // namespace mp3d
-extern "C" __attribute__((visibility("default"))) int mp3d_dbg_hstat(unsigned long long *out4) {
-    return (int)hipMemcpyFromSymbol(out4, HIP_SYMBOL(mp3d::g_hstat), 4 * sizeof(unsigned long long), 0,
+extern "C" __attribute__((visibility("default"))) int mp3d_dbg_hstat(unsigned long long *out8) {
+    return (int)hipMemcpyFromSymbol(out8, HIP_SYMBOL(mp3d::g_hstat), 8 * sizeof(unsigned long long), 0,
                                     hipMemcpyDeviceToHost);
 }
 """),
@@ -1260,6 +1260,28 @@ VARS["WPRE"] = [
                                 const uint32_t w = (pos + 31u) >> 5;
                                 pw0 = bits[(int)w - 1]; pw1 = bits[w]; pw2 = bits[w + 1];
                             }"""),
+]
+
+
+
+# HSTAT3: HSTAT2 plus the staging batches: g_hstat[4] += batches of a round
+# (the while loop's passes), g_hstat[5] += rounds, g_hstat[6] += lanes that
+# did not fit the first batch
+VARS["HSTAT3"] = [(a.replace("g_hstat[4]", "g_hstat[8]"), b.replace("g_hstat[4]", "g_hstat[8]"))
+                  for a, b in VARS["HSTAT2"]] + [
+    ("""            bool pending = dec;
+            while (__ballot(pending)) {""", """            bool pending = dec;
+            int nbatch = 0;
+            while (__ballot(pending)) {
+                nbatch++;"""),
+    ("""                pending = pending && !inb;
+            }""", """                pending = pending && !inb;
+                if (nbatch == 1 && pending) atomicAdd(&g_hstat[6], 1ull);
+            }
+            if (lane == 0) {
+                atomicAdd(&g_hstat[4], (unsigned long long)nbatch);
+                atomicAdd(&g_hstat[5], 1ull);
+            }"""),
 ]
 
 

@@ -143,11 +143,20 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
             const int scfsi = (gr == 1 && long_blk) ? scfsi_raw : 0;
             const bool need_g0 = dec && scfsi && first_gr == 0;
             const uint32_t g0_start = r.md_bit + (ch ? (uint32_t)(sq[0] >> 52) : 0u);
-            const uint32_t lo_bit = need_g0 ? g0_start : start;
-            const uint32_t w0 = lo_bit >> 5;
-            /* words [w0, w0 + len): through the unit end + 2 words of window
-             * margin, rounded to 4 words (16-B LDS stores) */
-            const uint32_t len = dec ? ((((start + p23 + 31) >> 5) + 2 - w0 + 3) & ~3u) : 0u;
+            /* the lane's staged words: for scfsi reuse (need_g0) first a piece
+             * of HUFF_G0W words at granule 0's scalefactors (their <= 126 bits
+             * from any bit offset, plus the window margin), then the unit's own
+             * words [w0, w0 + lenB): through the unit end + 2 words of window
+             * margin, rounded to 4 words (16-B LDS stores).  (Staged as one
+             * span from granule 0's start, such a unit took granule 0 of both
+             * channels too: C3's mean staged unit was 43 words, over the
+             * 2 304-word area's 36 per lane of a 64-unit round.) */
+            const uint32_t lenA = need_g0 ? HUFF_G0W : 0u;
+            const uint32_t w0 = start >> 5;
+            /* granule 0's piece, in words before the unit's own (from src) */
+            const uint32_t dA = need_g0 ? w0 - (g0_start >> 5) : 0u;
+            const uint32_t lenB = dec ? ((((start + p23 + 31) >> 5) + 2 - w0 + 3) & ~3u) : 0u;
+            const uint32_t len = lenA + lenB;
             const uint32_t incl = wave_incl_scan(len);
             const uint32_t off = incl - len;
             const uint32_t *src = (const uint32_t *)(md + (dec ? mdo : 0)) + w0;
@@ -163,8 +172,10 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                     for (uint32_t i = 0; i < len; i += 16) {
                         uint4 v[4];
 #pragma unroll
-                        for (int k = 0; k < 4; k++)
-                            if (i + 4 * k < len) v[k] = *(const uint4 *)(src + i + 4 * k);
+                        for (int k = 0; k < 4; k++) {
+                            const uint32_t q = i + 4 * k; /* (lenA is a multiple of 4: a block is in one piece) */
+                            if (q < len) v[k] = *(const uint4 *)(src + (int)(q < lenA ? q - dA : q - lenA));
+                        }
 #pragma unroll
                         for (int k = 0; k < 4; k++)
                             if (i + 4 * k < len)
@@ -174,7 +185,7 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                 }
                 wave_sync();
                 if (inb) {
-                    const uint32_t seg = 32u * (off - base) - 32u * w0; /* md bit -> staged bit */
+                    const uint32_t seg = 32u * (off - base + lenA) - 32u * w0; /* md bit -> staged bit */
                     uint32_t pos = start + seg;
                     int lsf_pre = 0;
                     if (r.lsf) {
@@ -190,7 +201,7 @@ __global__ void __launch_bounds__(HUFF_BLOCK) k_huffman(const uint8_t *__restric
                         if (need_g0) {
                             /* scfsi reuse: granule 0's scalefactors of this channel
                              * first, then granule 1's read over them in place */
-                            read_sf(bits, g0_start + seg, sq[ch], 0, sfw, s_slen);
+                            read_sf(bits, g0_start + seg - 32u * (lenA - dA), sq[ch], 0, sfw, s_slen); /* (its piece) */
                         }
                         pos = read_sf(bits, pos, side, scfsi, sfw, s_slen);
                         uint8_t *mrec = (uint8_t *)&meta[u];

@@ -33,6 +33,7 @@ namespace mp3d {
 #define HUFF_BLOCK (64 * HUFF_WAVES)
 #define HUFF_CAPW 2304 /* LDS words per wave (9.2 KB) of main-data staging; 16 waves + the tables in 160 KB */
 #define HUFF_STAGEW HUFF_CAPW /* staging words */
+#define HUFF_G0W 8u /* words staged at granule 0's scalefactors for scfsi reuse (<= 31 + 126 bits + the window margin) */
 
 /* wave-wide scan / min by ds_bpermute with the lane id re-derived at each
  * use (HIP's __shfl_up / __shfl_xor add width bounds whose lane-derived
