@@ -1285,6 +1285,17 @@ VARS["HSTAT3"] = [(a.replace("g_hstat[4]", "g_hstat[8]"), b.replace("g_hstat[4]"
 ]
 
 
+
+# NO2B (timing only; 4 % of C3's units not decoded): k_huffman's rounds decode
+# their first staging batch only -- what the second batches (1.26 per round
+# on C3 after the scfsi pieces) cost
+VARS["NO2B"] = [("""                pending = pending && !inb;
+            }
+            if (valid && !dec) {""", """                pending = false;
+            }
+            if (valid && !dec) {""")]
+
+
 if __name__ == "__main__":
     for n in (sys.argv[1:] or VARS):
         variant(n, VARS[n])
