@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Every stream of the full-size C3 and C5 batches (65 536 streams x 32
-frames each) against the oracle (oracle/liboracle.so, the double-precision
+frames each; and an LSF batch of the same size) against the oracle (oracle/liboracle.so, the double-precision
 checker, on a 16-thread pool): the largest |GPU - oracle| per stream in
 int16 LSB, as a histogram (tests/test_gpu_scale.py checks a stride-256
 sample of the same batches).  Prints one JSON line.
@@ -24,7 +24,8 @@ import _golden  # noqa: E402
 import _oracle  # noqa: E402
 import mp3_amd  # noqa: E402
 
-CFG = {"c3": (_gen.C3, 3_000_000), "c5": (_gen.C5, 5_000_000)}
+CFG = {"c3": (_gen.C3, 3_000_000), "c5": (_gen.C5, 5_000_000),
+       "lsf": (dict(_gen.C5, sr_idx=-2, short_pct=30, mixed_pct=40), 7_000_000)}  # MPEG-2 / 2.5 LSF, all six rates
 
 
 def run(name):
