@@ -467,7 +467,8 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
         vm = __builtin_amdgcn_raw_buffer_load_b32(r_meta, om, g * 2 * (int)sizeof(UnitMeta), 0);
         vr = __builtin_amdgcn_raw_buffer_load_b32(r_rec, orr, (g >> 1) * (int)sizeof(FrameRec), 0);
     };
-    /* The LDS-DMA as inline asm, one block per channel: M0 = the channel's
+    /* (The loads are nt: each is[] row is read once.)
+     * The LDS-DMA as inline asm, one block per channel: M0 = the channel's
      * LDS area (saved and restored), the five 256-B pieces at instruction
      * offsets 0 .. 1024 (the offset moves the memory AND the LDS address:
      * LDS = M0 + offset + 4 lane, probed on the box, tools/dbg/
@@ -499,11 +500,11 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                              "s_mov_b32 %0, m0\n\t"
                              "s_mov_b32 m0, %2\n\t"
                              "s_nop 0\n\t"
-                             "buffer_load_dword %1, %3, 0 offen lds\n\t"
-                             "buffer_load_dword %1, %3, 0 offen offset:256 lds\n\t"
-                             "buffer_load_dword %1, %3, 0 offen offset:512 lds\n\t"
-                             "buffer_load_dword %1, %3, 0 offen offset:768 lds\n\t"
-                             "buffer_load_dword %1, %3, 0 offen offset:1024 lds\n\t"
+                             "buffer_load_dword %1, %3, 0 offen nt lds\n\t"
+                             "buffer_load_dword %1, %3, 0 offen offset:256 nt lds\n\t"
+                             "buffer_load_dword %1, %3, 0 offen offset:512 nt lds\n\t"
+                             "buffer_load_dword %1, %3, 0 offen offset:768 nt lds\n\t"
+                             "buffer_load_dword %1, %3, 0 offen offset:1024 nt lds\n\t"
                              "s_mov_b32 m0, %0"
                              : "=&s"(keep)
                              : "v"(lo), "s"(lds0 + 1280u * c), "s"(rs)
@@ -586,15 +587,15 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                          "s_mov_b32 %0, m0\n\t"
                          "s_mov_b32 m0, %2\n\t"
                          "s_nop 0\n\t"
-                         "buffer_load_dword %1, %3, %4 offen lds\n\t"
-                         "buffer_load_dword %1, %3, %4 offen offset:256 lds\n\t"
-                         "buffer_load_dword %1, %3, %4 offen offset:512 lds\n\t"
-                         "buffer_load_dword %1, %3, %4 offen offset:768 lds\n\t"
-                         "buffer_load_dword %1, %3, %4 offen offset:1024 lds\n\t"
-                         "buffer_load_dword %1, %3, %4 offen offset:1280 lds\n\t"
-                         "buffer_load_dword %1, %3, %4 offen offset:1536 lds\n\t"
-                         "buffer_load_dword %1, %3, %4 offen offset:1792 lds\n\t"
-                         "buffer_load_dword %1, %3, %4 offen offset:2048 lds\n\t"
+                         "buffer_load_dword %1, %3, %4 offen nt lds\n\t"
+                         "buffer_load_dword %1, %3, %4 offen offset:256 nt lds\n\t"
+                         "buffer_load_dword %1, %3, %4 offen offset:512 nt lds\n\t"
+                         "buffer_load_dword %1, %3, %4 offen offset:768 nt lds\n\t"
+                         "buffer_load_dword %1, %3, %4 offen offset:1024 nt lds\n\t"
+                         "buffer_load_dword %1, %3, %4 offen offset:1280 nt lds\n\t"
+                         "buffer_load_dword %1, %3, %4 offen offset:1536 nt lds\n\t"
+                         "buffer_load_dword %1, %3, %4 offen offset:1792 nt lds\n\t"
+                         "buffer_load_dword %1, %3, %4 offen offset:2048 nt lds\n\t"
                          "s_mov_b32 m0, %0"
                          : "=&s"(keep)
                          : "v"(lo), "s"(lds0), "s"(rs), "s"(so)
@@ -606,7 +607,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
             __asm__ volatile("s_mov_b32 %0, m0\n\t"
                              "s_mov_b32 m0, %2\n\t"
                              "s_nop 0\n\t"
-                             "buffer_load_dword %1, %3, %4 offen lds\n\t"
+                             "buffer_load_dword %1, %3, %4 offen nt lds\n\t"
                              "s_mov_b32 m0, %0"
                              : "=&s"(keep1)
                              : "v"(lo), "s"(lds0 + 2304u), "s"(rs), "s"(so + 2304 + 2048)
@@ -1353,6 +1354,13 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                 /* output slots (2 tp, 2 tp + 1): lanes 0-31 hold L, lanes 32-63
                  * R; one half-wave swap leaves lane j with (L, R) of slot 2 tp
                  * and lane 32 + j with (L, R) of slot 2 tp + 1 */
+                /* The stereo stores are non-temporal (cache policy nt): each
+                 * instruction writes whole 128-B lines (256 / 512 B per wave)
+                 * that no kernel reads again, and streaming them past the L2
+                 * made the next step's demux -3 % and k_synth -0.5..1 % (C3,
+                 * C5, C2; profiles/r06_ab_bounds.txt box 24, with the nt is[]
+                 * loads above).  (k_huffman's is[] row stores must not be nt:
+                 * their lines fill over several stores) */
                 /* STEREO: a stereo frame past the warm-up (the common case):
                  * branch-free stores, so the window loop below is one basic
                  * block; otherwise the general sink (mono lanes, warm-up) */
@@ -1368,7 +1376,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                             const int vo = vo_st;
                             const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(o.x), __float_as_uint(o.y),
                                                                             false, false);
-                            __builtin_amdgcn_raw_buffer_store_b64((u32x2){r[0], r[1]}, r_pcm, vo + 512 * tp, so, 0);
+                            __builtin_amdgcn_raw_buffer_store_b64((u32x2){r[0], r[1]}, r_pcm, vo + 512 * tp, so, 2 /* nt */);
                         } else {
                             /* floor(x + 0.5) -> int32, then v_cvt_pk_i16_i32
                              * saturates to int16 and packs (L, R): 4 VALU per
@@ -1378,7 +1386,7 @@ __device__ __forceinline__ void synth_stream(const FrameRec *__restrict__ rec, c
                             const auto r = __builtin_amdgcn_permlane32_swap(p0, p1, false, false);
                             __builtin_amdgcn_raw_buffer_store_b32(
                                 __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16((int)r[0], (int)r[1])), r_pcm,
-                                vo + 256 * tp, so, 0);
+                                vo + 256 * tp, so, 2 /* nt */);
                         }
                     } else if (f < f0) {
                         /* warm-up frame: state only, no PCM */
